@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-2-medium pipeline-model-parallel training with gradient verification on.
+
+Metric (BASELINE.json): tokens/sec, GPT-2-medium, MP = number of GPUs (pp1/2/4/8), trust +
+gradient verification + output anomaly detection active in every step, bf16 compute with fp32
+master weights + fused AdamW, synthetic token data, random-init weights.
+
+    python bench.py                       # N=1 defaults
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \\
+        bench.py --gpus N --steps K --warmup W
+
+Weak scaling: the global batch is ``--batch-per-gpu`` (default 32 sequences of 1024 tokens, the
+README config's batch) times N, split into micro-batches of ``--mbs`` sequences; each stage does
+1/N of the layers for N times the tokens, so per-GPU work is fixed.  Timing: W untimed steps,
+then barrier + device sync, K timed optimizer steps, barrier + device sync; the MAX elapsed over
+ranks is reported.  ``value`` = whole-job tokens/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="gpt2-medium")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--batch-per-gpu", type=int, default=32)
+    ap.add_argument("--mbs", type=int, default=4, help="sequences per micro-batch")
+    ap.add_argument("--no-verify", action="store_true", help="disable detection/verification (ablation)")
+    ap.add_argument("--lr", type=float, default=5e-5)
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torch.distributed.run --nproc-per-node {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend="nccl" if use_cuda else "gloo",
+                                device_id=torch.device("cuda", local_rank) if use_cuda else None)
+
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.flat import AdamWConfig
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+
+    N = world
+    global_batch = args.batch_per_gpu * N
+    M = global_batch // args.mbs
+    model = get_model(args.model, seq_len=args.seq_len, seed=1234)
+    verify = not args.no_verify
+    cfg = EngineConfig(num_nodes=N, micro_batches=M, seq_len=args.seq_len,
+                       adamw=AdamWConfig(lr=args.lr, weight_decay=0.01, max_grad_norm=1.0),
+                       attack_detection=verify, gradient_verification=verify, quarantine=verify,
+                       reassign=False)
+    engine = PipelineEngine(model, cfg)
+    del model
+
+    g = torch.Generator().manual_seed(0)
+    V = 50257
+    batches = []
+    for _ in range(2):
+        ids = torch.randint(0, V, (global_batch, args.seq_len + 1), generator=g)
+        batches.append({"input": ids[:, :-1].contiguous().pin_memory() if use_cuda else ids[:, :-1].contiguous(),
+                        "target": ids[:, 1:].contiguous().pin_memory() if use_cuda else ids[:, 1:].contiguous()})
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        engine.train_step(batches[i % 2])
+    engine.flush()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        engine.train_step(batches[i % 2])
+    sync()
+    elapsed = time.perf_counter() - t0
+    engine.flush()
+    el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}" if use_cuda else "cpu")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el)
+    tokens = global_batch * args.seq_len * args.steps
+    tps = tokens / elapsed
+    if rank == 0:
+        line = {
+            "metric": "tokens/sec GPT-2-medium MP=N with grad-verify on",
+            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic tokens, random-init weights",
+            "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq_len,
+                       "micro_batch": args.mbs, "micro_batches": M, "parallelism": f"pp{N}",
+                       "grad_verify": verify, "output_detection": verify, "trust_update": True,
+                       "plan": engine.plan.describe(), "last_loss": engine.last_loss},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

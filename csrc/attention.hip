@@ -1,0 +1,365 @@
+// Causal flash attention for GPT-2 blocks, head dim 64, bf16 I/O, fp32 accumulate,
+// gfx950 MFMA v_mfma_f32_32x32x16_bf16.
+//
+// Reads q/k/v straight out of the packed c_attn output [B, T, 3, H, D] and writes o as [B, T, H, D]
+// (= the c_proj input), so no permute/contiguous copies exist around attention.
+//
+// Forward (per workgroup: 128 queries = 4 waves x 32; key blocks of 64 staged in LDS):
+//   S^T = K . Q^T  ("swapped": each lane owns ONE query and 16 keys of every 32-key tile, so the
+//   softmax row reductions are in-register + one cross-half shuffle).  The S^T accumulator is then
+//   used directly as the B operand of O^T = V^T . P^T (cdna_hip_programming.md §3 "accumulator tile as
+//   the next MFMA's operand"); V^T fragments come from a row-major LDS tile via ds_read_b64_tr_b16
+//   (T10) in the matching permuted key order.  O^T keeps query on the lane, so the online-softmax
+//   rescale is a per-lane scalar multiply.
+// Backward (per workgroup: 128 keys = 4 waves x 32; query tiles of 32 staged in LDS):
+//   S and dP are computed with the KEY on the lane; their accumulators feed dV^T += dO^T.P and
+//   dK^T += Q^T.dS without leaving registers; only dS crosses LDS (for dQ = dS.K), and dQ is
+//   pre-summed over the 4 waves in LDS before one fp32 atomic per element per workgroup.
+#include "common.h"
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+
+__device__ __forceinline__ short4_t tr_read(const bf16_t* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
+}
+// 8-element operand fragment from two transposed 4x16 LDS reads (rows r..r+3 and r+8..r+11).
+__device__ __forceinline__ bf16x8_t tr_pair(const bf16_t* p_lo, const bf16_t* p_hi) {
+    const short4_t a = tr_read(p_lo), b = tr_read(p_hi);
+    const short8_t c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, c);
+}
+__device__ __forceinline__ bf16x8_t cvt8(const f32x16& v, int base) {
+    bf16x8_t r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[base + j];
+    return r;
+}
+
+constexpr int HD = 64;
+
+// ============================================================================ forward
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                       float* __restrict__ lse, int T, int H, float scale_log2) {
+    constexpr int BM = 128, BN = 64;
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int ldq = 3 * H * HD;
+    const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
+    const bf16_t* kbase = qbase + H * HD;
+    const bf16_t* vbase = qbase + 2 * H * HD;
+    const int q0 = blockIdx.x * BM + 32 * w;
+    const int qi = q0 + r;
+    const int qrow = qi < T ? qi : T - 1;
+
+    bf16x8_t qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qbase + (size_t)qrow * ldq + 16 * s + 8 * h));
+
+    f32x16 o0 = {}, o1 = {};
+    float m = -1e30f, l = 0.f;
+    int nkb = T / BN;
+    if (CAUSAL) {
+        const int lim = (blockIdx.x * BM + BM + BN - 1) / BN;
+        nkb = lim < nkb ? lim : nkb;
+    }
+    // tr-read lane geometry (16-lane groups): lane 4q+p supplies row q, cols 4p..4p+3
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
+
+    for (int kb = 0; kb < nkb; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+            const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
+            const uint4 kv = *(const uint4*)(kbase + goff);
+            const uint4 vv = *(const uint4*)(vbase + goff);
+            *(uint4*)(Ks + row * HD + ((ch ^ (row & 7)) * 8)) = kv;
+            *(uint4*)(Vs + row * HD + ch * 8) = vv;
+        }
+        __syncthreads();
+        const bool active = !CAUSAL || (kb * BN <= q0 + 31);
+        if (active) {
+            f32x16 s0 = {}, s1 = {};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int r1 = 32 + r;
+                const bf16x8_t a0 = as_bf16x8(*(const uint4*)(Ks + r * HD + (((2 * s + h) ^ (r & 7)) * 8)));
+                const bf16x8_t a1 = as_bf16x8(*(const uint4*)(Ks + r1 * HD + (((2 * s + h) ^ (r1 & 7)) * 8)));
+                s0 = MFMA32(a0, qf[s], s0);
+                s1 = MFMA32(a1, qf[s], s1);
+            }
+            float mx = -1e30f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
+                float v0 = s0[i] * scale_log2, v1 = s1[i] * scale_log2;
+                if (CAUSAL) {
+                    if (key0 > qi) v0 = -INFINITY;
+                    if (key0 + 32 > qi) v1 = -INFINITY;
+                }
+                s0[i] = v0;
+                s1[i] = v1;
+                mx = fmaxf(mx, fmaxf(v0, v1));
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mn = fmaxf(m, mx);
+            const float alpha = exp2f(m - mn);
+            float rs = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0[i] = exp2f(s0[i] - mn);
+                s1[i] = exp2f(s1[i] - mn);
+                rs += s0[i] + s1[i];
+            }
+            rs += __shfl_xor(rs, 32, 64);
+            l = l * alpha + rs;
+            m = mn;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                o0[i] *= alpha;
+                o1[i] *= alpha;
+            }
+            const bf16x8_t p00 = cvt8(s0, 0), p01 = cvt8(s0, 8), p10 = cvt8(s1, 0), p11 = cvt8(s1, 8);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const bf16x8_t pf = t == 0 ? (s2 == 0 ? p00 : p01) : (s2 == 0 ? p10 : p11);
+                    const int kr = 32 * t + 16 * s2 + 4 * h + tq;
+                    const bf16x8_t v0 = tr_pair(Vs + kr * HD + tcol, Vs + (kr + 8) * HD + tcol);
+                    const bf16x8_t v1 = tr_pair(Vs + kr * HD + 32 + tcol, Vs + (kr + 8) * HD + 32 + tcol);
+                    o0 = MFMA32(v0, pf, o0);
+                    o1 = MFMA32(v1, pf, o1);
+                }
+        }
+        __syncthreads();
+    }
+    if (qi < T) {
+        const float inv_l = 1.f / l;
+        bf16_t* orow = out + ((size_t)b * T + qi) * (H * HD) + hd * HD;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int d = 8 * g + 4 * h;
+            float v[4] = {o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l, o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l};
+            *(uint2*)(orow + d) = pack4(v);
+            float u[4] = {o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l};
+            *(uint2*)(orow + 32 + d) = pack4(u);
+        }
+        if (h == 0) lse[(size_t)bh * T + qi] = (m + log2f(l)) * 0.6931471805599453f;
+    }
+}
+
+TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, int B, int T, int H, int D, float scale,
+                         int causal, hipStream_t s) {
+    (void)unused;
+    if (D != HD || T % 64 != 0) return (int)hipErrorInvalidValue;
+    const dim3 grid((T + 127) / 128, B * H);
+    const float sl2 = scale * 1.4426950408889634f;
+    if (causal) attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
+    else attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================================ backward
+// delta[bh, t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+                                                         float* __restrict__ delta, int B, int T, int H) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over B*T*H
+    if (idx >= B * T * H) return;
+    const int hd = idx % H, bt = idx / H, b = bt / T, t = bt - b * T;
+    const bf16_t* op = o + (size_t)bt * H * HD + hd * HD;
+    const bf16_t* dp = dout + (size_t)bt * H * HD + hd * HD;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < HD / 8; ++c) {
+        float a[8], g[8];
+        unpack8(((const uint4*)op)[c], a);
+        unpack8(((const uint4*)dp)[c], g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
+    }
+    delta[((size_t)b * H + hd) * T + t] = acc;
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+                                                       const float* __restrict__ lse, const float* __restrict__ delta,
+                                                       float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int T, int H,
+                                                       float scale) {
+    constexpr int BK = 128, BQ = 32;
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[BK * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t dSs[4][32 * 32];
+    __shared__ float dQr[BQ * HD];
+    __shared__ float lse_s[BQ], delta_s[BQ];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int ldq = 3 * H * HD, ldo = H * HD;
+    const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
+    const bf16_t* kbase = qbase + H * HD;
+    const bf16_t* vbase = qbase + 2 * H * HD;
+    const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
+    const int kblk = blockIdx.x * BK;
+    const int k0 = kblk + 32 * w;
+    const int kj = k0 + r;
+    const float* lse_row = lse + (size_t)bh * T;
+    const float* delta_row = delta + (size_t)bh * T;
+
+    bf16x8_t kf[4], vf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        kf[s] = as_bf16x8(*(const uint4*)(kbase + (size_t)kj * ldq + 16 * s + 8 * h));
+        vf[s] = as_bf16x8(*(const uint4*)(vbase + (size_t)kj * ldq + 16 * s + 8 * h));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+        *(uint4*)(Ks + row * HD + ch * 8) = *(const uint4*)(kbase + (size_t)(kblk + row) * ldq + ch * 8);
+    }
+    for (int e = tid; e < BQ * HD; e += 256) dQr[e] = 0.f;
+
+    f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
+    const int q_start = CAUSAL ? kblk : 0;
+
+    for (int qt = q_start; qt < T; qt += BQ) {
+        {
+            const int row = tid >> 3, ch = tid & 7;  // 256 chunks = 32 rows x 8
+            *(uint4*)(Qs + row * HD + ch * 8) = *(const uint4*)(qbase + (size_t)(qt + row) * ldq + ch * 8);
+            *(uint4*)(dOs + row * HD + ch * 8) = *(const uint4*)(dobase + (size_t)(qt + row) * ldo + ch * 8);
+            if (tid < BQ) {
+                lse_s[tid] = lse_row[qt + tid];
+                delta_s[tid] = delta_row[qt + tid];
+            }
+        }
+        __syncthreads();
+        const bool active = !CAUSAL || (qt + BQ - 1 >= k0);
+        if (active) {
+            f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qs + r * HD + 16 * s + 8 * h));
+                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOs + r * HD + 16 * s + 8 * h));
+                sacc = MFMA32(aq, kf[s], sacc);
+                dpacc = MFMA32(ad, vf[s], dpacc);
+            }
+            // lane = key kj; reg i = query qt + ql(i)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
+                float p = __expf(sacc[i] * scale - lse_s[ql]);
+                if (CAUSAL && kj > qt + ql) p = 0.f;
+                sacc[i] = p;
+                dpacc[i] = p * (dpacc[i] - delta_s[ql]);
+            }
+            const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
+            const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int qr = 16 * s2 + 4 * h + tq;
+                const bf16x8_t pb = s2 == 0 ? pb0 : pb1;
+                const bf16x8_t dsb = s2 == 0 ? db0 : db1;
+                const bf16x8_t ado0 = tr_pair(dOs + qr * HD + tcol, dOs + (qr + 8) * HD + tcol);
+                const bf16x8_t ado1 = tr_pair(dOs + qr * HD + 32 + tcol, dOs + (qr + 8) * HD + 32 + tcol);
+                dv0 = MFMA32(ado0, pb, dv0);
+                dv1 = MFMA32(ado1, pb, dv1);
+                const bf16x8_t aq0 = tr_pair(Qs + qr * HD + tcol, Qs + (qr + 8) * HD + tcol);
+                const bf16x8_t aq1 = tr_pair(Qs + qr * HD + 32 + tcol, Qs + (qr + 8) * HD + 32 + tcol);
+                dk0 = MFMA32(aq0, dsb, dk0);
+                dk1 = MFMA32(aq1, dsb, dk1);
+            }
+            bf16_t* dsw = dSs[w];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
+                dsw[ql * 32 + r] = f2bf(dpacc[i]);
+            }
+        }
+        __syncthreads();
+        if (active) {
+            f32x16 dq0 = {}, dq1 = {};
+            const bf16_t* dsw = dSs[w];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bf16x8_t a = as_bf16x8(*(const uint4*)(dsw + r * 32 + 16 * s + 8 * h));
+                const int kr = 32 * w + 16 * s + 8 * h + tq;
+                const bf16x8_t b0 = tr_pair(Ks + kr * HD + tcol, Ks + (kr + 4) * HD + tcol);
+                const bf16x8_t b1 = tr_pair(Ks + kr * HD + 32 + tcol, Ks + (kr + 4) * HD + 32 + tcol);
+                dq0 = MFMA32(a, b0, dq0);
+                dq1 = MFMA32(a, b1, dq1);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
+                atomicAdd(&dQr[ql * HD + r], dq0[i]);
+                atomicAdd(&dQr[ql * HD + 32 + r], dq1[i]);
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < BQ * HD; e += 256) {
+            const int ql = e >> 6, d = e & 63;
+            const float v = dQr[e];
+            if (v != 0.f) atomicAdd(dq_acc + (((size_t)b * T + qt + ql) * H + hd) * HD + d, v);
+            dQr[e] = 0.f;
+        }
+        // the staging writes of the next iteration are fenced by its __syncthreads before any read
+        __syncthreads();
+    }
+    // epilogue: lane = key kj; regs = d rows (i&3)+8(i>>2)+4h (+32 for tile 1)
+    bf16_t* dkrow = dqkv + ((size_t)b * T + kj) * ldq + H * HD + hd * HD;
+    bf16_t* dvrow = dkrow + H * HD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int d = 8 * g + 4 * h;
+        float a[4] = {dk0[4 * g] * scale, dk0[4 * g + 1] * scale, dk0[4 * g + 2] * scale, dk0[4 * g + 3] * scale};
+        *(uint2*)(dkrow + d) = pack4(a);
+        float a2[4] = {dk1[4 * g] * scale, dk1[4 * g + 1] * scale, dk1[4 * g + 2] * scale, dk1[4 * g + 3] * scale};
+        *(uint2*)(dkrow + 32 + d) = pack4(a2);
+        float v[4] = {dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]};
+        *(uint2*)(dvrow + d) = pack4(v);
+        float v2[4] = {dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]};
+        *(uint2*)(dvrow + 32 + d) = pack4(v2);
+    }
+}
+
+// dqkv[b,t,0,h,:] = bf16(dq_acc[b,t,h,:] * scale)
+__global__ __launch_bounds__(256) void attn_dq_finalize(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B,
+                                                        int T, int H, float scale) {
+    const size_t n4 = (size_t)B * T * H * HD / 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        const float4 v = ((const float4*)dq_acc)[i];
+        const size_t e = i * 4;
+        const size_t bt = e / (H * HD), rem = e - bt * (H * HD);
+        float f[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
+        *(uint2*)(dqkv + bt * (3 * H * HD) + rem) = pack4(f);
+    }
+}
+
+TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* dq_acc,
+                         float* delta, int B, int T, int H, int D, float scale, int causal, hipStream_t s) {
+    if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
+    hipMemsetAsync(dq_acc, 0, sizeof(float) * (size_t)B * T * H * HD, s);
+    attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
+    const dim3 grid(T / 128, B * H);
+    if (causal)
+        attn_bwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dq_acc,
+                                                   (bf16_t*)dqkv, T, H, scale);
+    else
+        attn_bwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dq_acc,
+                                                    (bf16_t*)dqkv, T, H, scale);
+    const size_t n4 = (size_t)B * T * H * HD / 4;
+    const int fg = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
+    attn_dq_finalize<<<fg, 256, 0, s>>>(dq_acc, (bf16_t*)dqkv, B, T, H, scale);
+    TDL_LAUNCH_CHECK();
+}

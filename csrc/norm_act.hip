@@ -1,0 +1,385 @@
+// LayerNorm, bias+GELU(tanh) and token/position embedding kernels (bf16 I/O, fp32 math).
+//
+// Replaces the torch LayerNorm / GELU / Embedding used by the GPT-2 blocks that the
+// reference partitions (distributed_trainer.py:124-135).
+// Parameter gradients are accumulated straight into fp32 "main_grad" buffers with one
+// float atomic per column per workgroup (row-summed on chip first), so the per-micro-batch
+// bf16 weight-grad tensor and its separate accumulate kernel never exist.
+#include "common.h"
+
+// ============================================================== LayerNorm forward
+// One wave per row; every lane owns CH chunks of VEC contiguous columns
+// (N == 64 * VEC * CH), so the whole row lives in registers: two-pass mean/var, exact.
+template <int VEC, int CH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                     const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int M, float eps) {
+    constexpr int N = 64 * VEC * CH;
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const bf16_t* xr = x + (size_t)row * N;
+    float v[CH][VEC];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * VEC;
+        if constexpr (VEC == 8) unpack8(*(const uint4*)(xr + col), v[c]);
+        else unpack4(*(const uint2*)(xr + col), v[c]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) s += v[c][i];
+    const float mean = wave_sum(s) * (1.0f / N);
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const float d = v[c][i] - mean;
+            q += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(q) * (1.0f / N) + eps);
+    bf16_t* yr = y + (size_t)row * N;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * VEC;
+        float wf[VEC], bf[VEC], o[VEC];
+        if constexpr (VEC == 8) {
+            unpack8(*(const uint4*)(w + col), wf);
+            unpack8(*(const uint4*)(b + col), bf);
+        } else {
+            unpack4(*(const uint2*)(w + col), wf);
+            unpack4(*(const uint2*)(b + col), bf);
+        }
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] = (v[c][i] - mean) * rstd * wf[i] + bf[i];
+        if constexpr (VEC == 8) *(uint4*)(yr + col) = pack8(o);
+        else *(uint2*)(yr + col) = pack4(o);
+    }
+    if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+}
+
+// Generic fallback: one 256-thread block per row, two passes over global memory.
+__global__ __launch_bounds__(256) void ln_fwd_generic(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const bf16_t* __restrict__ b, bf16_t* __restrict__ y,
+                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                      int M, int N, float eps) {
+    __shared__ float red[16];
+    const int row = blockIdx.x;
+    const bf16_t* xr = x + (size_t)row * N;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) s += bf2f(xr[i]);
+    const float mean = block_sum(s, red) / N;
+    float q = 0.f;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const float d = bf2f(xr[i]) - mean;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(block_sum(q, red) / N + eps);
+    for (int i = threadIdx.x; i < N; i += blockDim.x)
+        y[(size_t)row * N + i] = f2bf((bf2f(xr[i]) - mean) * rstd * bf2f(w[i]) + bf2f(b[i]));
+    if (threadIdx.x == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+}
+
+TDL_API int tdl_layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                              int M, int N, float eps, hipStream_t s) {
+    const dim3 blk(256), grd((M + 3) / 4);
+    auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto B = (const bf16_t*)b; auto Y = (bf16_t*)y;
+    switch (N) {
+        case 256:  ln_fwd_kernel<4, 1><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 512:  ln_fwd_kernel<8, 1><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 768:  ln_fwd_kernel<4, 3><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 1024: ln_fwd_kernel<8, 2><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 1280: ln_fwd_kernel<4, 5><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 1536: ln_fwd_kernel<8, 3><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        case 2048: ln_fwd_kernel<8, 4><<<grd, blk, 0, s>>>(X, W, B, Y, mean, rstd, M, eps); break;
+        default: ln_fwd_generic<<<M, 256, 0, s>>>(X, W, B, Y, mean, rstd, M, N, eps); break;
+    }
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== LayerNorm backward
+// 4 waves per block, each wave walks RPW rows; dgamma/dbeta are summed per lane over the
+// wave's rows, then across the 4 waves through LDS, then one fp32 atomic per column.
+template <int VEC, int CH, int RPW>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+                                                     float* __restrict__ dw_acc, float* __restrict__ db_acc, int M) {
+    constexpr int N = 64 * VEC * CH;
+    __shared__ float red[2][4][N];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float dw[CH][VEC], db[CH][VEC], wf[CH][VEC];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * VEC;
+        if constexpr (VEC == 8) unpack8(*(const uint4*)(w + col), wf[c]);
+        else unpack4(*(const uint2*)(w + col), wf[c]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) dw[c][i] = db[c][i] = 0.f;
+    }
+    const int row0 = (blockIdx.x * 4 + wid) * RPW;
+    for (int r = 0; r < RPW; ++r) {
+        const int row = row0 + r;
+        if (row >= M) break;
+        const float mu = mean_in[row], rs = rstd_in[row];
+        float xv[CH][VEC], gv[CH][VEC];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int col = (c * 64 + lane) * VEC;
+            if constexpr (VEC == 8) {
+                unpack8(*(const uint4*)(x + (size_t)row * N + col), xv[c]);
+                unpack8(*(const uint4*)(dy + (size_t)row * N + col), gv[c]);
+            } else {
+                unpack4(*(const uint2*)(x + (size_t)row * N + col), xv[c]);
+                unpack4(*(const uint2*)(dy + (size_t)row * N + col), gv[c]);
+            }
+        }
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+                const float xh = (xv[c][i] - mu) * rs;
+                xv[c][i] = xh;
+                dw[c][i] += gv[c][i] * xh;
+                db[c][i] += gv[c][i];
+                const float g = gv[c][i] * wf[c][i];
+                gv[c][i] = g;
+                s1 += g;
+                s2 += g * xh;
+            }
+        s1 = wave_sum(s1) * (1.0f / N);
+        s2 = wave_sum(s2) * (1.0f / N);
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int col = (c * 64 + lane) * VEC;
+            float o[VEC];
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) o[i] = rs * (gv[c][i] - s1 - xv[c][i] * s2);
+            if constexpr (VEC == 8) *(uint4*)(dx + (size_t)row * N + col) = pack8(o);
+            else *(uint2*)(dx + (size_t)row * N + col) = pack4(o);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const int col = (c * 64 + lane) * VEC + i;
+            red[0][wid][col] = dw[c][i];
+            red[1][wid][col] = db[c][i];
+        }
+    __syncthreads();
+    for (int col = threadIdx.x; col < N; col += 256) {
+        const float a = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
+        const float bb = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
+        atomicAdd(dw_acc + col, a);
+        atomicAdd(db_acc + col, bb);
+    }
+}
+
+__global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
+                                                      float* __restrict__ dw_acc, float* __restrict__ db_acc, int M, int N) {
+    __shared__ float red[16];
+    const int row = blockIdx.x;
+    const float mu = mean_in[row], rs = rstd_in[row];
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = threadIdx.x; i < N; i += 256) {
+        const float xh = (bf2f(x[(size_t)row * N + i]) - mu) * rs;
+        const float g = bf2f(dy[(size_t)row * N + i]) * bf2f(w[i]);
+        s1 += g;
+        s2 += g * xh;
+    }
+    s1 = block_sum(s1, red) / N;
+    s2 = block_sum(s2, red) / N;
+    for (int i = threadIdx.x; i < N; i += 256) {
+        const float xh = (bf2f(x[(size_t)row * N + i]) - mu) * rs;
+        const float gy = bf2f(dy[(size_t)row * N + i]);
+        dx[(size_t)row * N + i] = f2bf(rs * (gy * bf2f(w[i]) - s1 - xh * s2));
+        atomicAdd(dw_acc + i, gy * xh);
+        atomicAdd(db_acc + i, gy);
+    }
+}
+
+TDL_API int tdl_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                              void* dx, float* dw_acc, float* db_acc, int M, int N, int unused, hipStream_t s) {
+    (void)unused;
+    auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto DX = (bf16_t*)dx;
+    constexpr int RPW = 2;
+    const dim3 blk(256), grd((M + 4 * RPW - 1) / (4 * RPW));
+    switch (N) {
+        case 256:  ln_bwd_kernel<4, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 512:  ln_bwd_kernel<8, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 768:  ln_bwd_kernel<4, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 1024: ln_bwd_kernel<8, 2, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 1280: ln_bwd_kernel<4, 5, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 1536: ln_bwd_kernel<8, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        case 2048: ln_bwd_kernel<8, 4, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
+        default: ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M, N); break;
+    }
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== bias + GELU(tanh)
+__device__ __forceinline__ float gelu_tanh(float u) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    const float a = k0 * (u + k1 * u * u * u);
+    const float t = 1.0f - 2.0f / (__expf(2.0f * a) + 1.0f);
+    return 0.5f * u * (1.0f + t);
+}
+__device__ __forceinline__ float gelu_tanh_grad(float u) {
+    const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+    const float a = k0 * (u + k1 * u * u * u);
+    const float t = 1.0f - 2.0f / (__expf(2.0f * a) + 1.0f);
+    return 0.5f * (1.0f + t) + 0.5f * u * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * u * u);
+}
+
+// y = gelu(x + b); x,y [M,N] bf16 (may alias), N % 8 == 0.
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ b,
+                                                            bf16_t* __restrict__ y, int M, int N) {
+    const size_t nvec = (size_t)M * N / 8;
+    const int nv_row = N / 8;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+        const int cv = (int)(i % nv_row);
+        float v[8], bb[8];
+        unpack8(((const uint4*)x)[i], v);
+        unpack8(((const uint4*)b)[cv], bb);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = gelu_tanh(v[k] + bb[k]);
+        ((uint4*)y)[i] = pack8(v);
+    }
+}
+
+TDL_API int tdl_bias_gelu_fwd(const void* x, const void* b, void* y, int M, int N, hipStream_t s) {
+    const size_t nvec = (size_t)M * N / 8;
+    const int grid = (int)((nvec + 255) / 256 < 4096 ? (nvec + 255) / 256 : 4096);
+    bias_gelu_fwd_kernel<<<grid, 256, 0, s>>>((const bf16_t*)x, (const bf16_t*)b, (bf16_t*)y, M, N);
+    TDL_LAUNCH_CHECK();
+}
+
+// dx = dy * gelu'(x + b); db += colsum(dx).  b may be null (x already holds the biased pre-activation).  Block tile: R rows x 2048 columns (256 thr x 8).
+template <int R>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ b, bf16_t* __restrict__ dx,
+                                                            float* __restrict__ db_acc, int M, int N) {
+    const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+    if (col >= N) return;
+    const int row0 = blockIdx.y * R;
+    float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, acc[8];
+    if (b) unpack8(*(const uint4*)(b + col), bb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        if (row >= M) break;
+        const size_t off = (size_t)row * N + col;
+        float g[8], v[8];
+        unpack8(*(const uint4*)(dy + off), g);
+        unpack8(*(const uint4*)(x + off), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float d = g[k] * gelu_tanh_grad(v[k] + bb[k]);
+            v[k] = d;
+            acc[k] += d;
+        }
+        *(uint4*)(dx + off) = pack8(v);
+    }
+    if (db_acc) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(db_acc + col + k, acc[k]);
+    }
+}
+
+TDL_API int tdl_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, float* db_acc, int M, int N,
+                              int unused, hipStream_t s) {
+    (void)unused;
+    constexpr int R = 16;
+    const dim3 grd((N / 8 + 255) / 256, (M + R - 1) / R);
+    bias_gelu_bwd_kernel<R><<<grd, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)b, (bf16_t*)dx,
+                                                db_acc, M, N);
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== embeddings
+// out[b,t,:] = wte[ids[b,t],:] + wpe[t,:]   (one wave per token, H % 512 == 0 or H % 256 == 0)
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ wte,
+                                                        const bf16_t* __restrict__ wpe, bf16_t* __restrict__ out,
+                                                        int B, int T, int H) {
+    const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tok >= B * T) return;
+    const int lane = threadIdx.x & 63, t = tok % T;
+    const int64_t id = ids[tok];
+    for (int col = lane * 4; col < H; col += 256) {
+        float a[4], p[4];
+        unpack4(*(const uint2*)(wte + id * H + col), a);
+        unpack4(*(const uint2*)(wpe + (size_t)t * H + col), p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += p[k];
+        *(uint2*)(out + (size_t)tok * H + col) = pack4(a);
+    }
+}
+
+TDL_API int tdl_embedding_fwd(const int64_t* ids, const void* wte, const void* wpe, void* out, int B, int T, int H,
+                              int unused, hipStream_t s) {
+    (void)unused;
+    embed_fwd_kernel<<<(B * T + 3) / 4, 256, 0, s>>>(ids, (const bf16_t*)wte, (const bf16_t*)wpe, (bf16_t*)out, B, T, H);
+    TDL_LAUNCH_CHECK();
+}
+
+// wte_grad[ids[b,t],:] += dout[b,t,:] (fp32 atomics; repeated ids collide correctly)
+__global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ dout,
+                                                            float* __restrict__ wte_grad, int BT, int H) {
+    const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tok >= BT) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t id = ids[tok];
+    for (int col = lane * 4; col < H; col += 256) {
+        float g[4];
+        unpack4(*(const uint2*)(dout + (size_t)tok * H + col), g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) atomicAdd(wte_grad + id * H + col + k, g[k]);
+    }
+}
+// wpe_grad[t,:] += sum_b dout[b,t,:]  (single writer per element, no atomics)
+__global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const bf16_t* __restrict__ dout, float* __restrict__ wpe_grad,
+                                                            int B, int T, int H) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= (size_t)T * H) return;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += bf2f(dout[(size_t)b * T * H + i]);
+    wpe_grad[i] += acc;
+}
+
+TDL_API int tdl_embedding_bwd(const int64_t* ids, const void* dout, float* wte_grad, float* wpe_grad, int B, int T, int H,
+                              int unused, hipStream_t s) {
+    (void)unused;
+    if (wte_grad)
+        embed_bwd_wte_kernel<<<(B * T + 3) / 4, 256, 0, s>>>(ids, (const bf16_t*)dout, wte_grad, B * T, H);
+    if (wpe_grad)
+        embed_bwd_wpe_kernel<<<(int)(((size_t)T * H + 255) / 256), 256, 0, s>>>((const bf16_t*)dout, wpe_grad, B, T, H);
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== dst_f32 += src (bf16 or f32)
+__global__ __launch_bounds__(256) void add_into_f32_kernel(float* __restrict__ dst, const void* __restrict__ src,
+                                                           int64_t n, int src_bf16) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] += src_bf16 ? bf2f(((const bf16_t*)src)[i]) : ((const float*)src)[i];
+}
+
+TDL_API int tdl_add_into_f32(float* dst, const void* src, int64_t n, int src_bf16, hipStream_t s) {
+    const int64_t blocks = (n + 255) / 256;
+    add_into_f32_kernel<<<(int)(blocks < 8192 ? blocks : 8192), 256, 0, s>>>(dst, src, n, src_bf16);
+    TDL_LAUNCH_CHECK();
+}

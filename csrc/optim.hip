@@ -1,0 +1,78 @@
+// Fused AdamW over a stage's FLAT parameter space (replaces the
+// never-populated per-node optimizers of distributed_trainer.py:441-446).
+//
+// Every stage keeps its parameters in four contiguous fp32 buffers (master, exp_avg,
+// exp_avg_sq, main_grad) and the model-visible bf16 weights in one contiguous buffer, so
+// the whole optimizer step is ONE bandwidth-bound launch (float4 / 16-byte lanes) that also
+// zeroes the gradient.  `ctrl` is a 2-float device control block written by the
+// verification path: ctrl[0] = gradient scale (clipping), ctrl[1] != 0 => the stage's
+// gradient was flagged by the verifier: the update is skipped (quarantined) on device, with
+// no host round trip, and the gradient is still cleared.
+#include "common.h"
+
+__global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ master, float* __restrict__ m,
+                                                         float* __restrict__ v, float* __restrict__ grad,
+                                                         bf16_t* __restrict__ out, int64_t n, float lr, float b1,
+                                                         float b2, float eps, float wd, float bc1, float bc2,
+                                                         const float* __restrict__ ctrl, int zero_grad) {
+    const float gscale = ctrl ? ctrl[0] : 1.0f;
+    const bool skip = ctrl ? (ctrl[1] != 0.0f) : false;
+    const float step_size = lr / bc1;
+    const float inv_sqrt_bc2 = rsqrtf(bc2);
+    const int64_t n4 = n / 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 g = ((float4*)grad)[i];
+        if (!skip) {
+            float4 p = ((float4*)master)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+            float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w};
+            float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float gg = ga[k] * gscale;
+                ma[k] = b1 * ma[k] + (1.f - b1) * gg;
+                va[k] = b2 * va[k] + (1.f - b2) * gg * gg;
+                pa[k] = pa[k] * (1.f - lr * wd);
+                pa[k] -= step_size * ma[k] / (sqrtf(va[k]) * inv_sqrt_bc2 + eps);
+            }
+            ((float4*)master)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+            ((float4*)m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+            ((float4*)v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+            ((uint2*)out)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+        }
+        if (zero_grad) ((float4*)grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // tail (n % 4)
+    for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!skip) {
+            const float gg = grad[i] * gscale;
+            m[i] = b1 * m[i] + (1.f - b1) * gg;
+            v[i] = b2 * v[i] + (1.f - b2) * gg * gg;
+            float p = master[i] * (1.f - lr * wd);
+            p -= step_size * m[i] / (sqrtf(v[i]) * inv_sqrt_bc2 + eps);
+            master[i] = p;
+            out[i] = f2bf(p);
+        }
+        if (zero_grad) grad[i] = 0.f;
+    }
+}
+
+TDL_API int tdl_adamw_flat(float* master, float* m, float* v, float* grad, void* out_bf16, int64_t n, float lr, float b1,
+                           float b2, float eps, float wd, float bc1, float bc2, const float* ctrl, int zero_grad,
+                           hipStream_t s) {
+    const int64_t work = (n / 4 + 255) / 256;
+    const int grid = (int)(work < 2048 ? (work > 0 ? work : 1) : 2048);
+    adamw_flat_kernel<<<grid, 256, 0, s>>>(master, m, v, grad, (bf16_t*)out_bf16, n, lr, b1, b2, eps, wd, bc1, bc2, ctrl,
+                                           zero_grad);
+    TDL_LAUNCH_CHECK();
+}
+
+__global__ void fill_f32_kernel(float* __restrict__ p, int64_t n, float val) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = val;
+}
+
+TDL_API int tdl_fill_f32(float* p, int64_t n, float val, hipStream_t s) {
+    const int64_t work = (n + 255) / 256;
+    fill_f32_kernel<<<(int)(work < 4096 ? (work > 0 ? work : 1) : 4096), 256, 0, s>>>(p, n, val);
+    TDL_LAUNCH_CHECK();
+}

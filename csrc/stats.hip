@@ -1,0 +1,516 @@
+// Verification-path reduction kernels:
+//   K1 tensor_stats      one-pass moments (Chan/Pebay merge to the 4th moment) + min/max/L1/L2/Linf
+//   K2 histogram quantile approximate median / p25 / p75 from a 2048-bin histogram over [min,max]
+//   K3 grad_stats        segmented (per-parameter) norm / dot-with-EMA-reference / ref-norm over a
+//                        stage's FLAT fp32 gradient, EMA reference updated in the same pass
+//   K4 zscore_detect     device ring-buffer baseline + z-score decision (attack_detector.py:292-342)
+//   K5 trust_update      fused EMA/decay/FSM trust update over all nodes (trust_manager.py:92-181)
+// They replace the reference's host path: `.cpu().numpy()` of whole activations plus
+// numpy/scipy statistics (attack_detector.py:78,185-223) and per-tensor `.item()` syncs
+// (distributed_trainer.py:242-256).  Everything stays on device; the caller reads back a
+// few dozen floats asynchronously.
+#include "common.h"
+
+#define NSTAT 12
+#define NHIST 2048
+#define MAXPART 1024
+
+struct Moments {  // central-moment partial, fp64
+    double n, mean, m2, m3, m4, mn, mx, abssum;
+};
+
+__device__ __forceinline__ void merge(Moments& a, const Moments& b) {
+    if (b.n == 0.0) return;
+    if (a.n == 0.0) { a = b; return; }
+    const double na = a.n, nb = b.n, n = na + nb;
+    const double delta = b.mean - a.mean, dn = delta / n, dn2 = dn * dn;
+    const double t1 = delta * dn * na * nb;
+    const double m4 = a.m4 + b.m4 + t1 * dn2 * (na * na - na * nb + nb * nb) + 6.0 * dn2 * (na * na * b.m2 + nb * nb * a.m2) +
+                      4.0 * dn * (na * b.m3 - nb * a.m3);
+    const double m3 = a.m3 + b.m3 + t1 * dn * (na - nb) + 3.0 * dn * (na * b.m2 - nb * a.m2);
+    a.m2 = a.m2 + b.m2 + t1;
+    a.m3 = m3;
+    a.m4 = m4;
+    a.mean = a.mean + nb * dn;
+    a.n = n;
+    a.mn = fmin(a.mn, b.mn);
+    a.mx = fmax(a.mx, b.mx);
+    a.abssum += b.abssum;
+}
+
+__device__ __forceinline__ Moments shfl_xor_m(const Moments& m, int o) {
+    Moments r;
+    r.n = __shfl_xor(m.n, o, 64); r.mean = __shfl_xor(m.mean, o, 64);
+    r.m2 = __shfl_xor(m.m2, o, 64); r.m3 = __shfl_xor(m.m3, o, 64); r.m4 = __shfl_xor(m.m4, o, 64);
+    r.mn = __shfl_xor(m.mn, o, 64); r.mx = __shfl_xor(m.mx, o, 64); r.abssum = __shfl_xor(m.abssum, o, 64);
+    return r;
+}
+
+// Thread-local accumulator: shifted power sums in fp32 (shift = first value seen).
+struct ThreadAcc {
+    float c, s1, s2, s3, s4, mn, mx, abssum;
+    int n;
+    __device__ void init() { c = 0.f; s1 = s2 = s3 = s4 = 0.f; mn = INFINITY; mx = -INFINITY; abssum = 0.f; n = 0; }
+    __device__ __forceinline__ void add(float x) {
+        if (n == 0) c = x;
+        const float d = x - c, d2 = d * d;
+        s1 += d; s2 += d2; s3 += d2 * d; s4 += d2 * d2;
+        mn = fminf(mn, x); mx = fmaxf(mx, x); abssum += fabsf(x);
+        ++n;
+    }
+    __device__ Moments to_moments() const {
+        Moments m;
+        m.n = n; m.mn = mn; m.mx = mx; m.abssum = abssum;
+        if (n == 0) { m.mean = m.m2 = m.m3 = m.m4 = 0.0; return m; }
+        const double N = n, S1 = s1, S2 = s2, S3 = s3, S4 = s4, mu = S1 / N;
+        m.mean = (double)c + mu;
+        m.m2 = S2 - S1 * mu;
+        m.m3 = S3 - 3.0 * mu * S2 + 2.0 * S1 * mu * mu;
+        m.m4 = S4 - 4.0 * mu * S3 + 6.0 * mu * mu * S2 - 3.0 * S1 * mu * mu * mu;
+        if (m.m2 < 0.0) m.m2 = 0.0;
+        return m;
+    }
+};
+
+// Block merge of per-thread moments -> thread 0 holds the block result. `sh` >= 16 Moments.
+__device__ Moments block_merge(Moments m, Moments* sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Moments other = shfl_xor_m(m, o);
+        // fixed merge order keeps the reduction deterministic
+        if ((threadIdx.x & o) == 0) merge(m, other); else { merge(other, m); m = other; }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wid] = m;
+    __syncthreads();
+    Moments r = sh[0];
+    for (int w = 1; w < nw; ++w) merge(r, sh[w]);
+    return r;
+}
+
+__device__ __forceinline__ float load_elem(const void* x, int dtype, int64_t i) {
+    return dtype == 1 ? bf2f(((const bf16_t*)x)[i]) : ((const float*)x)[i];
+}
+
+// ------------------------------------------------------------------ K1 pass 1 (flat tensor)
+__global__ __launch_bounds__(256) void moments_partial_kernel(const void* __restrict__ x, int dtype, int64_t n,
+                                                              Moments* __restrict__ part, float* __restrict__ nonfinite) {
+    __shared__ Moments sh[16];
+    ThreadAcc acc;
+    acc.init();
+    int bad = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (dtype == 1) {
+        const int64_t nv = n / 8;
+        for (int64_t i = tid; i < nv; i += stride) {
+            float v[8];
+            unpack8(((const uint4*)x)[i], v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (isfinite(v[k])) acc.add(v[k]); else ++bad;
+            }
+        }
+        for (int64_t i = nv * 8 + tid; i < n; i += stride) {
+            const float v = bf2f(((const bf16_t*)x)[i]);
+            if (isfinite(v)) acc.add(v); else ++bad;
+        }
+    } else {
+        const int64_t nv = n / 4;
+        for (int64_t i = tid; i < nv; i += stride) {
+            const float4 f = ((const float4*)x)[i];
+            const float v[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (isfinite(v[k])) acc.add(v[k]); else ++bad;
+            }
+        }
+        for (int64_t i = nv * 4 + tid; i < n; i += stride) {
+            const float v = ((const float*)x)[i];
+            if (isfinite(v)) acc.add(v); else ++bad;
+        }
+    }
+    Moments r = block_merge(acc.to_moments(), sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+    if (bad) atomicAdd(nonfinite, (float)bad);
+}
+
+// Finalize moments (1 block): merge `np` partials in order, write the stat vector slots that
+// do not need quantiles, store [min,max] range for the histogram pass, zero the histogram.
+__device__ void write_moment_stats(const Moments& r, float* out, float* range) {
+    const double n = r.n > 0 ? r.n : 1.0;
+    const double var = r.m2 / n;
+    const double sd = sqrt(var);
+    out[0] = (float)r.mean;
+    out[1] = (float)sd;
+    out[2] = (float)r.mn;
+    out[3] = (float)r.mx;
+    out[5] = var > 0 ? (float)((r.m3 / n) / (var * sd)) : 0.f;
+    out[6] = var > 0 ? (float)((r.m4 / n) / (var * var) - 3.0) : -3.f;
+    out[9] = (float)r.abssum;
+    out[10] = (float)sqrt(r.m2 + r.n * r.mean * r.mean);
+    out[11] = (float)fmax(fabs(r.mn), fabs(r.mx));
+    range[0] = (float)r.mn;
+    range[1] = (float)r.mx;
+}
+
+__global__ __launch_bounds__(256) void moments_final_kernel(const Moments* __restrict__ part, int np, float* __restrict__ out,
+                                                            float* __restrict__ range, unsigned* __restrict__ hist) {
+    __shared__ Moments sh[16];
+    Moments m;
+    m.n = 0.0; m.mean = m.m2 = m.m3 = m.m4 = 0.0; m.mn = INFINITY; m.mx = -INFINITY; m.abssum = 0.0;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) merge(m, part[i]);
+    Moments r = block_merge(m, sh);
+    if (threadIdx.x == 0) write_moment_stats(r, out, range);
+    for (int i = threadIdx.x; i < NHIST; i += blockDim.x) hist[i] = 0u;
+}
+
+// ------------------------------------------------------------------ K2 histogram + quantiles
+__global__ __launch_bounds__(256) void hist_kernel(const void* __restrict__ x, int dtype, int64_t n,
+                                                   const float* __restrict__ range, unsigned* __restrict__ hist) {
+    __shared__ unsigned h[NHIST];
+    for (int i = threadIdx.x; i < NHIST; i += blockDim.x) h[i] = 0u;
+    __syncthreads();
+    const float lo = range[0], hi = range[1];
+    const float scale = hi > lo ? NHIST / (hi - lo) : 0.f;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float v = load_elem(x, dtype, i);
+        if (!isfinite(v)) continue;
+        int b = (int)((v - lo) * scale);
+        b = b < 0 ? 0 : (b >= NHIST ? NHIST - 1 : b);
+        atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NHIST; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+__device__ float hist_quantile(const unsigned* hist, double total, double q, float lo, float hi) {
+    if (total <= 0) return 0.f;
+    if (!(hi > lo)) return lo;
+    const double k = q * (total - 1.0);
+    double cum = 0.0;
+    const double w = (double)(hi - lo) / NHIST;
+    for (int b = 0; b < NHIST; ++b) {
+        const double c = hist[b];
+        if (c > 0 && k < cum + c) {
+            const double frac = (k - cum + 0.5) / c;
+            return (float)(lo + (b + frac) * w);
+        }
+        cum += c;
+    }
+    return hi;
+}
+
+__global__ void quantile_kernel(const unsigned* __restrict__ hist, const float* __restrict__ range, float* __restrict__ out) {
+    if (threadIdx.x >= 3) return;
+    double total = 0.0;
+    for (int b = 0; b < NHIST; ++b) total += hist[b];
+    const double qs[3] = {0.5, 0.25, 0.75};
+    const int slot[3] = {4, 7, 8};
+    out[slot[threadIdx.x]] = hist_quantile(hist, total, qs[threadIdx.x], range[0], range[1]);
+}
+
+// Workspace layout (bytes): [Moments x MAXPART][range 2 f32 | nonfinite f32 | pad][hist NHIST u32]
+TDL_API int64_t tdl_stats_workspace_bytes() {
+    return (int64_t)sizeof(Moments) * MAXPART + 16 + 4 * NHIST;
+}
+
+static inline int stat_grid(int64_t n) {
+    int64_t g = (n + 256 * 16 - 1) / (256 * 16);
+    if (g < 1) g = 1;
+    if (g > MAXPART) g = MAXPART;
+    if (g > 512) g = 512;
+    return (int)g;
+}
+
+// out[12] = TENSOR_STATS order; out[12] (if out_extra) = non-finite element count.
+TDL_API int tdl_tensor_stats(const void* x, int dtype, int64_t n, float* out, void* ws, int with_quantiles, hipStream_t s) {
+    Moments* part = (Moments*)ws;
+    float* range = (float*)((char*)ws + sizeof(Moments) * MAXPART);
+    float* nonfinite = range + 2;
+    unsigned* hist = (unsigned*)(range + 4);
+    const int g = stat_grid(n);
+    hipMemsetAsync(nonfinite, 0, sizeof(float), s);
+    moments_partial_kernel<<<g, 256, 0, s>>>(x, dtype, n, part, nonfinite);
+    moments_final_kernel<<<1, 256, 0, s>>>(part, g, out, range, hist);
+    if (with_quantiles) {
+        hist_kernel<<<g, 256, 0, s>>>(x, dtype, n, range, hist);
+        quantile_kernel<<<1, 64, 0, s>>>(hist, range, out);
+    }
+    hipMemcpyAsync(out + NSTAT, nonfinite, sizeof(float), hipMemcpyDeviceToDevice, s);
+    TDL_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ K3 segmented gradient stats
+// chunks: int64 [C][3] = (segment, start, end) with end - start <= CHUNK; ordered by segment.
+// seg_first: int32 [S + 1] first chunk of every segment.
+// part_seg: double [C][3] = (sum g^2, sum g*ref, sum ref^2) per chunk.
+// ref (nullable) is updated in place: ref <- beta*ref + (1-beta)*g  (ref_valid==0: ref <- g).
+__global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restrict__ g, float* __restrict__ ref,
+                                                           const int64_t* __restrict__ chunks, int ref_valid, float beta,
+                                                           Moments* __restrict__ part, double* __restrict__ part_seg,
+                                                           float* __restrict__ nonfinite) {
+    __shared__ Moments sh[16];
+    __shared__ float red[16];
+    const int c = blockIdx.x;
+    const int64_t start = chunks[3 * c + 1], end = chunks[3 * c + 2];
+    ThreadAcc acc;
+    acc.init();
+    float sq = 0.f, dot = 0.f, rsq = 0.f;
+    int bad = 0;
+    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+        const float v = g[i];
+        if (isfinite(v)) { acc.add(v); sq += v * v; } else ++bad;
+        if (ref) {
+            const float r = ref[i];
+            if (ref_valid) {
+                dot += v * r;
+                rsq += r * r;
+                ref[i] = beta * r + (1.f - beta) * (isfinite(v) ? v : 0.f);
+            } else {
+                ref[i] = isfinite(v) ? v : 0.f;
+            }
+        }
+    }
+    Moments r = block_merge(acc.to_moments(), sh);
+    sq = block_sum(sq, red);
+    dot = block_sum(dot, red);
+    rsq = block_sum(rsq, red);
+    if (threadIdx.x == 0) {
+        part[c] = r;
+        part_seg[3 * c] = sq;
+        part_seg[3 * c + 1] = dot;
+        part_seg[3 * c + 2] = rsq;
+    }
+    if (bad) atomicAdd(nonfinite, (float)bad);
+}
+
+// out layout: [0..11] tensor stats, [12] num_gradients, [13] grad_norms_mean, [14] grad_norms_std,
+// [15] grad_norms_max, [16] cosine_similarity, [17] nonfinite, [18 .. 18+S) norms, [18+S .. 18+2S) cos.
+__global__ __launch_bounds__(256) void grad_final_kernel(const Moments* __restrict__ part, const double* __restrict__ part_seg,
+                                                         const int* __restrict__ seg_first, int C, int S, int ref_valid,
+                                                         float* __restrict__ out, float* __restrict__ range,
+                                                         unsigned* __restrict__ hist, const float* __restrict__ nonfinite) {
+    __shared__ Moments sh[16];
+    __shared__ float red[16];
+    Moments m;
+    m.n = 0.0; m.mean = m.m2 = m.m3 = m.m4 = 0.0; m.mn = INFINITY; m.mx = -INFINITY; m.abssum = 0.0;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) merge(m, part[i]);
+    Moments r = block_merge(m, sh);
+    if (threadIdx.x == 0) write_moment_stats(r, out, range);
+    for (int i = threadIdx.x; i < NHIST; i += blockDim.x) hist[i] = 0u;
+    float* norms = out + 18;
+    float* coss = out + 18 + S;
+    float nsum = 0.f, nsq = 0.f, nmax = 0.f, csum = 0.f;
+    for (int sgi = threadIdx.x; sgi < S; sgi += blockDim.x) {
+        double sq = 0.0, dot = 0.0, rsq = 0.0;
+        for (int c = seg_first[sgi]; c < seg_first[sgi + 1]; ++c) {
+            sq += part_seg[3 * c];
+            dot += part_seg[3 * c + 1];
+            rsq += part_seg[3 * c + 2];
+        }
+        const float nrm = (float)sqrt(sq);
+        const double den = sqrt(sq * rsq);
+        const float cs = (ref_valid && den > 0.0) ? (float)(dot / den) : 1.f;
+        norms[sgi] = nrm;
+        coss[sgi] = cs;
+        nsum += nrm;
+        nsq += nrm * nrm;
+        nmax = fmaxf(nmax, nrm);
+        csum += cs;
+    }
+    nsum = block_sum(nsum, red);
+    nsq = block_sum(nsq, red);
+    csum = block_sum(csum, red);
+    nmax = block_max(nmax, red);
+    if (threadIdx.x == 0) {
+        const float mean = nsum / S;
+        out[12] = (float)S;
+        out[13] = mean;
+        out[14] = sqrtf(fmaxf(nsq / S - mean * mean, 0.f));
+        out[15] = nmax;
+        out[16] = csum / S;
+        out[17] = nonfinite[0];
+    }
+}
+
+// Workspace: [Moments x C][double x 3C][range 2f | nonfinite f | pad f][hist NHIST u32]; caller sizes it.
+TDL_API int tdl_grad_stats(const float* g, float* ref, const int64_t* table, int C, float* out, int64_t n, float beta,
+                           int S, void* ws, int ref_valid, int with_quantiles, hipStream_t s) {
+    Moments* part = (Moments*)ws;
+    double* part_seg = (double*)((char*)ws + sizeof(Moments) * (size_t)C);
+    float* range = (float*)(part_seg + 3 * (size_t)C);
+    float* nonfinite = range + 2;
+    unsigned* hist = (unsigned*)(range + 4);
+    const int* seg_first = (const int*)(table + 3 * (size_t)C);
+    hipMemsetAsync(nonfinite, 0, sizeof(float), s);
+    grad_partial_kernel<<<C, 256, 0, s>>>(g, ref, table, ref_valid, beta, part, part_seg, nonfinite);
+    grad_final_kernel<<<1, 256, 0, s>>>(part, part_seg, seg_first, C, S, ref_valid, out, range, hist, nonfinite);
+    if (with_quantiles) {
+        const int hg = stat_grid(n);
+        hist_kernel<<<hg, 256, 0, s>>>(g, 0, n, range, hist);
+        quantile_kernel<<<1, 64, 0, s>>>(hist, range, out);
+    }
+    TDL_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ K4 z-score detection
+// ring: f32 [H][K] history; state: int32 [4] = (count, head, quarantine_run, seen)
+// cur: f32 [K]; out: f32 [4 + K] = (flag, mean_z, confidence, n_valid, z_0..z_{K-1}; z = -1 if skipped)
+__global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, int* __restrict__ state,
+                                                     const float* __restrict__ cur, int K, int H, int warmup,
+                                                     float z_decision, int exclude_current, int max_quarantine,
+                                                     float* __restrict__ out) {
+    __shared__ float zs[64];
+    __shared__ int cnt_sh;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int count = state[0], head = state[1];
+    if (!exclude_current) {  // reference order: append, then baseline over the window incl. current
+        __syncthreads();
+        for (int k = threadIdx.x; k < K; k += blockDim.x) ring[(size_t)head * K + k] = cur[k];
+        __syncthreads();
+        head = (head + 1) % H;
+        count = count < H ? count + 1 : H;
+    }
+    const bool ready = count >= warmup;
+    for (int k = wid; k < K; k += 4) {
+        float s = 0.f;
+        for (int h = lane; h < count; h += 64) s += ring[(size_t)h * K + k];
+        const float mean = wave_sum(s) / (count > 0 ? count : 1);
+        float q = 0.f;
+        for (int h = lane; h < count; h += 64) {
+            const float d = ring[(size_t)h * K + k] - mean;
+            q += d * d;
+        }
+        const float sd = sqrtf(wave_sum(q) / (count > 0 ? count : 1));
+        if (lane == 0) {
+            float z = -1.f;
+            if (ready && sd > 0.f) {
+                const float c = cur[k];
+                z = isfinite(c) ? fabsf((c - mean) / sd) : 1e6f;
+            }
+            zs[k] = z;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float sum = 0.f;
+        int nv = 0;
+        for (int k = 0; k < K; ++k)
+            if (zs[k] >= 0.f) { sum += zs[k]; ++nv; }
+        const float mz = nv ? sum / nv : 0.f;
+        const bool flag = ready && mz > z_decision;
+        out[0] = flag ? 1.f : 0.f;
+        out[1] = mz;
+        out[2] = fminf(1.f, mz / 5.f);
+        out[3] = (float)nv;
+        int appended = 0;
+        if (exclude_current) {
+            if (flag && state[2] < max_quarantine) {
+                state[2] += 1;
+            } else {
+                state[2] = 0;
+                appended = 1;
+            }
+        }
+        cnt_sh = appended;
+        state[3] += 1;
+    }
+    for (int k = threadIdx.x; k < K; k += blockDim.x) out[4 + k] = zs[k];
+    __syncthreads();
+    if (exclude_current && cnt_sh) {
+        for (int k = threadIdx.x; k < K; k += blockDim.x) ring[(size_t)head * K + k] = cur[k];
+        head = (head + 1) % H;
+        count = count < H ? count + 1 : H;
+    }
+    if (threadIdx.x == 0) {
+        state[0] = count;
+        state[1] = head;
+    }
+}
+
+TDL_API int tdl_zscore_detect(float* ring, int* state, const float* cur, int K, int H, int warmup, float z_decision,
+                              float unused, int exclude_current, int max_quarantine, float* out, hipStream_t s) {
+    (void)unused;
+    zscore_kernel<<<1, 256, 0, s>>>(ring, state, cur, K, H, warmup, z_decision, exclude_current, max_quarantine, out);
+    TDL_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ K5 trust update
+// status codes: 0 TRUSTED, 1 SUSPICIOUS, 2 COMPROMISED, 3 RECOVERING, 4 OFFLINE
+__global__ void trust_update_kernel(float* __restrict__ values, int* __restrict__ counts, int* __restrict__ status,
+                                    const float* __restrict__ metrics, const float* __restrict__ w,
+                                    const int* __restrict__ flags, const float* __restrict__ recovery, int N, float thr,
+                                    float decay_rate, float dt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    int st = status[i];
+    if (st == 4) return;  // OFFLINE: frozen until the runtime re-admits the node
+    float old = values[i];
+    if (flags && flags[i]) {  // detection => mark_compromised (trust_manager.py:183-196)
+        st = 2;
+        old = 0.1f;
+    }
+    const float* m = metrics + 6 * i;
+    const float comp[6] = {1.f - fminf(1.f, m[0]), m[1], 1.f - fminf(1.f, m[2] / 10.f), fminf(1.f, m[3]),
+                           1.f - fminf(1.f, m[4]), m[5]};
+    float score = 0.f;
+    for (int k = 0; k < 6; ++k) score += w[k] * comp[k];
+    score = fminf(1.f, fmaxf(0.f, score));
+    const float decay = expf(-decay_rate * dt);
+    float fin = 0.9f * old * decay + 0.1f * score;
+    if (st == 3 && recovery) fin += recovery[i];
+    fin = fminf(1.f, fmaxf(0.f, fin));
+    int ns;
+    if (fin < 0.3f) ns = 2;
+    else if (fin < thr) ns = 1;
+    else if (st == 2 && fin > 0.8f) ns = 3;
+    else if (st == 3 && fin > 0.9f) ns = 0;
+    else ns = 0;  // fin >= thr
+    values[i] = fin;
+    status[i] = ns;
+    counts[i] += 1;
+}
+
+TDL_API int tdl_trust_update(float* values, int* counts, int* status, const float* metrics, const float* weights,
+                             const int* flags, const float* recovery, int N, float thr, float decay_rate, float dt,
+                             hipStream_t s) {
+    trust_update_kernel<<<(N + 63) / 64, 64, 0, s>>>(values, counts, status, metrics, weights, flags, recovery, N, thr,
+                                                     decay_rate, dt);
+    TDL_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ K7 KL(softmax(b) || softmax(a)), batchmean
+// a, b: f32 [R, C]; out f32 [1] (accumulated with atomics; caller zeroes).  One block per row.
+__global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ a, const float* __restrict__ b, int R, int C,
+                                                 float* __restrict__ out) {
+    __shared__ float red[16];
+    const int row = blockIdx.x;
+    const float* ar = a + (size_t)row * C;
+    const float* br = b + (size_t)row * C;
+    float ma = -INFINITY, mb = -INFINITY;
+    for (int j = threadIdx.x; j < C; j += 256) { ma = fmaxf(ma, ar[j]); mb = fmaxf(mb, br[j]); }
+    ma = block_max(ma, red);
+    mb = block_max(mb, red);
+    float sa = 0.f, sb = 0.f;
+    for (int j = threadIdx.x; j < C; j += 256) { sa += __expf(ar[j] - ma); sb += __expf(br[j] - mb); }
+    sa = block_sum(sa, red);
+    sb = block_sum(sb, red);
+    const float lsa = ma + __logf(sa), lsb = mb + __logf(sb);
+    float kl = 0.f;
+    for (int j = threadIdx.x; j < C; j += 256) {
+        const float lq = br[j] - lsb;  // log target prob
+        kl += __expf(lq) * (lq - (ar[j] - lsa));
+    }
+    kl = block_sum(kl, red);
+    if (threadIdx.x == 0) atomicAdd(out, kl / R);
+}
+
+TDL_API int tdl_kl_div_softmax(const float* a, const float* b, int R, int C, float* out, hipStream_t s) {
+    hipMemsetAsync(out, 0, sizeof(float), s);
+    kl_kernel<<<R, 256, 0, s>>>(a, b, R, C, out);
+    TDL_LAUNCH_CHECK();
+}

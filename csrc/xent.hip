@@ -1,0 +1,101 @@
+// Softmax cross-entropy over LM-head logits (replaces the
+// CrossEntropyLoss of distributed_trainer.py:435-439, applied to real logits).
+//
+// Logits are bf16 [M, ld] with ld >= V (vocab padded to a multiple of 64 so every row is
+// 16-byte aligned); columns >= V are padding and are masked out.  One 256-thread block per
+// row, online (max, sum-exp) per thread, a single block merge.  The backward recomputes
+// softmax from the saved log-sum-exp and writes dlogits in place (the logits buffer is dead
+// after the loss), scaled by a DEVICE scalar (grad_output / n_valid) so no host sync is needed.
+#include "common.h"
+
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+    const float mn = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+    m = mn;
+}
+
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss, float* __restrict__ lse_out, int V, int ld,
+                                                       int ignore_index) {
+    __shared__ float red_m[4], red_s[4];
+    const int row = blockIdx.x;
+    const bf16_t* lr = logits + (size_t)row * ld;
+    float m = -INFINITY, s = 0.f;
+    const int nvec = V / 8;
+    for (int i = threadIdx.x; i < nvec; i += 256) {
+        float v[8];
+        unpack8(((const uint4*)lr)[i], v);
+        float vm = v[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) vm = fmaxf(vm, v[k]);
+        float vs = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vs += __expf(v[k] - vm);
+        online_merge(m, s, vm, vs);
+    }
+    for (int j = nvec * 8 + threadIdx.x; j < V; j += 256) online_merge(m, s, bf2f(lr[j]), 1.f);
+    // wave merge
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+        online_merge(m, s, m2, s2);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red_m[wid] = m;
+        red_s[wid] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float M0 = red_m[0], S0 = red_s[0];
+        for (int w = 1; w < 4; ++w) online_merge(M0, S0, red_m[w], red_s[w]);
+        const float lse = M0 + __logf(S0);
+        lse_out[row] = lse;
+        const int64_t lab = labels[row];
+        loss[row] = (lab == ignore_index || lab < 0 || lab >= V) ? 0.f : lse - bf2f(lr[lab]);
+    }
+}
+
+TDL_API int tdl_xent_fwd(const void* logits, const int64_t* labels, float* loss, float* lse, int M, int V, int ld,
+                         hipStream_t s) {
+    xent_fwd_kernel<<<M, 256, 0, s>>>((const bf16_t*)logits, labels, loss, lse, V, ld, -100);
+    TDL_LAUNCH_CHECK();
+}
+
+// dlogits[r, j] = (softmax_j - [j == label]) * scale  for j < V, 0 for padding columns.
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                       const float* __restrict__ lse_in, const float* __restrict__ scale_ptr,
+                                                       bf16_t* __restrict__ dlogits, int V, int ld, int ignore_index) {
+    const int row = blockIdx.x;
+    const int64_t lab = labels[row];
+    const bool ign = (lab == ignore_index || lab < 0 || lab >= V);
+    const float lse = lse_in[row];
+    const float sc = ign ? 0.f : scale_ptr[0];
+    const bf16_t* lr = logits + (size_t)row * ld;
+    bf16_t* dr = dlogits + (size_t)row * ld;
+    const int nvec = ld / 8;
+    for (int i = threadIdx.x; i < nvec; i += 256) {
+        float v[8];
+        unpack8(((const uint4*)lr)[i], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = i * 8 + k;
+            float p = j < V ? __expf(v[k] - lse) : 0.f;
+            if (j == lab) p -= 1.f;
+            v[k] = p * sc;
+        }
+        ((uint4*)dr)[i] = pack8(v);
+    }
+    for (int j = nvec * 8 + threadIdx.x; j < ld; j += 256) {
+        float p = j < V ? __expf(bf2f(lr[j]) - lse) : 0.f;
+        if (j == lab) p -= 1.f;
+        dr[j] = f2bf(p * sc);
+    }
+}
+
+TDL_API int tdl_xent_bwd(const void* logits, const int64_t* labels, const float* lse, const float* scale_ptr, void* dlogits,
+                         int M, int V, int ld, float unused, hipStream_t s) {
+    (void)unused;
+    xent_bwd_kernel<<<M, 256, 0, s>>>((const bf16_t*)logits, labels, lse, scale_ptr, (bf16_t*)dlogits, V, ld, -100);
+    TDL_LAUNCH_CHECK();
+}

@@ -1,0 +1,305 @@
+"""Numerics of every native HIP kernel against a plain PyTorch fp32 reference (GPU only)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from trustworthy_dl.ops import _lib
+    _lib.lib()  # must load: no silent fallback
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("N", [768, 1024, 300])
+def test_layernorm(N):
+    from trustworthy_dl.ops import layer_norm
+    M = 257
+    x = torch.randn(M, N, device=DEV).bfloat16().requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16().requires_grad_(True)
+    b = (0.1 * torch.randn(N, device=DEV)).bfloat16().requires_grad_(True)
+    y = layer_norm(x, w, b, 1e-5)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (N,), wr, br, 1e-5)
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 2e-2
+
+
+def test_linear_gelu_and_main_grad():
+    from trustworthy_dl.ops import linear
+    M, K, N = 512, 256, 1024
+    x = torch.randn(M, K, device=DEV).bfloat16().requires_grad_(True)
+    W = (torch.randn(K, N, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16().requires_grad_(True)
+    W.main_grad = torch.zeros(K, N, device=DEV)
+    b.main_grad = torch.zeros(N, device=DEV)
+    for act in ("gelu", None):
+        W.main_grad.zero_()
+        b.main_grad.zero_()
+        x.grad = None
+        y = linear(x, W, b, act)
+        g = torch.randn_like(y)
+        y.backward(g)
+        xr, Wr, br = (t.detach().float().requires_grad_(True) for t in (x, W, b))
+        yr = xr @ Wr + br
+        if act == "gelu":
+            yr = torch.nn.functional.gelu(yr, approximate="tanh")
+        yr.backward(g.float())
+        assert _rel(y, yr) < 1e-2, act
+        assert _rel(x.grad, xr.grad) < 2e-2, act
+        assert _rel(W.main_grad, Wr.grad) < 2e-2, act
+        assert _rel(b.main_grad, br.grad) < 2e-2, act
+        assert W.grad is None and b.grad is None
+
+
+def test_linear_t():
+    from trustworthy_dl.ops.layers import linear_t
+    M, K, N = 384, 128, 640
+    x = torch.randn(M, K, device=DEV).bfloat16().requires_grad_(True)
+    W = (torch.randn(N, K, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    y = linear_t(x, W)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, Wr = x.detach().float().requires_grad_(True), W.detach().float().requires_grad_(True)
+    (xr @ Wr.t()).backward(g.float())
+    assert _rel(y, xr @ Wr.t()) < 1e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(W.grad, Wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("T,H", [(128, 2), (256, 4)])
+def test_flash_attention(T, H):
+    from trustworthy_dl.ops import causal_attention
+    B, D = 2, 64
+    qkv = (torch.randn(B, T, 3 * H * D, device=DEV)).bfloat16().requires_grad_(True)
+    o = causal_attention(qkv, H, True)
+    g = torch.randn_like(o)
+    o.backward(g)
+    x = qkv.detach().float().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)
+    ref = ref.transpose(1, 2).reshape(B, T, H * D)
+    ref.backward(g.float())
+    assert _rel(o, ref) < 2e-2
+    assert _rel(qkv.grad, x.grad) < 3e-2
+
+
+def test_attention_rescale_branch():
+    """Force the online-softmax running max to jump inside a row (rule 26)."""
+    from trustworthy_dl.ops import causal_attention
+    B, T, H, D = 1, 256, 1, 64
+    qkv = torch.randn(B, T, 3 * H * D, device=DEV) * 0.1
+    qkv[0, 200, 64:128] = 3.0   # a late key with a huge score for every query
+    qkv[0, :, 0:64] = 3.0 / 8
+    qkv = qkv.bfloat16()
+    o = causal_attention(qkv, H, True)
+    x = qkv.float()
+    q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, H * D)
+    assert _rel(o, ref) < 2e-2
+
+
+def test_embedding():
+    from trustworthy_dl.ops import embedding
+    B, T, Hd, V = 2, 128, 256, 1000
+    ids = torch.randint(0, V, (B, T), device=DEV)
+    ids[0, :5] = 7  # repeated ids collide in the scatter
+    wte = torch.randn(V, Hd, device=DEV).bfloat16().requires_grad_(True)
+    wpe = torch.randn(T, Hd, device=DEV).bfloat16().requires_grad_(True)
+    y = embedding(ids, wte, wpe)
+    g = torch.randn_like(y)
+    y.backward(g)
+    wr, pr = wte.detach().float().requires_grad_(True), wpe.detach().float().requires_grad_(True)
+    yr = wr[ids] + pr[:T]
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(wte.grad, wr.grad) < 2e-2
+    assert _rel(wpe.grad, pr.grad) < 2e-2
+
+
+def test_cross_entropy_padded_vocab():
+    from trustworthy_dl.ops import cross_entropy
+    M, V, ld = 64, 1000, 1024
+    logits = torch.randn(M, ld, device=DEV).bfloat16().requires_grad_(True)
+    labels = torch.randint(0, V, (M,), device=DEV)
+    loss = cross_entropy(logits, labels, V)
+    loss.backward()
+    lr = logits.detach().float()[:, :V].requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, labels)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-2
+    assert _rel(logits.grad[:, :V], lr.grad) < 2e-2
+    assert float(logits.grad[:, V:].abs().max()) == 0.0
+
+
+def test_adamw_flat_matches_torch():
+    from trustworthy_dl.parallel.flat import AdamWConfig, FlatParams
+    m = torch.nn.Linear(64, 32)
+    ref = torch.nn.Linear(64, 32)
+    ref.load_state_dict(m.state_dict())
+    fp = FlatParams(m.to(DEV), DEV, torch.float32)
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.0)
+    cfg = AdamWConfig(lr=1e-2, weight_decay=0.0)
+    for _ in range(3):
+        g = torch.randn(fp.numel)
+        fp.grad.copy_(g.to(DEV))
+        off = 0
+        for p, q in zip(fp.params, ref.parameters()):
+            pass
+        # map flat grads onto the reference params by name
+        names = dict(ref.named_parameters())
+        for i, n in enumerate(fp.names):
+            names[n].grad = g[fp.offsets[i]:fp.offsets[i + 1]].view(fp.shapes[i]).clone()
+        fp.adamw_step(cfg)
+        opt.step()
+    names = dict(ref.named_parameters())
+    for i, n in enumerate(fp.names):
+        assert torch.allclose(fp.view(fp.master, i).cpu(), names[n].detach(), atol=1e-5)
+
+
+def test_adamw_skip_flag():
+    from trustworthy_dl.parallel.flat import AdamWConfig, FlatParams
+    m = torch.nn.Linear(16, 16).to(DEV)
+    fp = FlatParams(m, DEV, torch.bfloat16)
+    before = fp.master.clone()
+    fp.grad.fill_(1.0)
+    ctrl = torch.tensor([1.0, 1.0], device=DEV)
+    fp.adamw_step(AdamWConfig(lr=1e-1), ctrl=ctrl)
+    assert torch.equal(fp.master, before)
+    assert float(fp.grad.abs().max()) == 0.0
+
+
+def test_tensor_stats():
+    from trustworthy_dl.ops.stats import tensor_stats
+    from trustworthy_dl.security.attack_detection import numpy_tensor_statistics, TENSOR_STATS
+    x = torch.randn(1 << 20, device=DEV) * 2 + 0.5
+    x[::1000] += 5.0
+    for dt in (torch.float32, torch.bfloat16):
+        xt = x.to(dt)
+        v = tensor_stats(xt).cpu()
+        ref = numpy_tensor_statistics(xt.float().cpu().numpy())
+        rng = ref["max"] - ref["min"]
+        for i, k in enumerate(TENSOR_STATS):
+            tol = rng / 2048 * 1.5 if k in ("median", "percentile_25", "percentile_75") else \
+                1e-3 * max(1.0, abs(ref[k]))
+            assert abs(float(v[i]) - ref[k]) <= tol, (dt, k, float(v[i]), ref[k])
+        assert float(v[12]) == 0.0
+    y = x.clone()
+    y[3] = float("nan")
+    assert float(tensor_stats(y)[12]) == 1.0
+
+
+def test_grad_stats_matches_cpu():
+    from trustworthy_dl.ops.stats import FlatGradStats
+    sizes = [1000, 70000, 5, 40000]
+    n = sum(sizes)
+    gpu = FlatGradStats(sizes, DEV)
+    cpu = FlatGradStats(sizes, "cpu")
+    for step in range(3):
+        g = torch.randn(n)
+        a = gpu.compute(g.to(DEV)).cpu()
+        b = cpu.compute(g.clone())
+        # moments, norms, cosines
+        for i in list(range(4)) + [5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17]:
+            assert abs(float(a[i]) - float(b[i])) <= 2e-3 * max(1.0, abs(float(b[i]))), (step, i, a[i], b[i])
+        assert torch.allclose(a[18:], b[18:], rtol=1e-3, atol=1e-4)
+
+
+def test_zscore_matches_cpu():
+    from trustworthy_dl.ops.stats import DeviceZScore
+    K = 17
+    dg = DeviceZScore(K, DEV, history=50, warmup=10)
+    dc = DeviceZScore(K, "cpu", history=50, warmup=10)
+    g = torch.Generator().manual_seed(1)
+    for step in range(80):
+        cur = torch.randn(K, generator=g)
+        if step in (30, 31, 60):
+            cur = cur * 20
+        a = dg.observe(cur.to(DEV)).cpu()
+        b = dc.observe(cur.clone())
+        assert float(a[0]) == float(b[0]), step
+        assert abs(float(a[1]) - float(b[1])) < 1e-3 * max(1, float(b[1])), step
+
+
+def test_trust_update_matches_python():
+    from trustworthy_dl.core.trust_manager import STATUS_CODES, TrustManager
+    from trustworthy_dl.ops.stats import trust_update
+    N = 5
+    tm = TrustManager(N, 0.7, decay_clock="step")
+    vals = torch.ones(N, device=DEV)
+    cnt = torch.zeros(N, dtype=torch.int32, device=DEV)
+    st = torch.zeros(N, dtype=torch.int32, device=DEV)
+    w = torch.tensor(tm.weights_vector(), device=DEV)
+    g = torch.Generator().manual_seed(0)
+    for step in range(40):
+        tm.advance_step()
+        met = torch.rand(N, 6, generator=g)
+        met[:, 1] = 1 - met[:, 1] * 0.5
+        flags = torch.zeros(N, dtype=torch.int32)
+        if step == 10:
+            flags[2] = 1
+            tm.mark_compromised(2)
+        for i in range(N):
+            tm.update_trust_score(i, float(met[i, 0]), float(met[i, 1]), communication_latency=float(met[i, 2]),
+                                  resource_utilization=float(met[i, 3]), error_rate=float(met[i, 4]),
+                                  uptime=float(met[i, 5]))
+        trust_update(vals, cnt, st, met.to(DEV), w, 0.7, tm.decay_rate, 1.0, flags.to(DEV), None)
+        for i in range(N):
+            assert abs(float(vals[i]) - tm.get_trust_score(i)) < 1e-5, (step, i)
+            assert int(st[i]) == STATUS_CODES[tm.get_node_status(i)], (step, i)
+
+
+def test_attack_inject_modes():
+    from trustworthy_dl.ops.attack import AttackMode, inject_
+    x = torch.randn(10001, device=DEV)
+    y = x.clone()
+    inject_(y, AttackMode.SCALE, 10.0)
+    assert torch.allclose(y, x * 10)
+    y = x.clone()
+    inject_(y, AttackMode.SIGN_FLIP, 1.0)
+    assert torch.allclose(y, -x)
+    y = x.clone()
+    inject_(y, AttackMode.NOISE, 1.0, seed=3, offset=7)
+    z = x.clone()
+    inject_(z, AttackMode.NOISE, 1.0, seed=3, offset=7)
+    assert torch.equal(y, z)  # deterministic
+    d = (y - x)
+    assert abs(float(d.mean())) < 0.05 and abs(float(d.std()) - 1.0) < 0.05
+    yb = x.bfloat16()
+    inject_(yb, AttackMode.ZERO, 0.0)
+    assert float(yb.float().abs().max()) == 0.0
+
+
+def test_gpt2_engine_step_matches_cpu():
+    """A GPT-2-tiny pipeline step on the GPU (bf16 native kernels) tracks the CPU fp32 reference."""
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    torch.manual_seed(0)
+    ids = torch.randint(0, 50257, (4, 129))
+    batch = {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+    losses = {}
+    for dev in ("cpu", "cuda:0"):
+        m = get_model("gpt2-tiny", seq_len=128, seed=3)
+        eng = PipelineEngine(m, EngineConfig(num_nodes=2, micro_batches=2, seq_len=128, device=dev))
+        out = []
+        for _ in range(4):
+            eng.train_step(batch)
+        eng.flush()
+        losses[dev] = eng.last_loss
+    assert abs(losses["cpu"] - losses["cuda:0"]) < 0.05 * losses["cpu"], losses

@@ -1,0 +1,117 @@
+"""Loader for the native HIP kernel library (``trustworthy_dl/_native/libtdl_kernels.so``).
+
+The kernels are plain HIP C++ (csrc/*.hip) compiled for gfx950 by ``build_native.py`` and
+exported through a C ABI: every entry point takes device pointers, sizes and the HIP
+stream to launch on, and returns a ``hipError_t``.  Using a C ABI (instead of a torch C++
+extension) keeps the build to seconds per file and makes every launch capturable in a
+HIP graph (the caller passes the capturing stream).
+
+Policy: a CUDA(HIP) tensor ALWAYS goes to the native kernel.  If the library is missing
+on a machine with a GPU the op raises — there is no silent eager fallback.  CPU tensors
+use the PyTorch reference implementations in the op modules (used by the CPU/gloo tests).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch
+
+_LIB_NAME = "libtdl_kernels.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "_native", _LIB_NAME))
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the native kernel library; raise loudly if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeLibraryMissing(
+                    f"{LIB_PATH} not found: run `python build_native.py` (hipcc --offload-arch=gfx950)")
+            _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            _declare(_lib)
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (NativeLibraryMissing, OSError):
+        return False
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t: Optional[torch.Tensor]) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def check(err: int, name: str):
+    if err != 0:
+        raise RuntimeError(f"native kernel {name} failed with hipError {err}")
+
+
+_P, _I, _L, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+# name -> argtypes (restype is int for all)
+_SIGNATURES = {
+    # norm_act.hip
+    "tdl_layernorm_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
+    "tdl_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_bias_gelu_fwd": [_P, _P, _P, _I, _I, _P],
+    "tdl_bias_gelu_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_embedding_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "tdl_embedding_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
+    "tdl_add_into_f32": [_P, _P, _L, _I, _P],
+    # xent.hip
+    "tdl_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _F, _P],
+    # optim.hip
+    "tdl_adamw_flat": [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _F, _P, _I, _P],
+    "tdl_fill_f32": [_P, _L, _F, _P],
+    # stats.hip
+    "tdl_tensor_stats": [_P, _I, _L, _P, _P, _I, _P],
+    "tdl_grad_stats": [_P, _P, _P, _I, _P, _L, _F, _I, _P, _I, _I, _P],
+    "tdl_zscore_detect": [_P, _P, _P, _I, _I, _I, _F, _F, _I, _I, _P, _P],
+    "tdl_trust_update": [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _P],
+    "tdl_kl_div_softmax": [_P, _P, _I, _I, _P, _P],
+    "tdl_stats_workspace_bytes": [],
+    # attack.hip
+    "tdl_attack_inject": [_P, _I, _L, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P],
+    # attention.hip
+    "tdl_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
+    "tdl_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
+}
+
+
+def _declare(l: ctypes.CDLL):
+    for name, argtypes in _SIGNATURES.items():
+        fn = getattr(l, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int64 if name.endswith("_bytes") else ctypes.c_int
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name)
+    check(fn(*args), name)
+
+
+DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

@@ -1,0 +1,361 @@
+"""Autograd ops for the model compute path.
+
+GPU tensors run the native gfx950 kernels (csrc/norm_act.hip, xent.hip, attention.hip) and
+hipBLASLt GEMMs (csrc/blaslt.cpp); CPU tensors run an equivalent PyTorch reference, which is
+what the CPU/gloo tests exercise.
+
+Gradient accumulation fusion: a parameter may carry ``.main_grad`` — an fp32 view into its
+stage's flat gradient buffer (parallel/flat.py).  Ops then accumulate that parameter's
+gradient straight into ``main_grad`` (fp32 atomics / beta=1 GEMM epilogue on GPU) and return
+``None`` to autograd, so per-micro-batch bf16 weight-gradient tensors never exist.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import ptr, stream_ptr
+
+
+def _accumulate(param: Optional[torch.Tensor], grad: Optional[torch.Tensor]):
+    """Route a parameter gradient: into ``param.main_grad`` if present (returns None), else return it."""
+    if param is None or grad is None:
+        return None
+    mg = getattr(param, "main_grad", None)
+    if mg is None:
+        return grad.to(param.dtype)
+    if grad.is_cuda and grad.dtype != torch.float32 and grad.is_contiguous():
+        _lib.call("tdl_add_into_f32", ptr(mg), ptr(grad), grad.numel(), 1, stream_ptr(grad.device))
+    else:
+        mg.add_(grad.reshape(mg.shape).float())
+    return None
+
+
+def _wants_main_grad(p: Optional[torch.Tensor]) -> bool:
+    return p is not None and getattr(p, "main_grad", None) is not None
+
+
+def _f32_acc(p: torch.Tensor) -> torch.Tensor:
+    """fp32 buffer the kernels accumulate a param gradient into (main_grad or a fresh zero buffer)."""
+    mg = getattr(p, "main_grad", None)
+    return mg if mg is not None else torch.zeros(p.shape, dtype=torch.float32, device=p.device)
+
+
+# ============================================================== LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        M, N = x2.shape
+        if x.is_cuda:
+            y = torch.empty_like(x2)
+            mean = torch.empty(M, dtype=torch.float32, device=x.device)
+            rstd = torch.empty_like(mean)
+            _lib.call("tdl_layernorm_fwd", ptr(x2), ptr(weight), ptr(bias), ptr(y), ptr(mean), ptr(rstd),
+                      M, N, float(eps), stream_ptr(x.device))
+        else:
+            xf = x2.float()
+            mean = xf.mean(-1)
+            rstd = torch.rsqrt(xf.var(-1, unbiased=False) + eps)
+            y = ((xf - mean[:, None]) * rstd[:, None] * weight.float() + bias.float()).to(x.dtype)
+        ctx.save_for_backward(x2, weight, bias, mean, rstd)
+        ctx.shape = shape
+        return y.reshape(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, bias, mean, rstd = ctx.saved_tensors
+        M, N = x2.shape
+        dy2 = dy.reshape(M, N).contiguous()
+        if dy.is_cuda:
+            dx = torch.empty_like(x2)
+            dw = _f32_acc(weight)
+            db = _f32_acc(bias)
+            _lib.call("tdl_layernorm_bwd", ptr(dy2), ptr(x2), ptr(weight), ptr(mean), ptr(rstd), ptr(dx),
+                      ptr(dw), ptr(db), M, N, 0, stream_ptr(dy.device))
+            gw = None if _wants_main_grad(weight) else dw.to(weight.dtype)
+            gb = None if _wants_main_grad(bias) else db.to(bias.dtype)
+            return dx.reshape(ctx.shape), gw, gb, None
+        xf, g = x2.float(), dy2.float()
+        xh = (xf - mean[:, None]) * rstd[:, None]
+        gw_ = g * weight.float()
+        dx = rstd[:, None] * (gw_ - gw_.mean(-1, keepdim=True) - xh * (gw_ * xh).mean(-1, keepdim=True))
+        return (dx.to(dy.dtype).reshape(ctx.shape), _accumulate(weight, (g * xh).sum(0)),
+                _accumulate(bias, g.sum(0)), None)
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5):
+    return _LayerNorm.apply(x, weight, bias, eps)
+
+
+# ============================================================== Linear (HF Conv1D layout: weight [in, out])
+def _gemm_backend(t: torch.Tensor) -> str:
+    if not t.is_cuda:
+        return "cpu"
+    return os.environ.get("TDL_GEMM", "blaslt")
+
+
+class _Linear(torch.autograd.Function):
+    """y = x @ W + b with W stored [in, out] (HF GPT-2 Conv1D); ``act='gelu'`` fuses bias+GELU(tanh)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        backend = _gemm_backend(x)
+        pre = None
+        if backend == "blaslt":
+            from . import blaslt
+            y, pre = blaslt.linear_fwd(x2, weight, bias, act)
+        elif backend == "cpu":
+            y = x2 @ weight
+            if bias is not None:
+                y = y + bias
+            if act == "gelu":
+                pre = y
+                y = F.gelu(y, approximate="tanh")
+        else:  # torch GEMM + native bias-GELU kernel
+            if act == "gelu":
+                pre = torch.mm(x2, weight)
+                y = torch.empty_like(pre)
+                _lib.call("tdl_bias_gelu_fwd", ptr(pre), ptr(bias), ptr(y), pre.shape[0], pre.shape[1],
+                          stream_ptr(x.device))
+            else:
+                y = torch.addmm(bias, x2, weight) if bias is not None else torch.mm(x2, weight)
+        ctx.save_for_backward(x2, weight, bias, pre)
+        ctx.act = act
+        ctx.backend = backend
+        ctx.shape = shape
+        return y.reshape(*shape[:-1], weight.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, bias, pre = ctx.saved_tensors
+        dy2 = dy.reshape(-1, weight.shape[1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        backend = ctx.backend
+        if backend == "blaslt":
+            from . import blaslt
+            dx, gw, gb = blaslt.linear_bwd(x2, weight, bias, pre, dy2, ctx.act,
+                                           ctx.needs_input_grad[0])
+        elif backend == "cpu":
+            if ctx.act == "gelu":
+                pre_ = pre.detach().requires_grad_(True)
+                with torch.enable_grad():
+                    out = F.gelu(pre_, approximate="tanh")
+                dy2 = torch.autograd.grad(out, pre_, dy2)[0]
+            dx = dy2 @ weight.t() if ctx.needs_input_grad[0] else None
+            gw = _accumulate(weight, x2.t() @ dy2)
+            gb = _accumulate(bias, dy2.sum(0)) if bias is not None else None
+        else:
+            if ctx.act == "gelu":
+                dpre = torch.empty_like(pre)
+                db = _f32_acc(bias)
+                _lib.call("tdl_bias_gelu_bwd", ptr(dy2), ptr(pre), ptr(bias), ptr(dpre), ptr(db),
+                          pre.shape[0], pre.shape[1], 0, stream_ptr(dy.device))
+                dy2 = dpre
+                gb = None if _wants_main_grad(bias) else db.to(bias.dtype)
+            else:
+                gb = _accumulate(bias, dy2.float().sum(0)) if bias is not None else None
+            dx = torch.mm(dy2, weight.t()) if ctx.needs_input_grad[0] else None
+            gw = _accumulate(weight, torch.mm(x2.t(), dy2))
+        if dx is not None:
+            dx = dx.reshape(ctx.shape)
+        return dx, gw, gb, None
+
+
+def linear(x, weight, bias=None, act: Optional[str] = None):
+    return _Linear.apply(x, weight, bias, act)
+
+
+# ============================================================== causal self-attention on packed qkv
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, n_head, causal):
+        B, T, C3 = qkv.shape
+        D = C3 // (3 * n_head)
+        scale = 1.0 / math.sqrt(D)
+        qkv = qkv.contiguous()
+        if qkv.is_cuda:
+            if D != 64 or T % 128 != 0:
+                raise ValueError(f"native attention supports head_dim 64 and T % 128 == 0 (got D={D}, T={T})")
+            out = torch.empty(B, T, n_head * D, dtype=qkv.dtype, device=qkv.device)
+            lse = torch.empty(B * n_head, T, dtype=torch.float32, device=qkv.device)
+            _lib.call("tdl_attn_fwd", ptr(qkv), ptr(out), ptr(lse), None, B, T, n_head, D, scale, int(causal),
+                      stream_ptr(qkv.device))
+        else:
+            q, k, v = qkv.float().view(B, T, 3, n_head, D).permute(2, 0, 3, 1, 4)
+            att = (q @ k.transpose(-1, -2)) * scale
+            if causal:
+                mask = torch.ones(T, T, dtype=torch.bool).triu(1)
+                att = att.masked_fill(mask, float("-inf"))
+            lse = torch.logsumexp(att, -1).reshape(B * n_head, T)
+            out = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, n_head * D).to(qkv.dtype)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.n_head, ctx.causal, ctx.scale = n_head, causal, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        B, T, C3 = qkv.shape
+        H = ctx.n_head
+        D = C3 // (3 * H)
+        dout = dout.contiguous()
+        if qkv.is_cuda:
+            dqkv = torch.empty_like(qkv)
+            dq_acc = torch.empty(B, T, H, D, dtype=torch.float32, device=qkv.device)
+            delta = torch.empty(B * H, T, dtype=torch.float32, device=qkv.device)
+            _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), ptr(dq_acc), ptr(delta),
+                      B, T, H, D, ctx.scale, int(ctx.causal), stream_ptr(qkv.device))
+            return dqkv, None, None
+        with torch.enable_grad():
+            x = qkv.detach().float().requires_grad_(True)
+            q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+            att = (q @ k.transpose(-1, -2)) * ctx.scale
+            if ctx.causal:
+                att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1), float("-inf"))
+            o = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, H * D)
+            (g,) = torch.autograd.grad(o, x, dout.float())
+        return g.to(qkv.dtype), None, None
+
+
+def causal_attention(qkv: torch.Tensor, n_head: int, causal: bool = True) -> torch.Tensor:
+    """qkv: [B, T, 3*H*D] packed (c_attn output) -> [B, T, H*D]."""
+    return _Attention.apply(qkv, n_head, causal)
+
+
+# ============================================================== token + position embedding
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, wte, wpe):
+        B, T = ids.shape
+        H = wte.shape[1]
+        ids = ids.contiguous()
+        if ids.is_cuda:
+            out = torch.empty(B, T, H, dtype=wte.dtype, device=wte.device)
+            _lib.call("tdl_embedding_fwd", ptr(ids), ptr(wte), ptr(wpe), ptr(out), B, T, H, 0,
+                      stream_ptr(ids.device))
+        else:
+            out = wte[ids] + wpe[:T].unsqueeze(0)
+        ctx.save_for_backward(ids, wte, wpe)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ids, wte, wpe = ctx.saved_tensors
+        B, T = ids.shape
+        H = wte.shape[1]
+        dout = dout.contiguous()
+        if dout.is_cuda:
+            gte = _f32_acc(wte)
+            gpe = _f32_acc(wpe)
+            _lib.call("tdl_embedding_bwd", ptr(ids), ptr(dout), ptr(gte), ptr(gpe), B, T, H, 0,
+                      stream_ptr(dout.device))
+            return (None, None if _wants_main_grad(wte) else gte.to(wte.dtype),
+                    None if _wants_main_grad(wpe) else gpe.to(wpe.dtype))
+        gte = torch.zeros(wte.shape, dtype=torch.float32)
+        gte.index_add_(0, ids.reshape(-1), dout.reshape(-1, H).float())
+        gpe = torch.zeros(wpe.shape, dtype=torch.float32)
+        gpe[:T] = dout.float().sum(0)
+        return None, _accumulate(wte, gte), _accumulate(wpe, gpe)
+
+
+def embedding(ids, wte, wpe):
+    return _Embedding.apply(ids, wte, wpe)
+
+
+# ============================================================== softmax cross-entropy (padded vocab aware)
+class _CrossEntropy(torch.autograd.Function):
+    """Mean CE over rows of logits [M, ld] whose first ``V`` columns are real classes."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, V):
+        M, ld = logits.shape
+        labels = labels.reshape(-1).contiguous()
+        if logits.is_cuda:
+            loss_rows = torch.empty(M, dtype=torch.float32, device=logits.device)
+            lse = torch.empty(M, dtype=torch.float32, device=logits.device)
+            _lib.call("tdl_xent_fwd", ptr(logits), ptr(labels), ptr(loss_rows), ptr(lse), M, V, ld,
+                      stream_ptr(logits.device))
+        else:
+            lf = logits[:, :V].float()
+            lse = torch.logsumexp(lf, -1)
+            valid = labels >= 0
+            picked = lf.gather(1, labels.clamp(min=0)[:, None])[:, 0]
+            loss_rows = torch.where(valid, lse - picked, torch.zeros_like(lse))
+        n_valid = (labels >= 0).sum().clamp(min=1).float()
+        ctx.save_for_backward(logits, labels, lse, n_valid)
+        ctx.V = V
+        return loss_rows.sum() / n_valid
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse, n_valid = ctx.saved_tensors
+        M, ld = logits.shape
+        V = ctx.V
+        scale = (g.float() / n_valid).reshape(1).contiguous()
+        if logits.is_cuda:
+            # in place: the logits buffer is dead once the loss has been taken
+            _lib.call("tdl_xent_bwd", ptr(logits), ptr(labels), ptr(lse), ptr(scale), ptr(logits), M, V, ld, 0.0,
+                      stream_ptr(logits.device))
+            return logits, None, None
+        p = torch.exp(logits.float() - lse[:, None])
+        p[:, V:] = 0.0
+        valid = labels >= 0
+        p[torch.arange(M)[valid], labels[valid]] -= 1.0
+        p = p * valid[:, None].float() * scale
+        return p.to(logits.dtype), None, None
+
+
+def cross_entropy(logits, labels, num_classes: Optional[int] = None):
+    V = logits.shape[-1] if num_classes is None else num_classes
+    return _CrossEntropy.apply(logits.reshape(-1, logits.shape[-1]), labels, V)
+
+
+# ============================================================== Linear with nn.Linear weight layout [out, in]
+class _LinearT(torch.autograd.Function):
+    """y = x @ W^T, W stored [out, in] (used by the tied LM head: W = wte [vocab, n_embd])."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        backend = _gemm_backend(x)
+        if backend == "blaslt":
+            from . import blaslt
+            y = blaslt.linear_t_fwd(x2, weight)
+        elif backend == "cpu":
+            y = x2 @ weight.t()
+        else:
+            y = torch.mm(x2, weight.t())
+        ctx.save_for_backward(x2, weight)
+        ctx.backend, ctx.shape = backend, shape
+        return y.reshape(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, weight.shape[0])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        if ctx.backend == "blaslt":
+            from . import blaslt
+            dx, gw = blaslt.linear_t_bwd(x2, weight, dy2, ctx.needs_input_grad[0])
+        else:
+            dx = (dy2 @ weight) if ctx.needs_input_grad[0] else None
+            gw = _accumulate(weight, dy2.t() @ x2)
+        return (dx.reshape(ctx.shape) if dx is not None else None), gw
+
+
+def linear_t(x, weight):
+    return _LinearT.apply(x, weight)

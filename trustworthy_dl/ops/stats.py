@@ -1,0 +1,266 @@
+"""Device statistics, detection and trust kernels (csrc/stats.hip) with CPU references.
+
+Statistic vector layouts match ``security.attack_detection.TENSOR_STATS`` / ``GRAD_STATS``.
+Quantiles on the GPU come from a 2048-bin histogram over [min, max] (error <= one bin width,
+i.e. (max - min) / 2048); the CPU path is exact (numpy definitions).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ptr, stream_ptr
+
+N_TENSOR_STATS = 12
+N_GRAD_STATS = 17
+NHIST = 2048
+CHUNK = 1 << 15
+
+_ws_cache = {}
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    w = _ws_cache.get(key)
+    if w is None or w.numel() < nbytes:
+        w = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+        _ws_cache[key] = w
+    return w
+
+
+# ------------------------------------------------------------------ CPU reference
+def _cpu_stats(x: torch.Tensor) -> torch.Tensor:
+    from ..security.attack_detection import numpy_tensor_statistics, TENSOR_STATS
+    arr = x.detach().float().reshape(-1).numpy()
+    fin = np.isfinite(arr)
+    st = numpy_tensor_statistics(arr[fin]) if fin.any() else {k: 0.0 for k in TENSOR_STATS}
+    return torch.tensor([st[k] for k in TENSOR_STATS] + [float((~fin).sum())], dtype=torch.float32)
+
+
+def tensor_stats(x: torch.Tensor, with_quantiles: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[13] float32: TENSOR_STATS + non-finite count.  Device-resident for GPU input."""
+    if not x.is_cuda:
+        return _cpu_stats(x)
+    x = x.detach()
+    if not x.is_contiguous():
+        x = x.contiguous()
+    code = _lib.DTYPE_CODE[x.dtype] if x.dtype in (torch.float32, torch.bfloat16) else None
+    if code is None:
+        x = x.float()
+        code = 0
+    if out is None:
+        out = torch.empty(N_TENSOR_STATS + 1, dtype=torch.float32, device=x.device)
+    ws = _workspace(x.device, int(_lib.lib().tdl_stats_workspace_bytes()))
+    _lib.call("tdl_tensor_stats", ptr(x), code, x.numel(), ptr(out), ptr(ws), int(with_quantiles),
+              stream_ptr(x.device))
+    return out
+
+
+def build_chunk_table(sizes: Sequence[int], device) -> torch.Tensor:
+    """int64 table: C rows of (segment, start, end) followed by S+1 int32 'first chunk' offsets
+    packed into int64 storage (read as int32 by the kernel)."""
+    rows, first = [], []
+    off = 0
+    for s, n in enumerate(sizes):
+        first.append(len(rows))
+        st = off
+        while st < off + n:
+            en = min(st + CHUNK, off + n)
+            rows.append((s, st, en))
+            st = en
+        if n == 0:
+            pass
+        off += n
+    first.append(len(rows))
+    C = len(rows)
+    tab = torch.tensor([v for r in rows for v in r], dtype=torch.int64)
+    f32 = np.array(first, dtype=np.int32)
+    if f32.size % 2:
+        f32 = np.concatenate([f32, np.zeros(1, np.int32)])
+    tail = torch.from_numpy(f32.view(np.int64).copy())
+    return torch.cat([tab, tail]).to(device), C
+
+
+class FlatGradStats:
+    """Segmented statistics over a stage's flat fp32 gradient (one segment per parameter)."""
+
+    def __init__(self, sizes: Sequence[int], device, ref_beta: float = 0.9, track_reference: bool = True):
+        self.sizes = list(sizes)
+        self.S = len(self.sizes)
+        self.n = int(sum(self.sizes))
+        self.device = torch.device(device)
+        self.ref_beta = float(ref_beta)
+        self.ref = torch.zeros(self.n, dtype=torch.float32, device=self.device) if track_reference else None
+        self.ref_valid = False
+        self.out = torch.zeros(18 + 2 * self.S, dtype=torch.float32, device=self.device)
+        if self.device.type == "cuda":
+            self.table, self.C = build_chunk_table(self.sizes, self.device)
+            nbytes = 64 * self.C + 24 * self.C + 16 + 4 * NHIST + 64
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+
+    def compute(self, flat_grad: torch.Tensor, with_quantiles: bool = True) -> torch.Tensor:
+        """Returns the device vector [18 + 2S]: GRAD_STATS(17), nonfinite, norms[S], cos[S]."""
+        if flat_grad.is_cuda:
+            _lib.call("tdl_grad_stats", ptr(flat_grad), ptr(self.ref), ptr(self.table), self.C, ptr(self.out),
+                      self.n, self.ref_beta, self.S, ptr(self.ws), int(self.ref_valid), int(with_quantiles),
+                      stream_ptr(flat_grad.device))
+        else:
+            self.out.copy_(self._cpu(flat_grad))
+        if self.ref is not None:
+            self.ref_valid = True
+        return self.out
+
+    def _cpu(self, g: torch.Tensor) -> torch.Tensor:
+        st = _cpu_stats(g)
+        segs = torch.split(g.detach().float(), self.sizes)
+        norms = torch.stack([s.norm() for s in segs]) if segs else torch.zeros(0)
+        if self.ref is not None and self.ref_valid:
+            rsegs = torch.split(self.ref, self.sizes)
+            cos = []
+            for a, b in zip(segs, rsegs):
+                den = float(a.norm() * b.norm())
+                cos.append(float((a * b).sum()) / den if den > 0 else 1.0)
+            cos = torch.tensor(cos)
+        else:
+            cos = torch.ones(self.S)
+        if self.ref is not None:
+            gg = torch.nan_to_num(g.detach().float(), nan=0.0, posinf=0.0, neginf=0.0)
+            if self.ref_valid:
+                self.ref.mul_(self.ref_beta).add_(gg, alpha=1 - self.ref_beta)
+            else:
+                self.ref.copy_(gg)
+        extra = torch.tensor([float(self.S), float(norms.mean()) if self.S else 0.0,
+                              float(norms.std(unbiased=False)) if self.S else 0.0,
+                              float(norms.max()) if self.S else 0.0, float(cos.mean()) if self.S else 1.0])
+        return torch.cat([st[:12], extra, st[12:13], norms.float(), cos.float()])
+
+
+def grad_stats(grads: Sequence[torch.Tensor], reference: Optional[Sequence[torch.Tensor]] = None,
+               cosine_mode: str = "reference") -> torch.Tensor:
+    """GRAD_STATS vector [17] for an arbitrary list of (GPU) gradient tensors."""
+    grads = [g.detach() for g in grads]
+    dev = grads[0].device
+    flat = torch.cat([g.float().reshape(-1) for g in grads])
+    fs = FlatGradStats([g.numel() for g in grads], dev, track_reference=reference is not None)
+    if reference is not None:
+        fs.ref.copy_(torch.cat([r.float().reshape(-1) for r in reference]))
+        fs.ref_valid = True
+    out = fs.compute(flat)
+    vec = out[:17].clone()
+    if cosine_mode == "pairwise":
+        from ..security.attack_detection import _cosine
+        vec[16] = _cosine(grads, None, "pairwise")
+    return vec
+
+
+class DeviceZScore:
+    """Device ring-buffer baseline + z-score decision for one monitored signal (K4)."""
+
+    def __init__(self, k: int, device, history: int = 1000, warmup: int = 10, z_decision: float = 2.5,
+                 exclude_current: bool = True, max_quarantine: int = 50):
+        self.k, self.history, self.warmup = k, history, warmup
+        self.z_decision = z_decision
+        self.exclude_current = exclude_current
+        self.max_quarantine = max_quarantine
+        self.device = torch.device(device)
+        self.ring = torch.zeros(history, k, dtype=torch.float32, device=self.device)
+        self.state = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self.out = torch.zeros(4 + k, dtype=torch.float32, device=self.device)
+
+    def observe(self, cur: torch.Tensor) -> torch.Tensor:
+        """Returns device vector [4 + k]: flag, mean_z, confidence, n_valid, z[k] (-1 = skipped)."""
+        cur = cur[: self.k].contiguous()
+        if self.device.type == "cuda":
+            _lib.call("tdl_zscore_detect", ptr(self.ring), ptr(self.state), ptr(cur), self.k, self.history,
+                      self.warmup, self.z_decision, 0.0, int(self.exclude_current), self.max_quarantine,
+                      ptr(self.out), stream_ptr(self.device))
+        else:
+            self._cpu(cur)
+        return self.out
+
+    def _cpu(self, cur: torch.Tensor):
+        count, head, qrun, seen = [int(v) for v in self.state.tolist()]
+        H = self.history
+
+        def append(c, h):
+            self.ring[h] = cur
+            return min(c + 1, H), (h + 1) % H
+
+        if not self.exclude_current:
+            count, head = append(count, head)
+        ready = count >= self.warmup
+        zs = torch.full((self.k,), -1.0)
+        if count > 0:
+            hist = self.ring[:count]
+            mean = hist.mean(0)
+            sd = hist.std(0, unbiased=False)
+            for j in range(self.k):
+                if ready and sd[j] > 0:
+                    c = float(cur[j])
+                    zs[j] = abs((c - float(mean[j])) / float(sd[j])) if math.isfinite(c) else 1e6
+        valid = zs >= 0
+        mz = float(zs[valid].mean()) if valid.any() else 0.0
+        flag = ready and mz > self.z_decision
+        if self.exclude_current:
+            if flag and qrun < self.max_quarantine:
+                qrun += 1
+            else:
+                qrun = 0
+                count, head = append(count, head)
+        self.state.copy_(torch.tensor([count, head, qrun, seen + 1], dtype=torch.int32))
+        self.out.copy_(torch.cat([torch.tensor([1.0 if flag else 0.0, mz, min(1.0, mz / 5.0), float(valid.sum())]),
+                                  zs]))
+
+
+def trust_update(values: torch.Tensor, counts: torch.Tensor, status: torch.Tensor, metrics: torch.Tensor,
+                 weights: torch.Tensor, threshold: float, decay_rate: float, dt: float = 1.0,
+                 flags: Optional[torch.Tensor] = None, recovery: Optional[torch.Tensor] = None):
+    """Fused trust update over all nodes (K5), in place on (values, counts, status)."""
+    N = values.numel()
+    if values.is_cuda:
+        _lib.call("tdl_trust_update", ptr(values), ptr(counts), ptr(status), ptr(metrics.contiguous()),
+                  ptr(weights), ptr(flags), ptr(recovery), N, float(threshold), float(decay_rate), float(dt),
+                  stream_ptr(values.device))
+        return
+    from ..core.trust_manager import NodeStatus, STATUS_CODES, STATUS_FROM_CODE, next_status
+    w = weights.double().tolist()
+    for i in range(N):
+        st = STATUS_FROM_CODE[int(status[i])]
+        if st == NodeStatus.OFFLINE:
+            continue
+        old = float(values[i])
+        if flags is not None and int(flags[i]):
+            st, old = NodeStatus.COMPROMISED, 0.1
+        m = metrics[i].double().tolist()
+        comp = [1 - min(1.0, m[0]), m[1], 1 - min(1.0, m[2] / 10.0), min(1.0, m[3]), 1 - min(1.0, m[4]), m[5]]
+        score = min(1.0, max(0.0, sum(a * b for a, b in zip(w, comp))))
+        fin = 0.9 * old * math.exp(-decay_rate * dt) + 0.1 * score
+        if st == NodeStatus.RECOVERING and recovery is not None:
+            fin += float(recovery[i])
+        fin = min(1.0, max(0.0, fin))
+        values[i] = fin
+        status[i] = STATUS_CODES[next_status(st, fin, threshold)]
+        counts[i] += 1
+
+
+def kl_div_softmax(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """KL(softmax(b) || softmax(a)) with 'batchmean' over the last dim (attack_detector.py:172-176)."""
+    a2 = a.detach().float().reshape(-1, a.shape[-1]).contiguous()
+    b2 = b.detach().float().reshape(-1, b.shape[-1]).contiguous()
+    if a2.is_cuda:
+        out = torch.empty(1, dtype=torch.float32, device=a2.device)
+        _lib.call("tdl_kl_div_softmax", ptr(a2), ptr(b2), a2.shape[0], a2.shape[1], ptr(out), stream_ptr(a2.device))
+        return out[0]
+    return torch.nn.functional.kl_div(torch.log_softmax(a2, -1), torch.softmax(b2, -1), reduction="batchmean")
+
+
+def cosine_gram(xs: List[torch.Tensor]) -> torch.Tensor:
+    """N x N cosine similarity of flattened tensors (MFMA GEMM via hipBLASLt on GPU)."""
+    X = torch.stack([x.detach().float().reshape(-1) for x in xs])
+    nrm = X.norm(dim=1).clamp(min=1e-30)
+    G = X @ X.t()
+    return G / (nrm[:, None] * nrm[None, :])

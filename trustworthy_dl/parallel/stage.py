@@ -1,0 +1,116 @@
+"""One pipeline stage: its layer modules, flat parameter buffers and device verifier.
+
+A stage owns a contiguous range ``[a, b)`` of the model's ``pipeline_layers()``.  Its module is
+an ``nn.Sequential`` of (deep copies of) those layers, so stage-local parameter names are
+``"<i>.<name>"`` exactly like the reference's ``nn.Sequential(h[i:j])`` partitions
+(distributed_trainer.py:132-134; checkpoint layout 448-459).
+"""
+from __future__ import annotations
+
+import copy
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from .flat import FlatParams
+from ..security.stage_verifier import StageVerifier
+
+
+def tied_groups(model: nn.Module) -> List[List[Tuple[int, str]]]:
+    """Parameters shared between pipeline layers, as lists of (layer index, attribute)."""
+    layers = model.pipeline_layers()
+    by_id: Dict[int, List[Tuple[int, str]]] = {}
+    for li, layer in enumerate(layers):
+        for name, p in layer.named_parameters(recurse=False):
+            by_id.setdefault(id(p), []).append((li, name))
+        for mname, m in layer.named_modules():
+            if not mname:
+                continue
+            for pname, p in m.named_parameters(recurse=False):
+                by_id.setdefault(id(p), []).append((li, f"{mname}.{pname}"))
+    return [v for v in by_id.values() if len({li for li, _ in v}) > 1]
+
+
+class Stage:
+    def __init__(self, model: nn.Module, layer_range: Tuple[int, int], stage_id: int, num_stages: int,
+                 device, compute_dtype: torch.dtype, verifier_kwargs: Optional[dict] = None,
+                 layers: Optional[List[nn.Module]] = None):
+        self.layer_range = tuple(layer_range)
+        self.stage_id = stage_id
+        self.num_stages = num_stages
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        a, b = self.layer_range
+        if layers is None:
+            layers = copy.deepcopy(model.pipeline_layers()[a:b])
+        # fp32 on the device first: FlatParams copies the fp32 init into the master buffer and
+        # then re-binds every parameter to its compute-dtype (bf16) view
+        self.module = nn.Sequential(*layers).to(self.device)
+        self.takes_tokens = bool(getattr(layers[0], "takes_tokens", False)) or a == 0
+        self.computes_loss = bool(getattr(layers[-1], "computes_loss", False))
+        self.flat = FlatParams(self.module, self.device, compute_dtype)
+        self._hooks = []
+        for p in self.flat.params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._fold_grad))
+        vk = dict(verifier_kwargs or {})
+        self.verifier = StageVerifier(self.flat.sizes, self.device, **vk)
+
+    @staticmethod
+    def _fold_grad(p: torch.Tensor):
+        """Modules not routed through the fused ops (convs, BN, nn.Linear) produce ``.grad``;
+        fold it into the flat fp32 accumulator so every stage verifies/steps one buffer."""
+        if p.grad is not None:
+            p.main_grad.add_(p.grad.float())
+            p.grad = None
+
+    @property
+    def is_first(self) -> bool:
+        return self.layer_range[0] == 0
+
+    def forward(self, x, labels=None):
+        """Returns (output, monitored_activation).  Loss stages return the (scalar) loss."""
+        layers = list(self.module)
+        for layer in layers[:-1]:
+            x = layer(x)
+        last = layers[-1]
+        if self.computes_loss:
+            mon = x if len(layers) > 1 else None
+            out = last(x, labels)
+            if mon is None:
+                mon = getattr(last, "_last_logits", None)
+            return out, mon
+        y = last(x)
+        return y, y
+
+    def local_param(self, layer_idx: int, attr: str) -> Optional[nn.Parameter]:
+        a, b = self.layer_range
+        if not a <= layer_idx < b:
+            return None
+        mod = self.module[layer_idx - a]
+        obj = mod
+        for part in attr.split("."):
+            obj = getattr(obj, part)
+        return obj
+
+    # ---------------------------------------------------------------- migration helpers
+    def layer_state(self, layer_idx: int) -> Dict[str, torch.Tensor]:
+        """fp32 master / exp_avg / exp_avg_sq of one layer's parameters, keyed by layer-local name."""
+        a, _ = self.layer_range
+        pre = f"{layer_idx - a}."
+        out = {}
+        for i, n in enumerate(self.flat.names):
+            if n.startswith(pre):
+                local = n[len(pre):]
+                out[local] = torch.stack([self.flat.view(self.flat.master, i).reshape(-1),
+                                          self.flat.view(self.flat.exp_avg, i).reshape(-1),
+                                          self.flat.view(self.flat.exp_avg_sq, i).reshape(-1)])
+        return out
+
+    def buffers_state(self) -> Dict[str, torch.Tensor]:
+        return {k: v.detach().clone() for k, v in self.module.named_buffers()}
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,452 @@
+"""Statistical attack detection on stage outputs and gradients.
+
+Parity target: reference ``attack_detector.py`` (AttackType, AttackDetectionResult,
+AttackDetector; attack_detector.py:20-487).  Public API, thresholds and the statistic
+set are kept.  Statistics are produced by the device kernels in
+``trustworthy_dl.ops.stats`` (one fused pass, no host copy of the tensor) when the input
+lives on the GPU, and by an exact NumPy path on the CPU; the decision logic below works
+on the resulting small vectors.
+
+Changes vs. the reference, each selectable (``compat=True`` restores the reference):
+
+* ``exclude_current`` — the reference appends the current sample to the history before
+  recomputing the baseline (attack_detector.py:84-98), which inflates the baseline with
+  the attacked sample (recall 0.54 at x10 scaling).  Default: the baseline
+  is built from the history *before* the current sample.
+* ``quarantine_flagged`` — flagged samples are kept out of the baseline window (for up to
+  ``max_quarantine`` consecutive flags, after which the detector assumes a legitimate
+  distribution shift and re-admits samples).
+* gradient ``cosine_similarity`` is the mean per-tensor cosine against an EMA reference
+  gradient (same shapes by construction) instead of the O(P^2) cross-tensor cosine that
+  crashes on mixed shapes (A10).
+* Byzantine detection uses the median pairwise similarity by default (A12).
+* TP/FP counters are updated when ground truth is supplied (A13).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import time
+from collections import defaultdict, deque
+from dataclasses import dataclass
+from enum import Enum
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+logger = logging.getLogger(__name__)
+
+
+class AttackType(Enum):
+    DATA_POISONING = "data_poisoning"
+    MODEL_POISONING = "model_poisoning"
+    GRADIENT_POISONING = "gradient_poisoning"
+    BYZANTINE = "byzantine"
+    BACKDOOR = "backdoor"
+    ADVERSARIAL_INPUT = "adversarial_input"
+
+
+@dataclass
+class AttackDetectionResult:
+    is_attack: bool
+    attack_type: Optional[AttackType]
+    confidence: float
+    evidence: Dict[str, Any]
+    timestamp: float
+    node_id: int
+
+
+# Statistic layout shared with the device kernels (ops/stats.py, csrc/stats.hip).
+TENSOR_STATS = ("mean", "std", "min", "max", "median", "skewness", "kurtosis",
+                "percentile_25", "percentile_75", "norm_l1", "norm_l2", "norm_inf")
+GRAD_EXTRA_STATS = ("num_gradients", "grad_norms_mean", "grad_norms_std",
+                    "grad_norms_max", "cosine_similarity")
+GRAD_STATS = TENSOR_STATS + GRAD_EXTRA_STATS
+
+WARMUP = 10            # attack_detector.py:91,126
+Z_EVIDENCE = 3.0       # attack_detector.py:320
+Z_DECISION = 2.5       # attack_detector.py:330
+BYZANTINE_SIM = 0.5    # attack_detector.py:158
+BACKDOOR_KL = 2.0      # attack_detector.py:179
+
+
+def numpy_tensor_statistics(x: np.ndarray) -> Dict[str, float]:
+    """Exact host statistics with the reference definitions (attack_detector.py:185-200):
+    population std, biased skewness, Fisher (excess) kurtosis."""
+    x = np.asarray(x, dtype=np.float64).ravel()
+    n = x.size
+    mean = float(x.mean())
+    d = x - mean
+    m2 = float(np.mean(d * d))
+    m3 = float(np.mean(d * d * d))
+    m4 = float(np.mean((d * d) ** 2))
+    std = m2 ** 0.5
+    skew = m3 / m2 ** 1.5 if m2 > 0 else 0.0
+    kurt = m4 / (m2 * m2) - 3.0 if m2 > 0 else -3.0
+    return {
+        "mean": mean, "std": std, "min": float(x.min()), "max": float(x.max()),
+        "median": float(np.median(x)), "skewness": skew, "kurtosis": kurt,
+        "percentile_25": float(np.percentile(x, 25)),
+        "percentile_75": float(np.percentile(x, 75)),
+        "norm_l1": float(np.abs(x).sum()), "norm_l2": float(np.sqrt((x * x).sum())),
+        "norm_inf": float(np.abs(x).max()) if n else 0.0,
+    }
+
+
+def tensor_statistics(t: torch.Tensor) -> Dict[str, float]:
+    """Statistics of one tensor; fused device kernel for GPU tensors."""
+    if t.is_cuda:
+        from ..ops import stats as dstats
+        vec = dstats.tensor_stats(t).cpu().tolist()
+        return dict(zip(TENSOR_STATS, vec))
+    return numpy_tensor_statistics(t.detach().float().cpu().numpy())
+
+
+def gradient_statistics(grads: Sequence[torch.Tensor],
+                        reference: Optional[Sequence[torch.Tensor]] = None,
+                        cosine_mode: str = "reference") -> Dict[str, float]:
+    """Stats over a stage's gradient list (attack_detector.py:202-223).
+
+    The moments/quantiles/norms are over all elements (no concatenation on device);
+    ``cosine_similarity`` follows ``cosine_mode``: ``"reference"`` = mean per-tensor cosine
+    vs ``reference`` (EMA gradient; 1.0 when no reference yet), ``"pairwise"`` = reference
+    behaviour restricted to same-shaped pairs (no crash on mixed shapes).
+    """
+    grads = [g for g in grads if g is not None]
+    if not grads:
+        return {}
+    if grads[0].is_cuda:
+        from ..ops import stats as dstats
+        vec = dstats.grad_stats(grads, reference, cosine_mode).cpu().tolist()
+        return dict(zip(GRAD_STATS, vec))
+    flat = torch.cat([g.detach().float().reshape(-1) for g in grads]).numpy()
+    out = numpy_tensor_statistics(flat)
+    norms = np.array([float(g.detach().float().norm()) for g in grads])
+    out.update({"num_gradients": float(len(grads)), "grad_norms_mean": float(norms.mean()),
+                "grad_norms_std": float(norms.std()), "grad_norms_max": float(norms.max()),
+                "cosine_similarity": _cosine(grads, reference, cosine_mode)})
+    return out
+
+
+def _cosine(grads, reference, mode) -> float:
+    if mode == "pairwise":
+        sims = []
+        for i in range(len(grads)):
+            for j in range(i + 1, len(grads)):
+                if grads[i].shape == grads[j].shape:
+                    a, b = grads[i].float().reshape(-1), grads[j].float().reshape(-1)
+                    sims.append(float(torch.nn.functional.cosine_similarity(a, b, dim=0)))
+        return float(np.mean(sims)) if sims else 1.0
+    if reference is None:
+        return 1.0
+    sims = []
+    for g, r in zip(grads, reference):
+        a, b = g.float().reshape(-1), r.float().reshape(-1)
+        den = float(a.norm() * b.norm())
+        sims.append(float((a * b).sum()) / den if den > 0 else 1.0)
+    return float(np.mean(sims)) if sims else 1.0
+
+
+def baseline_from_history(values: np.ndarray, names: Sequence[str], extended: bool) -> Dict[str, Dict]:
+    """Per-statistic baseline over a [H, K] history window (attack_detector.py:241-290)."""
+    base = {}
+    for k, name in enumerate(names):
+        col = values[:, k]
+        entry = {"mean": float(col.mean()), "std": float(col.std())}
+        if extended:
+            entry["min"] = float(col.min())
+            entry["max"] = float(col.max())
+        entry["percentile_5"] = float(np.percentile(col, 5))
+        entry["percentile_95"] = float(np.percentile(col, 95))
+        base[name] = entry
+    return base
+
+
+class AttackDetector:
+    """Detection system (reference attack_detector.py:38-487)."""
+
+    def __init__(self, detection_threshold: float = 0.8, history_size: int = 1000,
+                 compat: bool = False, exclude_current: Optional[bool] = None,
+                 quarantine_flagged: Optional[bool] = None, max_quarantine: int = 50,
+                 byzantine_method: Optional[str] = None, cosine_mode: Optional[str] = None):
+        self.detection_threshold = detection_threshold
+        self.history_size = history_size
+        self.compat = compat
+        self.exclude_current = (not compat) if exclude_current is None else exclude_current
+        self.quarantine_flagged = (not compat) if quarantine_flagged is None else quarantine_flagged
+        self.max_quarantine = max_quarantine
+        self.byzantine_method = byzantine_method or ("mean" if compat else "median")
+        self.cosine_mode = cosine_mode or ("pairwise" if compat else "reference")
+
+        self.output_history: Dict[int, deque] = defaultdict(lambda: deque(maxlen=history_size))
+        self.gradient_history: Dict[int, deque] = defaultdict(lambda: deque(maxlen=history_size))
+        self.loss_history: Dict[int, deque] = defaultdict(lambda: deque(maxlen=history_size))
+        self.output_baselines: Dict[int, Dict] = defaultdict(dict)
+        self.gradient_baselines: Dict[int, Dict] = defaultdict(dict)
+        self.reference_gradients: Dict[int, List[torch.Tensor]] = {}
+        self.reference_beta = 0.9
+        self._quarantine_run: Dict[str, int] = defaultdict(int)
+        self.anomaly_detectors: Dict[int, Any] = {}
+        self.clustering_models: Dict[int, Any] = {}
+        self.last_result: Optional[AttackDetectionResult] = None
+        self.detection_stats = {"total_detections": 0, "false_positives": 0,
+                                "true_positives": 0, "false_negatives": 0,
+                                "true_negatives": 0, "attack_types": defaultdict(int)}
+        logger.info("AttackDetector initialized")
+
+    # ------------------------------------------------------------------ shared engine
+    def _observe(self, kind: str, node_id: int, step: int, stats: Dict[str, float],
+                 names: Sequence[str]) -> AttackDetectionResult:
+        hist = self.output_history[node_id] if kind == "output" else self.gradient_history[node_id]
+        baselines = self.output_baselines if kind == "output" else self.gradient_baselines
+        entry = {"step": step, "stats": stats, "timestamp": time.time()}
+        result = AttackDetectionResult(False, None, 0.0, {}, time.time(), node_id)
+
+        if not self.exclude_current:
+            hist.append(entry)
+        if len(hist) >= WARMUP:
+            vals = np.array([[h["stats"].get(n, 0.0) for n in names] for h in hist], dtype=np.float64)
+            baselines[node_id] = baseline_from_history(vals, names, extended=(kind == "output"))
+            result = self._detect_statistical_anomaly(stats, baselines[node_id], node_id)
+        if self.exclude_current:
+            qkey = f"{kind}{node_id}"
+            if result.is_attack and self.quarantine_flagged and self._quarantine_run[qkey] < self.max_quarantine:
+                self._quarantine_run[qkey] += 1
+            else:
+                self._quarantine_run[qkey] = 0
+                hist.append(entry)
+        self.last_result = result
+        return result
+
+    def _record(self, result: AttackDetectionResult, ground_truth: Optional[bool], count_type: bool):
+        if result.is_attack:
+            self.detection_stats["total_detections"] += 1
+            if count_type and result.attack_type is not None:
+                self.detection_stats["attack_types"][result.attack_type.value] += 1
+        if ground_truth is not None:
+            key = ("true_positives" if ground_truth else "false_positives") if result.is_attack else \
+                  ("false_negatives" if ground_truth else "true_negatives")
+            self.detection_stats[key] += 1
+
+    # ------------------------------------------------------------------ public API
+    def detect_output_anomaly(self, output: Optional[torch.Tensor], node_id: int, step: int,
+                              ground_truth: Optional[bool] = None,
+                              stats: Optional[Dict[str, float]] = None) -> bool:
+        """Z-score test on the stage output statistics (attack_detector.py:71-107)."""
+        if output is None and stats is None:
+            return True
+        if stats is None:
+            stats = tensor_statistics(output.detach())
+        res = self._observe("output", node_id, step, stats, TENSOR_STATS)
+        if res.is_attack:
+            logger.warning("Output anomaly detected on node %d: %s", node_id, res.attack_type)
+        self._record(res, ground_truth, count_type=True)
+        return res.is_attack
+
+    def detect_gradient_poisoning(self, gradients: Optional[Sequence[torch.Tensor]], node_id: int,
+                                  step: int, ground_truth: Optional[bool] = None,
+                                  stats: Optional[Dict[str, float]] = None) -> bool:
+        """Z-score test on gradient statistics (attack_detector.py:109-141)."""
+        if stats is None:
+            if not gradients:
+                return False
+            ref = self.reference_gradients.get(node_id)
+            stats = gradient_statistics(gradients, ref, self.cosine_mode)
+            self._update_reference(node_id, gradients)
+        res = self._observe("gradient", node_id, step, stats, GRAD_STATS)
+        if res.is_attack:
+            logger.warning("Gradient poisoning detected on node %d", node_id)
+        self._record(res, ground_truth, count_type=not self.compat)
+        return res.is_attack
+
+    def _update_reference(self, node_id: int, grads: Sequence[torch.Tensor]):
+        if self.cosine_mode != "reference":
+            return
+        ref = self.reference_gradients.get(node_id)
+        if ref is None or len(ref) != len(grads):
+            self.reference_gradients[node_id] = [g.detach().float().clone() for g in grads]
+            return
+        b = self.reference_beta
+        for r, g in zip(ref, grads):
+            r.mul_(b).add_(g.detach().float(), alpha=1.0 - b)
+
+    def detect_byzantine_behavior(self, node_outputs: Dict[int, torch.Tensor], step: int) -> List[int]:
+        """Cross-replica similarity test (attack_detector.py:143-162).
+
+        Only meaningful between outputs that *should* agree (data-parallel replicas or a
+        shadow recompute of the same stage).  Default statistic: median similarity."""
+        if len(node_outputs) < 3:
+            return []
+        sims = self._calculate_output_similarities(node_outputs)
+        flagged = []
+        for nid, row in sims.items():
+            vals = list(row.values())
+            score = float(np.median(vals)) if self.byzantine_method == "median" else float(np.mean(vals))
+            if score < BYZANTINE_SIM:
+                flagged.append(nid)
+                logger.warning("Byzantine behavior detected on node %d", nid)
+        return flagged
+
+    def detect_backdoor_attack(self, model_outputs: Optional[torch.Tensor],
+                               expected_outputs: Optional[torch.Tensor], node_id: int) -> bool:
+        """KL(softmax(expected) || softmax(out)) > 2.0 (attack_detector.py:164-183)."""
+        if model_outputs is None or expected_outputs is None:
+            return False
+        from ..ops import stats as dstats
+        div = float(dstats.kl_div_softmax(model_outputs, expected_outputs))
+        if div > BACKDOOR_KL:
+            logger.warning("Potential backdoor attack detected on node %d", node_id)
+            return True
+        return False
+
+    # ------------------------------------------------------------------ internals (reference names)
+    def _calculate_tensor_statistics(self, tensor) -> Dict[str, float]:
+        if isinstance(tensor, torch.Tensor):
+            return tensor_statistics(tensor)
+        return numpy_tensor_statistics(np.asarray(tensor))
+
+    def _calculate_gradient_statistics(self, gradients: Sequence[torch.Tensor]) -> Dict[str, float]:
+        return gradient_statistics(gradients, None, self.cosine_mode)
+
+    def _calculate_output_similarities(self, node_outputs: Dict[int, torch.Tensor]) -> Dict[int, Dict[int, float]]:
+        from ..ops import stats as dstats
+        ids = list(node_outputs.keys())
+        gram = dstats.cosine_gram([node_outputs[i] for i in ids]).cpu().numpy()
+        return {a: {b: float(gram[i, j]) for j, b in enumerate(ids) if b != a} for i, a in enumerate(ids)}
+
+    def _detect_statistical_anomaly(self, current: Dict[str, float], baseline: Dict[str, Dict],
+                                    node_id: int) -> AttackDetectionResult:
+        """Mean |z| over statistics with non-zero spread (attack_detector.py:292-342)."""
+        if not baseline:
+            return AttackDetectionResult(False, None, 0.0, {}, time.time(), node_id)
+        zs, evidence = [], {}
+        for name, value in current.items():
+            b = baseline.get(name)
+            if b is None or not b["std"] > 0:
+                continue
+            z = abs((value - b["mean"]) / b["std"])
+            zs.append(z)
+            if z > Z_EVIDENCE:
+                evidence[name] = {"z_score": z, "current_value": value,
+                                  "baseline_mean": b["mean"], "baseline_std": b["std"]}
+        score = float(np.mean(zs)) if zs else 0.0
+        is_attack = score > Z_DECISION
+        atype = self._classify_attack_type(evidence, current)
+        return AttackDetectionResult(is_attack, atype if is_attack else None,
+                                     min(1.0, score / 5.0), evidence, time.time(), node_id)
+
+    def _detect_gradient_anomaly(self, grad_stats, baseline, node_id) -> AttackDetectionResult:
+        return self._detect_statistical_anomaly(grad_stats, baseline, node_id)
+
+    def _update_output_baseline(self, node_id: int):
+        hist = self.output_history[node_id]
+        if len(hist) >= WARMUP:
+            vals = np.array([[h["stats"].get(n, 0.0) for n in TENSOR_STATS] for h in hist])
+            self.output_baselines[node_id] = baseline_from_history(vals, TENSOR_STATS, True)
+
+    def _update_gradient_baseline(self, node_id: int):
+        hist = self.gradient_history[node_id]
+        if len(hist) >= WARMUP:
+            vals = np.array([[h["stats"].get(n, 0.0) for n in GRAD_STATS] for h in hist])
+            self.gradient_baselines[node_id] = baseline_from_history(vals, GRAD_STATS, False)
+
+    @staticmethod
+    def _classify_attack_type(evidence: Dict, stats: Dict) -> Optional[AttackType]:
+        """Rule table (attack_detector.py:350-363)."""
+        if not evidence:
+            return None
+        if "norm_l2" in evidence and evidence["norm_l2"]["z_score"] > 5:
+            return AttackType.GRADIENT_POISONING
+        if "std" in evidence and evidence["std"]["z_score"] > 4:
+            return AttackType.DATA_POISONING
+        if "skewness" in evidence or "kurtosis" in evidence:
+            return AttackType.ADVERSARIAL_INPUT
+        return AttackType.BYZANTINE
+
+    # ------------------------------------------------------------------ ML detectors (host, off hot path)
+    def update_detection_models(self):
+        """IsolationForest + DBSCAN per node with >=50 samples (attack_detector.py:381-409)."""
+        from sklearn.cluster import DBSCAN
+        from sklearn.ensemble import IsolationForest
+        for nid, hist in self.output_history.items():
+            if len(hist) < 50:
+                continue
+            feats = np.array([[h["stats"][n] for n in TENSOR_STATS] for h in hist])
+            self.anomaly_detectors[nid] = IsolationForest(
+                contamination=0.1, random_state=42, n_estimators=100).fit(feats)
+            self.clustering_models[nid] = DBSCAN(eps=0.5, min_samples=5).fit(feats)
+        logger.info("Detection models updated")
+
+    def detect_with_ml_models(self, stats: Dict[str, float], node_id: int) -> bool:
+        model = self.anomaly_detectors.get(node_id)
+        if model is None:
+            return False
+        vec = np.array([stats[n] for n in TENSOR_STATS]).reshape(1, -1)
+        return bool(model.predict(vec)[0] == -1)
+
+    # ------------------------------------------------------------------ reporting
+    def get_detection_statistics(self) -> Dict:
+        ds = self.detection_stats
+        total = ds["total_detections"]
+        tp, fp, fn = ds["true_positives"], ds["false_positives"], ds["false_negatives"]
+        prec = tp / (tp + fp) if tp + fp else 0.0
+        rec = tp / (tp + fn) if tp + fn else 0.0
+        return {
+            "total_detections": total,
+            "false_positive_rate": fp / max(1, total),
+            "true_positive_rate": tp / max(1, total),
+            "precision": prec, "recall": rec,
+            "f1": 2 * prec * rec / (prec + rec) if prec + rec else 0.0,
+            "attack_type_distribution": dict(ds["attack_types"]),
+            "nodes_monitored": len(self.output_history),
+            "average_history_length": float(np.mean([len(h) for h in self.output_history.values()]))
+            if self.output_history else 0.0,
+        }
+
+    def set_detection_threshold(self, threshold: float):
+        self.detection_threshold = float(np.clip(threshold, 0.0, 1.0))
+
+    def reset_node_history(self, node_id: int):
+        for d in (self.output_history, self.gradient_history):
+            if node_id in d:
+                d[node_id].clear()
+        self.output_baselines.pop(node_id, None)
+        self.gradient_baselines.pop(node_id, None)
+        self.reference_gradients.pop(node_id, None)
+
+    def export_detection_data(self, filepath: str):
+        """JSON export, reference schema (attack_detector.py:460-478)."""
+        data = {
+            "detection_stats": {k: (dict(v) if isinstance(v, defaultdict) else v)
+                                for k, v in self.detection_stats.items()},
+            "baselines": {"output": {str(k): v for k, v in self.output_baselines.items()},
+                          "gradient": {str(k): v for k, v in self.gradient_baselines.items()}},
+            "history_lengths": {str(k): len(h) for k, h in self.output_history.items()},
+        }
+        with open(filepath, "w") as f:
+            json.dump(data, f, indent=2, default=float)
+
+    def state_dict(self) -> Dict:
+        return {
+            "output_history": {k: list(v) for k, v in self.output_history.items()},
+            "gradient_history": {k: list(v) for k, v in self.gradient_history.items()},
+            "detection_stats": {k: (dict(v) if isinstance(v, defaultdict) else v)
+                                for k, v in self.detection_stats.items()},
+        }
+
+    def load_state_dict(self, sd: Dict):
+        for k, v in sd["output_history"].items():
+            self.output_history[int(k)] = deque(v, maxlen=self.history_size)
+        for k, v in sd["gradient_history"].items():
+            self.gradient_history[int(k)] = deque(v, maxlen=self.history_size)
+        ds = dict(sd["detection_stats"])
+        ds["attack_types"] = defaultdict(int, ds.get("attack_types", {}))
+        self.detection_stats.update(ds)
+
+    def cleanup(self):
+        self.output_history.clear()
+        self.gradient_history.clear()
+        self.loss_history.clear()
+        self.anomaly_detectors.clear()
+        self.clustering_models.clear()

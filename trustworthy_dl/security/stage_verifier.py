@@ -1,0 +1,179 @@
+"""Device-resident verification of one pipeline stage (the engine's fast path).
+
+Per training step, without any host synchronisation:
+
+1. output statistics of the stage's first micro-batch output (K1+K2, on a side HIP stream so it
+   overlaps the next micro-batch's compute) -> z-score decision against a device ring baseline (K4);
+2. segmented gradient statistics over the stage's flat fp32 gradient (K3: per-parameter norms,
+   cosine vs an EMA reference gradient, moments, quantiles, non-finite count) -> z-score decision;
+3. trust metrics (reference formulas distributed_trainer.py:228-271, with the symmetric
+   gradient-consistency fix) from device EMA baselines;
+4. a fixed-size float "digest" row that the engine all-gathers across ranks; every rank then
+   runs the fused trust update (K5) on identical data, and the optimizer reads a 2-float control
+   block (grad scale, skip) written here — a flagged gradient is quarantined on device.
+
+The host mirrors (TrustManager / AttackDetector / attack_history) are fed from the digests one
+step later through a pinned, non-blocking copy.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from ..ops import stats as S
+
+# digest layout (floats)
+D_LOSS, D_OUT_FLAG, D_OUT_Z, D_GRAD_FLAG, D_GRAD_Z = 0, 1, 2, 3, 4
+D_METRICS = 5  # 6 trust metrics: output_deviation, gradient_consistency, latency, utilization, error, uptime
+D_GRAD_SUMSQ, D_OUT_MEAN, D_OUT_STD, D_GRAD_L2, D_NONFINITE, D_GRAD_COS = 11, 12, 13, 14, 15, 16
+D_ATTACK_TRUTH, D_PRESENT, D_STAGE, D_OUT_CONF, D_GRAD_CONF = 17, 18, 19, 20, 21
+DIGEST = 24
+
+
+class StageVerifier:
+    def __init__(self, param_sizes: Sequence[int], device, *, history: int = 1000, warmup: int = 10,
+                 z_decision: float = 2.5, exclude_current: bool = True, max_quarantine: int = 50,
+                 ema_beta: float = 0.95, symmetric_consistency: bool = True, quarantine: bool = True,
+                 output_detection: bool = True, gradient_verification: bool = True):
+        self.device = torch.device(device)
+        self.output_detection = output_detection
+        self.gradient_verification = gradient_verification
+        self.quarantine = quarantine
+        self.symmetric = symmetric_consistency
+        self.beta = ema_beta
+        self.warmup = warmup
+        kw = dict(history=history, warmup=warmup, z_decision=z_decision, exclude_current=exclude_current,
+                  max_quarantine=max_quarantine)
+        self.out_det = S.DeviceZScore(12, self.device, **kw)
+        self.grad_det = S.DeviceZScore(17, self.device, **kw)
+        self.grad_stats = S.FlatGradStats(param_sizes, self.device) if len(param_sizes) else None
+        self.S = len(param_sizes)
+        z = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.out_stats = z(13)
+        self.out_mu, self.out_sd, self.out_n = z(1), z(1), z(1)
+        self.norm_ema = z(max(self.S, 1))
+        self.norm_n = z(1)
+        self.ctrl = z(2)
+        self.ctrl[0] = 1.0
+        self.digest = z(DIGEST)
+        self._have_out = False
+        self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+
+    # ---------------------------------------------------------------- output path
+    def observe_output(self, y: torch.Tensor):
+        """Queue statistics of a stage output (call once per step, e.g. for micro-batch 0)."""
+        if not self.output_detection:
+            return
+        if self.side is not None:
+            cur = torch.cuda.current_stream(self.device)
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                S.tensor_stats(y.detach(), out=self.out_stats)
+            y.record_stream(self.side)
+        else:
+            self.out_stats.copy_(S.tensor_stats(y.detach()))
+        self._have_out = True
+
+    # ---------------------------------------------------------------- gradient path + digest
+    @torch.no_grad()
+    def finish_step(self, flat_grad: Optional[torch.Tensor], loss: Optional[torch.Tensor],
+                    host_metrics: Sequence[float], attack_truth: bool, stage_id: int) -> torch.Tensor:
+        """Run detection on this step's signals and fill the digest row (device)."""
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+        d = self.digest
+        d.zero_()
+        d[D_PRESENT] = 1.0
+        d[D_STAGE] = float(stage_id)
+        if loss is not None:
+            d[D_LOSS] = loss.detach().float().reshape(())
+        # ---- output anomaly
+        if self.output_detection and self._have_out:
+            res = self.out_det.observe(self.out_stats[:12])
+            d[D_OUT_FLAG] = res[0]
+            d[D_OUT_Z] = res[1]
+            d[D_OUT_CONF] = res[2]
+            mu, sd = self.out_stats[0:1], self.out_stats[1:2]
+            d[D_OUT_MEAN] = mu[0]
+            d[D_OUT_STD] = sd[0]
+            ready = (self.out_n >= self.warmup).float()
+            dev = torch.clamp((torch.abs(mu - self.out_mu) + torch.abs(sd - self.out_sd)) /
+                              (2.0 * torch.clamp(self.out_sd, min=1e-12)), max=1.0)
+            d[D_METRICS + 0] = (dev * ready)[0]
+            keep = 1.0 - res[0:1]  # do not fold flagged observations into the baseline
+            first = (self.out_n == 0).float()
+            b = self.beta * (1 - first) + 0.0 * first
+            self.out_mu.copy_(keep * (b * self.out_mu + (1 - b) * mu) + (1 - keep) * self.out_mu)
+            self.out_sd.copy_(keep * (b * self.out_sd + (1 - b) * sd) + (1 - keep) * self.out_sd)
+            self.out_n.add_(keep)
+            d[D_NONFINITE] += self.out_stats[12]
+        # ---- gradient verification
+        gflag = None
+        if self.grad_stats is not None and flat_grad is not None:
+            g = self.grad_stats.compute(flat_grad)
+            Sn = self.S
+            norms = g[18:18 + Sn]
+            d[D_GRAD_SUMSQ] = (norms * norms).sum()
+            d[D_GRAD_L2] = g[10]
+            d[D_GRAD_COS] = g[16]
+            d[D_NONFINITE] += g[17]
+            if self.gradient_verification:
+                res = self.grad_det.observe(g[:17])
+                gflag = res[0:1]
+                d[D_GRAD_FLAG] = res[0]
+                d[D_GRAD_Z] = res[1]
+                d[D_GRAD_CONF] = res[2]
+            ready = (self.norm_n >= self.warmup).float()
+            r = norms / torch.clamp(self.norm_ema[:Sn], min=1e-30)
+            if self.symmetric:
+                sc = torch.minimum(r, 1.0 / torch.clamp(r, min=1e-30))
+            else:
+                sc = torch.clamp(r, max=1.0)
+            valid = (self.norm_ema[:Sn] > 0).float()
+            cons = (sc * valid).sum() / torch.clamp(valid.sum(), min=1.0)
+            d[D_METRICS + 1] = ready[0] * cons + (1 - ready[0]) * 1.0
+            keep = 1.0 - (gflag if gflag is not None else torch.zeros(1, device=self.device))
+            first = (self.norm_n == 0).float()
+            b = self.beta * (1 - first)
+            self.norm_ema[:Sn].copy_(keep * (b * self.norm_ema[:Sn] + (1 - b) * norms) + (1 - keep) * self.norm_ema[:Sn])
+            self.norm_n.add_(keep)
+        else:
+            d[D_METRICS + 1] = 1.0
+        # ---- host-side runtime metrics (latency, utilization, error, uptime), one step lagged
+        hm = torch.tensor(list(host_metrics), dtype=torch.float32).pin_memory() \
+            if self.device.type == "cuda" else torch.tensor(list(host_metrics), dtype=torch.float32)
+        d[D_METRICS + 2:D_METRICS + 6].copy_(hm, non_blocking=True)
+        # error rate metric: any non-finite value this step counts as an error
+        d[D_METRICS + 4] = torch.clamp(d[D_METRICS + 4] + (d[D_NONFINITE] > 0).float(), max=1.0)
+        d[D_ATTACK_TRUTH] = 1.0 if attack_truth else 0.0
+        # ---- optimizer control block: quarantine flagged gradients on device
+        if self.quarantine and gflag is not None:
+            self.ctrl[1:2].copy_(torch.maximum(gflag, (d[D_NONFINITE:D_NONFINITE + 1] > 0).float()))
+        else:
+            self.ctrl[1] = 0.0
+        self._have_out = False
+        return d
+
+    def set_clip_scale(self, total_sumsq: torch.Tensor, max_norm: float):
+        """ctrl[0] = min(1, max_norm / ||g||_global) from the all-gathered per-stage sumsq (device)."""
+        if max_norm and max_norm > 0:
+            tot = torch.sqrt(torch.clamp(total_sumsq, min=0.0))
+            self.ctrl[0:1].copy_(torch.clamp(max_norm / (tot + 1e-6), max=1.0).reshape(1))
+        else:
+            self.ctrl[0] = 1.0
+
+    def state_dict(self):
+        return {k: v.detach().cpu() for k, v in {
+            "out_ring": self.out_det.ring, "out_state": self.out_det.state,
+            "grad_ring": self.grad_det.ring, "grad_state": self.grad_det.state,
+            "out_mu": self.out_mu, "out_sd": self.out_sd, "out_n": self.out_n,
+            "norm_ema": self.norm_ema, "norm_n": self.norm_n}.items()}
+
+    def load_state_dict(self, sd):
+        for k, t in (("out_ring", self.out_det.ring), ("out_state", self.out_det.state),
+                     ("grad_ring", self.grad_det.ring), ("grad_state", self.grad_det.state),
+                     ("out_mu", self.out_mu), ("out_sd", self.out_sd), ("out_n", self.out_n),
+                     ("norm_ema", self.norm_ema), ("norm_n", self.norm_n)):
+            if k in sd and sd[k].shape == t.shape:
+                t.copy_(sd[k])
