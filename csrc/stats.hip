@@ -360,11 +360,32 @@ TDL_API int tdl_grad_stats(const float* g, float* ref, const int64_t* table, int
 // ------------------------------------------------------------------ K4 z-score detection
 // ring: f32 [H][K] history; state: int32 [4] = (count, head, quarantine_run, seen)
 // cur: f32 [K]; out: f32 [4 + K] = (flag, mean_z, confidence, n_valid, z_0..z_{K-1}; z = -1 if skipped)
+// Exact order statistic of v[0..n) (n <= 128, one wave): value of rank `r` (0-based).
+__device__ float wave_select(const float* v, int n, int r, int lane) {
+    float found = 0.f;
+    for (int i = lane; i < n; i += 64) {
+        const float vi = v[i];
+        int lt = 0, eq_before = 0;
+        for (int j = 0; j < n; ++j) {
+            const float vj = v[j];
+            lt += vj < vi;
+            eq_before += (vj == vi) && (j < i);
+        }
+        if (lt + eq_before == r) found = vi;
+    }
+    // exactly one lane holds rank r; others hold 0 -> take the sum
+    return wave_sum(found);
+}
+
+// robust = 1: baseline over the `window` most recent entries, center = median, scale = 1.4826 * MAD
+//             (robust to the drift of real training and to earlier attacked samples);
+// robust = 0: reference mean / population std over the whole history window.
 __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, int* __restrict__ state,
                                                      const float* __restrict__ cur, int K, int H, int warmup,
-                                                     float z_decision, int exclude_current, int max_quarantine,
-                                                     float* __restrict__ out) {
+                                                     float z_decision, int window, int exclude_current,
+                                                     int max_quarantine, int robust, float* __restrict__ out) {
     __shared__ float zs[64];
+    __shared__ float col[4][128];
     __shared__ int cnt_sh;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int count = state[0], head = state[1];
@@ -376,21 +397,43 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
         count = count < H ? count + 1 : H;
     }
     const bool ready = count >= warmup;
+    const int wn = robust ? (count < window ? count : window) : count;
     for (int k = wid; k < K; k += 4) {
-        float s = 0.f;
-        for (int h = lane; h < count; h += 64) s += ring[(size_t)h * K + k];
-        const float mean = wave_sum(s) / (count > 0 ? count : 1);
-        float q = 0.f;
-        for (int h = lane; h < count; h += 64) {
-            const float d = ring[(size_t)h * K + k] - mean;
-            q += d * d;
+        float center, scale;
+        if (robust) {
+            float* v = col[wid];
+            for (int j = lane; j < wn; j += 64) {
+                const int idx = ((head - 1 - j) % H + H) % H;  // most recent first
+                v[j] = ring[(size_t)idx * K + k];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const float med = (wn & 1) ? wave_select(v, wn, wn / 2, lane)
+                                       : 0.5f * (wave_select(v, wn, wn / 2 - 1, lane) + wave_select(v, wn, wn / 2, lane));
+            __builtin_amdgcn_wave_barrier();
+            for (int j = lane; j < wn; j += 64) v[j] = fabsf(v[j] - med);
+            __builtin_amdgcn_wave_barrier();
+            const float mad = (wn & 1) ? wave_select(v, wn, wn / 2, lane)
+                                       : 0.5f * (wave_select(v, wn, wn / 2 - 1, lane) + wave_select(v, wn, wn / 2, lane));
+            __builtin_amdgcn_wave_barrier();
+            center = med;
+            scale = 1.4826f * mad;
+        } else {
+            float s = 0.f;
+            for (int h = lane; h < count; h += 64) s += ring[(size_t)h * K + k];
+            const float mean = wave_sum(s) / (count > 0 ? count : 1);
+            float q = 0.f;
+            for (int h = lane; h < count; h += 64) {
+                const float d = ring[(size_t)h * K + k] - mean;
+                q += d * d;
+            }
+            center = mean;
+            scale = sqrtf(wave_sum(q) / (count > 0 ? count : 1));
         }
-        const float sd = sqrtf(wave_sum(q) / (count > 0 ? count : 1));
         if (lane == 0) {
             float z = -1.f;
-            if (ready && sd > 0.f) {
+            if (ready && scale > 0.f) {
                 const float c = cur[k];
-                z = isfinite(c) ? fabsf((c - mean) / sd) : 1e6f;
+                z = isfinite(c) ? fabsf((c - center) / scale) : 1e6f;
             }
             zs[k] = z;
         }
@@ -433,9 +476,11 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
 }
 
 TDL_API int tdl_zscore_detect(float* ring, int* state, const float* cur, int K, int H, int warmup, float z_decision,
-                              float unused, int exclude_current, int max_quarantine, float* out, hipStream_t s) {
-    (void)unused;
-    zscore_kernel<<<1, 256, 0, s>>>(ring, state, cur, K, H, warmup, z_decision, exclude_current, max_quarantine, out);
+                              int window, int exclude_current, int max_quarantine, int robust, float* out,
+                              hipStream_t s) {
+    if (K > 64 || (robust && window > 128)) return (int)hipErrorInvalidValue;
+    zscore_kernel<<<1, 256, 0, s>>>(ring, state, cur, K, H, warmup, z_decision, window, exclude_current,
+                                    max_quarantine, robust, out);
     TDL_LAUNCH_CHECK();
 }
 

@@ -1,0 +1,142 @@
+"""Local-simulation backend: partitioning, fault injection -> detection -> trust -> re-shard, checkpoints."""
+import os
+
+import pytest
+import torch
+
+from trustworthy_dl.attacks import AdversarialAttacker, AttackConfig
+from trustworthy_dl.core.trust_manager import NodeStatus, TrustManager
+from trustworthy_dl.models import get_model
+from trustworthy_dl.parallel.flat import AdamWConfig
+from trustworthy_dl.parallel.partition import balanced_partition, even_partition, make_plan, PlacementPlan
+from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+from trustworthy_dl.security.attack_detection import AttackDetector
+from trustworthy_dl.utils.metrics import MetricsCollector
+
+
+def test_partitioners_never_drop_layers():
+    for L, S in [(12, 8), (26, 8), (17, 2), (5, 5)]:
+        for parts in (even_partition(L, S), balanced_partition([1.0] * L, S)):
+            assert parts[0][0] == 0 and parts[-1][1] == L
+            assert all(a < b for a, b in parts)
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(S - 1))
+    # GPT-2-medium 8 stages: the LM head (~3.5 blocks) gets its own stage
+    m = get_model("gpt2-medium")
+    costs = m.layer_costs(1024)
+    parts = balanced_partition(costs, 8)
+    assert parts[-1] == (25, 26)
+    per = [sum(costs[a:b]) for a, b in parts]
+    assert max(per) / (sum(per) / 8) < 1.2
+
+
+def test_plan_encoding_roundtrip():
+    p = make_plan([1, 2, 3, 4, 5], [0, 2, 3], version=4)
+    q = PlacementPlan.from_list(p.to_list())
+    assert q.ranks == p.ranks and q.ranges == p.ranges and q.version == 4
+    assert q.owner_of_layer(4) == 3
+
+
+def _batches(n, bs=8, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    for _ in range(n):
+        ids = torch.randint(0, 500, (bs, 33), generator=g)
+        yield {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+
+
+def _engine(nodes=3, attacker=None, reassign=True, **kw):
+    m = get_model("gpt2-tiny", seq_len=32, seed=0, vocab_size=1024)
+    cfg = EngineConfig(num_nodes=nodes, micro_batches=2, seq_len=32, device="cpu",
+                       adamw=AdamWConfig(lr=1e-3), reassign=reassign, **kw)
+    return PipelineEngine(m, cfg, TrustManager(nodes), attacker=attacker, metrics=MetricsCollector(),
+                          detector=AttackDetector())
+
+
+def test_training_reduces_loss_and_trust_healthy():
+    eng = _engine(nodes=2)
+    first = None
+    for b in _batches(40):
+        eng.train_step(b)
+        if first is None and eng.last_loss is not None:
+            first = eng.last_loss
+    eng.flush()
+    assert eng.last_loss < first
+    assert all(eng.trust.get_node_status(i) == NodeStatus.TRUSTED for i in range(2))
+    assert not eng.attack_history
+    assert eng.reassignment_history == []
+
+
+def test_gradient_poisoning_detected_quarantined_and_resharded():
+    atk = AdversarialAttacker(AttackConfig(["gradient_poisoning"], target_nodes=[1], intensity=0.5, start_step=25))
+    atk.activate_attacks()
+    eng = _engine(nodes=3, attacker=atk)
+    plan0 = eng.plan.describe()
+    for b in _batches(40):
+        eng.train_step(b)
+    eng.flush()
+    det = [r for r in eng.attack_history if r["node_id"] == 1]
+    assert det and det[0]["step"] == 25 and det[0]["ground_truth"]
+    assert eng.reassignment_history and eng.reassignment_history[0]["from_nodes"] == [1]
+    assert 1 not in eng.plan.ranks and eng.plan.describe() != plan0
+    # every layer still placed, training continues with the remaining two nodes
+    assert eng.plan.ranges[0][0] == 0 and eng.plan.ranges[-1][1] == eng.num_layers
+    assert eng.trust.get_node_status(1) == NodeStatus.COMPROMISED
+    st = atk.get_attack_statistics()
+    assert st["tp"] >= 1 and st["fp"] == 0
+    assert all(eng.trust.get_node_status(i) == NodeStatus.TRUSTED for i in (0, 2))
+
+
+def test_byzantine_output_tamper_detected():
+    atk = AdversarialAttacker(AttackConfig(["byzantine"], target_nodes=[0], intensity=0.5, start_step=20))
+    atk.activate_attacks()
+    eng = _engine(nodes=2, attacker=atk, reassign=False)
+    for b in _batches(24):
+        eng.train_step(b)
+    eng.flush()
+    assert any(r["node_id"] == 0 and r["step"] >= 20 for r in eng.attack_history)
+
+
+def test_reshard_preserves_function_and_optimizer_state():
+    eng = _engine(nodes=3, reassign=False)
+    for b in _batches(5):
+        eng.train_step(b)
+    eng.flush()
+    batch = next(_batches(1, seed=99))
+    before = eng.eval_step(batch)
+    step_before = {n: st.flat.step_count for n, st in eng.stages.items()}
+    eng.reassign([2])
+    after = eng.eval_step(batch)
+    assert after == pytest.approx(before, rel=1e-5)
+    assert all(st.flat.step_count == list(step_before.values())[0] for st in eng.stages.values())
+    assert sorted(eng.stages) == [0, 1]
+    for b in _batches(3, seed=5):
+        eng.train_step(b)
+    assert eng.flush() is not None
+
+
+def test_trainer_facade_checkpoint_roundtrip(tmp_path):
+    from trustworthy_dl import DistributedTrainer
+    from trustworthy_dl.utils.checkpoint import consolidate
+    tr = DistributedTrainer(model_name="gpt2-tiny", num_nodes=2, trust_threshold=0.7, seq_len=32, micro_batches=2,
+                            batch_size=8, checkpoint_interval=0, checkpoint_dir=str(tmp_path), device="cpu",
+                            batches_per_epoch=4)
+    tr.train(dataset="openwebtext", epochs=2, trust_manager=TrustManager(initial_trust=0.9, decay_rate=0.1,
+                                                                        recovery_rate=0.05))
+    stats = tr.get_training_stats()
+    assert stats["global_step"] == 8 and stats["training_state"] == "completed"
+    path = tr.save_checkpoint()
+    assert os.path.basename(path) == "checkpoint_step_8.pt"
+    ck = consolidate(path)
+    for key in ("epoch", "global_step", "model_partitions", "optimizers", "trust_scores", "attack_history",
+                "reassignment_history"):
+        assert key in ck
+    assert set(ck["model_partitions"]) == {0, 1}
+    assert any(k.endswith("attn.c_attn.weight") for k in ck["model_partitions"][0])
+    batch = next(_batches(1, seed=3))
+    ref = tr.engine.eval_step(batch)
+    tr2 = DistributedTrainer(model_name="gpt2-tiny", num_nodes=2, seq_len=32, micro_batches=2, batch_size=8,
+                             checkpoint_dir=str(tmp_path), device="cpu")
+    tr2.create_model_partitions()
+    tr2.load_checkpoint(path)
+    assert tr2.global_step == 8
+    assert tr2.engine.eval_step(batch) == pytest.approx(ref, rel=1e-6)
+    assert tr2.trust_manager.get_trust_score(0) == pytest.approx(tr.trust_manager.get_trust_score(0))

@@ -137,10 +137,10 @@ def test_cross_entropy_padded_vocab():
     from trustworthy_dl.ops import cross_entropy
     M, V, ld = 64, 1000, 1024
     logits = torch.randn(M, ld, device=DEV).bfloat16().requires_grad_(True)
+    lr = logits.detach().float()[:, :V].clone().requires_grad_(True)  # before: backward reuses the buffer
     labels = torch.randint(0, V, (M,), device=DEV)
     loss = cross_entropy(logits, labels, V)
     loss.backward()
-    lr = logits.detach().float()[:, :V].requires_grad_(True)
     ref = torch.nn.functional.cross_entropy(lr, labels)
     ref.backward()
     assert abs(float(loss) - float(ref)) < 1e-2

@@ -1,0 +1,203 @@
+"""Adversary / fault injection: ``AttackConfig`` and ``AdversarialAttacker``.
+
+The reference imports these (experiment_runner.py:23, 91-97, 157-160, 187-188, 231, 285, 598;
+README.md:61) but never ships them.  Inferred API kept:
+``AttackConfig(attack_types, target_nodes, intensity, start_step)``; ``activate_attacks()``,
+``is_active()``, ``apply_attacks(batch, batch_idx)``, ``get_attack_statistics()``,
+``get_final_statistics()``, ``cleanup()``.
+
+Attacks act on *stages* through engine hooks, in place on device tensors via the Philox-seeded
+injection kernel (csrc/attack.hip), and every injection is logged as ground truth so detection
+precision / recall / F1 and time-to-detect are measured, not simulated (cf. the simulated curves
+of experiment_runner.py:439-451):
+
+* ``gradient_poisoning`` — the stage's accumulated gradient is scaled / noised / sign-flipped /
+  zeroed before verification (``gradient_mode``);
+* ``model_poisoning`` (param perturbation) — the stage's weights are multiplicatively perturbed;
+* ``byzantine`` — the stage's output activations are tampered before they are sent downstream;
+* ``data_poisoning`` — labels are flipped and inputs perturbed in the batch (consumed by stage 0).
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import time
+from collections import defaultdict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops.attack import AttackMode, inject_
+
+logger = logging.getLogger(__name__)
+
+ATTACK_TYPES = ("gradient_poisoning", "model_poisoning", "byzantine", "data_poisoning",
+                "backdoor", "adversarial_input")
+_GRAD_MODES = {"scale": AttackMode.SCALE, "noise": AttackMode.REL_NOISE, "sign_flip": AttackMode.SIGN_FLIP,
+               "zero": AttackMode.ZERO, "additive_noise": AttackMode.NOISE}
+
+
+@dataclass
+class AttackConfig:
+    attack_types: List[str] = field(default_factory=lambda: ["gradient_poisoning"])
+    target_nodes: List[int] = field(default_factory=lambda: [1])
+    intensity: float = 0.5
+    start_step: int = 0
+    end_step: Optional[int] = None
+    probability: float = 1.0            # per-step, per-target attack probability
+    gradient_mode: str = "scale"        # scale | noise | sign_flip | zero | additive_noise
+    gradient_scale: Optional[float] = None   # default 1 + 18 * intensity (0.5 -> x10)
+    param_noise: Optional[float] = None      # relative weight noise, default intensity
+    activation_noise: Optional[float] = None  # relative activation noise, default 4 * intensity
+    label_flip_fraction: Optional[float] = None  # default intensity
+    seed: int = 1234
+
+    def grad_factor(self) -> float:
+        return self.gradient_scale if self.gradient_scale is not None else 1.0 + 18.0 * self.intensity
+
+
+class AdversarialAttacker:
+    def __init__(self, config: AttackConfig):
+        for t in config.attack_types:
+            if t not in ATTACK_TYPES:
+                raise ValueError(f"unknown attack type {t!r}; choose from {ATTACK_TYPES}")
+        self.config = config
+        self.active = False
+        self.injections: List[Dict] = []          # ground-truth log
+        self.detections: Dict[int, List[int]] = defaultdict(list)
+        self.counts = defaultdict(int)
+        self.outcomes = defaultdict(int)          # tp/fp/fn/tn from the engine's detector
+        self.first_attack_step: Dict[int, int] = {}
+        self.first_detect_step: Dict[int, int] = {}
+        self.last_batch_truth: Dict[int, bool] = {}
+
+    # ---------------------------------------------------------------- activation
+    def activate_attacks(self):
+        self.active = True
+        logger.warning("Attacks activated: %s on nodes %s", self.config.attack_types, self.config.target_nodes)
+
+    def deactivate_attacks(self):
+        self.active = False
+
+    def is_active(self) -> bool:
+        return self.active
+
+    def _fires(self, kind: str, node: int, step: int) -> bool:
+        c = self.config
+        if not self.active or kind not in c.attack_types or node not in c.target_nodes:
+            return False
+        if step < c.start_step or (c.end_step is not None and step > c.end_step):
+            return False
+        if c.probability >= 1.0:
+            return True
+        h = hashlib.blake2b(f"{c.seed}:{kind}:{node}:{step}".encode(), digest_size=8).digest()
+        return int.from_bytes(h, "little") / 2.0 ** 64 < c.probability
+
+    def _log(self, kind: str, node: int, step: int, **info):
+        self.injections.append({"type": kind, "node": node, "step": step, "timestamp": time.time(), **info})
+        self.counts[kind] += 1
+        self.first_attack_step.setdefault(node, step)
+
+    def _seed(self, node: int, step: int) -> int:
+        return (self.config.seed * 1_000_003 + node * 7919 + step) & 0xFFFFFFFFFFFF
+
+    # ---------------------------------------------------------------- engine hooks
+    def on_gradients(self, node: int, flat_grad: torch.Tensor, step: int) -> bool:
+        if not self._fires("gradient_poisoning", node, step):
+            return False
+        c = self.config
+        mode = _GRAD_MODES[c.gradient_mode]
+        a = {AttackMode.SCALE: c.grad_factor(), AttackMode.REL_NOISE: 10.0 * c.intensity,
+             AttackMode.SIGN_FLIP: 1.0, AttackMode.ZERO: 0.0, AttackMode.NOISE: c.intensity}[mode]
+        if mode == AttackMode.NOISE:  # absolute noise scaled to the gradient's RMS
+            a = float(c.intensity * 10.0 * flat_grad.float().pow(2).mean().sqrt().item() + 1e-12)
+        inject_(flat_grad, mode, a, self._seed(node, step), 0)
+        self._log("gradient_poisoning", node, step, mode=c.gradient_mode, magnitude=a)
+        return True
+
+    def on_parameters(self, node: int, flat, step: int) -> bool:
+        if not self._fires("model_poisoning", node, step):
+            return False
+        a = self.config.param_noise if self.config.param_noise is not None else self.config.intensity
+        inject_(flat.master, AttackMode.REL_NOISE, a, self._seed(node, step), 0)
+        if flat.data is not flat.master:
+            flat.data.copy_(flat.master)
+        self._log("model_poisoning", node, step, magnitude=a)
+        return True
+
+    def on_output(self, node: int, y: torch.Tensor, step: int) -> Optional[torch.Tensor]:
+        if not self._fires("byzantine", node, step):
+            return None
+        a = self.config.activation_noise if self.config.activation_noise is not None else 4.0 * self.config.intensity
+        yt = y.detach()
+        if not yt.is_contiguous():
+            return None
+        # in place, before any consumer has read the activation (the producer saved none of it)
+        inject_(yt, AttackMode.REL_NOISE, a, self._seed(node, step), 0)
+        inject_(yt, AttackMode.SIGN_FLIP, 1.0)
+        self._log("byzantine", node, step, magnitude=a)
+        return y
+
+    def apply_attacks(self, batch: Dict[str, torch.Tensor], batch_idx: int) -> Dict[str, torch.Tensor]:
+        """Data poisoning on the batch (experiment_runner.py:187-188): label flipping + input noise.
+        The poisoned data is consumed by stage 0, which is the ground-truth target."""
+        self.last_batch_truth = {}
+        c = self.config
+        if not (self.active and "data_poisoning" in c.attack_types and batch_idx >= c.start_step
+                and (c.end_step is None or batch_idx <= c.end_step)):
+            return batch
+        if c.probability < 1.0:
+            h = hashlib.blake2b(f"{c.seed}:data:{batch_idx}".encode(), digest_size=8).digest()
+            if int.from_bytes(h, "little") / 2.0 ** 64 >= c.probability:
+                return batch
+        frac = self.config.label_flip_fraction if self.config.label_flip_fraction is not None else self.config.intensity
+        g = torch.Generator().manual_seed(self._seed(0, batch_idx))
+        out = dict(batch)
+        tgt = batch["target"].clone()
+        mask = torch.rand(tgt.shape, generator=g) < frac
+        hi = int(tgt.max()) + 1 if tgt.numel() else 1
+        tgt[mask] = torch.randint(0, max(hi, 2), (int(mask.sum()),), generator=g)
+        out["target"] = tgt
+        x = batch["input"]
+        if x.is_floating_point():
+            out["input"] = x + torch.randn(x.shape, generator=g) * (4.0 * frac) * x.std()
+        self._log("data_poisoning", 0, batch_idx, fraction=frac)
+        self.last_batch_truth[0] = True
+        return out
+
+    # ---------------------------------------------------------------- detection bookkeeping
+    def record_detection(self, node: int, step: int, detected: bool, truth: bool):
+        key = ("tp" if truth else "fp") if detected else ("fn" if truth else "tn")
+        self.outcomes[key] += 1
+        if detected:
+            self.detections[node].append(step)
+            if truth:
+                self.first_detect_step.setdefault(node, step)
+
+    def detection_metrics(self) -> Dict[str, float]:
+        tp, fp, fn, tn = (self.outcomes[k] for k in ("tp", "fp", "fn", "tn"))
+        p = tp / (tp + fp) if tp + fp else 0.0
+        r = tp / (tp + fn) if tp + fn else 0.0
+        ttd = {n: self.first_detect_step[n] - self.first_attack_step[n]
+               for n in self.first_detect_step if n in self.first_attack_step}
+        return {"tp": tp, "fp": fp, "fn": fn, "tn": tn, "precision": p, "recall": r,
+                "f1": 2 * p * r / (p + r) if p + r else 0.0,
+                "time_to_detect_steps": ttd,
+                "mean_time_to_detect_steps": float(np.mean(list(ttd.values()))) if ttd else None}
+
+    def get_attack_statistics(self) -> Dict:
+        return {"active": self.active, "total_injections": len(self.injections),
+                "by_type": dict(self.counts), "target_nodes": list(self.config.target_nodes),
+                **self.detection_metrics()}
+
+    def get_final_statistics(self) -> Dict:
+        s = self.get_attack_statistics()
+        s["config"] = {k: (list(v) if isinstance(v, list) else v) for k, v in self.config.__dict__.items()}
+        s["injections"] = self.injections[-1000:]
+        return s
+
+    def cleanup(self):
+        self.active = False
+        logger.info("AdversarialAttacker cleanup completed")

@@ -96,9 +96,31 @@ def layer_norm(x, weight, bias, eps: float = 1e-5):
 
 # ============================================================== Linear (HF Conv1D layout: weight [in, out])
 def _gemm_backend(t: torch.Tensor) -> str:
+    """GEMM route for GPU tensors: ``torch`` (default: torch.mm on the hipBLASLt build torch ships
+    with) or ``blaslt`` (direct binding, csrc/blaslt.hip; opt-in via TDL_GEMM=blaslt — it links the
+    system ROCm 7.2 hipBLASLt while torch loads its own copy under the same SONAME)."""
     if not t.is_cuda:
         return "cpu"
-    return os.environ.get("TDL_GEMM", "blaslt")
+    return os.environ.get("TDL_GEMM", "torch")
+
+
+_MM_F32_OK = None
+
+
+def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """param grad += a @ b, accumulating in fp32 into ``main_grad`` when present."""
+    global _MM_F32_OK
+    mg = getattr(param, "main_grad", None)
+    if mg is None or not a.is_cuda:
+        return _accumulate(param, a @ b)
+    if _MM_F32_OK is not False:
+        try:
+            mg.add_(torch.mm(a, b, out_dtype=torch.float32).view(mg.shape))
+            _MM_F32_OK = True
+            return None
+        except (RuntimeError, TypeError):
+            _MM_F32_OK = False
+    return _accumulate(param, torch.mm(a, b))
 
 
 class _Linear(torch.autograd.Function):
@@ -167,7 +189,7 @@ class _Linear(torch.autograd.Function):
             else:
                 gb = _accumulate(bias, dy2.float().sum(0)) if bias is not None else None
             dx = torch.mm(dy2, weight.t()) if ctx.needs_input_grad[0] else None
-            gw = _accumulate(weight, torch.mm(x2.t(), dy2))
+            gw = _wgrad_into(weight, x2.t(), dy2)
         if dx is not None:
             dx = dx.reshape(ctx.shape)
         return dx, gw, gb, None
@@ -353,7 +375,7 @@ class _LinearT(torch.autograd.Function):
             dx, gw = blaslt.linear_t_bwd(x2, weight, dy2, ctx.needs_input_grad[0])
         else:
             dx = (dy2 @ weight) if ctx.needs_input_grad[0] else None
-            gw = _accumulate(weight, dy2.t() @ x2)
+            gw = _wgrad_into(weight, dy2.t(), x2)
         return (dx.reshape(ctx.shape) if dx is not None else None), gw
 
 

@@ -157,12 +157,22 @@ def grad_stats(grads: Sequence[torch.Tensor], reference: Optional[Sequence[torch
     return vec
 
 
+def _lower_upper_median(x: torch.Tensor) -> torch.Tensor:
+    """Column medians with the kernel's convention (mean of the two middle values when even)."""
+    s, _ = torch.sort(x, dim=0)
+    n = s.shape[0]
+    return s[n // 2] if n % 2 else 0.5 * (s[n // 2 - 1] + s[n // 2])
+
+
 class DeviceZScore:
     """Device ring-buffer baseline + z-score decision for one monitored signal (K4)."""
 
     def __init__(self, k: int, device, history: int = 1000, warmup: int = 10, z_decision: float = 2.5,
-                 exclude_current: bool = True, max_quarantine: int = 50):
+                 exclude_current: bool = True, max_quarantine: int = 50, robust: bool = True, window: int = 100):
+        """``robust``: median / 1.4826*MAD over the ``window`` most recent entries (default);
+        otherwise the reference's mean / population std over the whole ``history``."""
         self.k, self.history, self.warmup = k, history, warmup
+        self.robust, self.window = bool(robust), int(min(window, 128))
         self.z_decision = z_decision
         self.exclude_current = exclude_current
         self.max_quarantine = max_quarantine
@@ -176,8 +186,8 @@ class DeviceZScore:
         cur = cur[: self.k].contiguous()
         if self.device.type == "cuda":
             _lib.call("tdl_zscore_detect", ptr(self.ring), ptr(self.state), ptr(cur), self.k, self.history,
-                      self.warmup, self.z_decision, 0.0, int(self.exclude_current), self.max_quarantine,
-                      ptr(self.out), stream_ptr(self.device))
+                      self.warmup, self.z_decision, self.window, int(self.exclude_current), self.max_quarantine,
+                      int(self.robust), ptr(self.out), stream_ptr(self.device))
         else:
             self._cpu(cur)
         return self.out
@@ -195,9 +205,16 @@ class DeviceZScore:
         ready = count >= self.warmup
         zs = torch.full((self.k,), -1.0)
         if count > 0:
-            hist = self.ring[:count]
-            mean = hist.mean(0)
-            sd = hist.std(0, unbiased=False)
+            if self.robust:
+                wn = min(count, self.window)
+                idx = [(head - 1 - j) % H for j in range(wn)]
+                hist = self.ring[idx]
+                mean = _lower_upper_median(hist)
+                sd = 1.4826 * _lower_upper_median((hist - mean).abs())
+            else:
+                hist = self.ring[:count]
+                mean = hist.mean(0)
+                sd = hist.std(0, unbiased=False)
             for j in range(self.k):
                 if ready and sd[j] > 0:
                     c = float(cur[j])

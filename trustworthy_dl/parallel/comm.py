@@ -64,9 +64,9 @@ class P2PComm:
 
 def all_gather_rows(vec: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """All-gather a fixed-size 1-D float tensor from every rank -> [world, K] (identical on all ranks)."""
-    out = torch.empty(world, vec.numel(), dtype=vec.dtype, device=vec.device)
-    dist.all_gather_into_tensor(out, vec.contiguous(), group=group)
-    return out
+    out = torch.empty(world * vec.numel(), dtype=vec.dtype, device=vec.device)
+    dist.all_gather_into_tensor(out, vec.contiguous().reshape(-1), group=group)
+    return out.view(world, vec.numel())
 
 
 def broadcast_ints(values: Optional[Sequence[int]], src: int, device, max_len: int = 256, group=None) -> List[int]:

@@ -62,6 +62,7 @@ class EngineConfig:
     max_reassignment_attempts: int = 3
     min_stages: int = 1
     output_check: str = "first"          # which micro-batch output is monitored: first|none
+    compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
     seed: int = 0
 
 
@@ -185,6 +186,7 @@ class PipelineEngine:
                                      dtype=torch.int32, device=dev)
         self.t_weights = torch.tensor(self.trust.weights_vector(), dtype=torch.float32, device=dev)
         self.t_recovery = torch.full((N,), self.trust.recovery_rate, dtype=torch.float32, device=dev)
+        self.t_flagrun = torch.zeros(N, dtype=torch.int32, device=dev)
 
     # ================================================================== helpers
     def my_stage(self) -> Optional[Stage]:
@@ -211,13 +213,13 @@ class PipelineEngine:
         self.global_step += 1
         self.trust.advance_step(self.global_step)
         t0 = time.perf_counter()
-        if self.attacker is not None:
-            batch = self.attacker.apply_attacks(batch, self.global_step) if hasattr(self.attacker, "apply_attacks") \
-                else batch
+        truth: Dict[int, bool] = {}
+        if self.attacker is not None and hasattr(self.attacker, "apply_attacks"):
+            batch = self.attacker.apply_attacks(batch, self.global_step)
+            truth.update(getattr(self.attacker, "last_batch_truth", {}) or {})
         M = self.cfg.micro_batches
         inputs = split_micro(batch["input"], M)
         targets = split_micro(batch["target"], M)
-        truth: Dict[int, bool] = {}
         if self.distributed:
             loss = self._run_1f1b(inputs, targets, truth)
         else:
@@ -381,8 +383,11 @@ class PipelineEngine:
             probe = sample_in.to(st.device)
         out_shape = None
         if s < S - 1:
+            was_training = st.module.training
+            st.module.eval()  # shape probe must not touch BatchNorm running statistics
             with torch.no_grad():
                 y, _ = st.forward(probe, None)
+            st.module.train(was_training)
             out_shape = y.shape
             hdr[0] = len(out_shape)
             hdr[1:1 + len(out_shape)] = torch.tensor(list(out_shape), dtype=torch.int64)
@@ -441,7 +446,10 @@ class PipelineEngine:
         total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
         present_nodes = list(self.plan.ranks)
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
-        flags = torch.maximum(D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG]).to(torch.int32)
+        raw = torch.maximum(D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG]).to(torch.int32)
+        # a single flag quarantines that step's update; k consecutive flags compromise the node
+        self.t_flagrun.copy_((self.t_flagrun + 1) * raw)
+        flags = (self.t_flagrun >= max(1, self.cfg.compromise_after)).to(torch.int32)
         metrics = D[:, SV.D_METRICS:SV.D_METRICS + 6].contiguous()
         if len(present_nodes) == N:
             dstats.trust_update(self.t_values, self.t_counts, self.t_status, metrics, self.t_weights,

@@ -34,8 +34,16 @@ DIGEST = 24
 class StageVerifier:
     def __init__(self, param_sizes: Sequence[int], device, *, history: int = 1000, warmup: int = 10,
                  z_decision: float = 2.5, exclude_current: bool = True, max_quarantine: int = 50,
-                 ema_beta: float = 0.95, symmetric_consistency: bool = True, quarantine: bool = True,
-                 output_detection: bool = True, gradient_verification: bool = True):
+                 ema_beta: float = 0.8, symmetric_consistency: bool = True, quarantine: bool = True,
+                 output_detection: bool = True, gradient_verification: bool = True,
+                 consistency_tolerance: float = 2.0, deviation_deadzone: float = 0.25,
+                 robust_baseline: bool = True, baseline_window: int = 100):
+        """``consistency_tolerance`` / ``deviation_deadzone`` make the trust metrics tolerate the
+        legitimate drift of training (gradient norms routinely move 2x within a few steps early in
+        training): a norm ratio r scores min(1, tol * min(r, 1/r)), an output deviation d scores
+        max(0, d - dz) / (1 - dz).  tol=1, dz=0 gives the reference formulas exactly."""
+        self.tol = float(consistency_tolerance)
+        self.deadzone = float(deviation_deadzone)
         self.device = torch.device(device)
         self.output_detection = output_detection
         self.gradient_verification = gradient_verification
@@ -44,7 +52,7 @@ class StageVerifier:
         self.beta = ema_beta
         self.warmup = warmup
         kw = dict(history=history, warmup=warmup, z_decision=z_decision, exclude_current=exclude_current,
-                  max_quarantine=max_quarantine)
+                  max_quarantine=max_quarantine, robust=robust_baseline, window=baseline_window)
         self.out_det = S.DeviceZScore(12, self.device, **kw)
         self.grad_det = S.DeviceZScore(17, self.device, **kw)
         self.grad_stats = S.FlatGradStats(param_sizes, self.device) if len(param_sizes) else None
@@ -100,6 +108,7 @@ class StageVerifier:
             ready = (self.out_n >= self.warmup).float()
             dev = torch.clamp((torch.abs(mu - self.out_mu) + torch.abs(sd - self.out_sd)) /
                               (2.0 * torch.clamp(self.out_sd, min=1e-12)), max=1.0)
+            dev = torch.clamp(dev - self.deadzone, min=0.0) / (1.0 - self.deadzone)
             d[D_METRICS + 0] = (dev * ready)[0]
             keep = 1.0 - res[0:1]  # do not fold flagged observations into the baseline
             first = (self.out_n == 0).float()
@@ -130,6 +139,7 @@ class StageVerifier:
                 sc = torch.minimum(r, 1.0 / torch.clamp(r, min=1e-30))
             else:
                 sc = torch.clamp(r, max=1.0)
+            sc = torch.clamp(sc * self.tol, max=1.0)
             valid = (self.norm_ema[:Sn] > 0).float()
             cons = (sc * valid).sum() / torch.clamp(valid.sum(), min=1.0)
             d[D_METRICS + 1] = ready[0] * cons + (1 - ready[0]) * 1.0
