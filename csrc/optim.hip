@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
             ((float4*)master)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
             ((float4*)m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
             ((float4*)v)[i] = make_float4(va[0], va[1], va[2], va[3]);
-            ((uint2*)out)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+            if (out) ((uint2*)out)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
         }
         if (zero_grad) ((float4*)grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
             float p = master[i] * (1.f - lr * wd);
             p -= step_size * m[i] / (sqrtf(v[i]) * inv_sqrt_bc2 + eps);
             master[i] = p;
-            out[i] = f2bf(p);
+            if (out) out[i] = f2bf(p);
         }
         if (zero_grad) grad[i] = 0.f;
     }

@@ -12,9 +12,10 @@ for t in $ids; do
   timeout -k 10 ${TEST_TIMEOUT:-180} python -u -m pytest "$t" -x -q -s -p no:cacheprovider >> $LOG 2>&1
   rc=$?
   echo "rc=$rc" >> $LOG
+  if [ $rc -eq 1 ]; then FAILED="$FAILED $t"; continue; fi
   if [ $rc -ne 0 ]; then echo "STOP at $t rc=$rc"; tail -40 $LOG; exit $rc; fi
 done
-grep -c "^rc=0" $LOG
+grep -c "^rc=0" $LOG; echo "FAILED:$FAILED"
 if [ -n "$SKIP_BENCH" ]; then exit 0; fi
 timeout -k 10 420 python -u bench.py --steps ${BENCH_STEPS:-5} --warmup 2 ${BENCH_ARGS} > gpurun_out/bench1.log 2>&1
 rc2=$?

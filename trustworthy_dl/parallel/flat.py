@@ -105,7 +105,8 @@ class FlatParams:
                 if n <= 0:
                     continue
                 _lib.call("tdl_adamw_flat", ptr(self.master[lo:]), ptr(self.exp_avg[lo:]), ptr(self.exp_avg_sq[lo:]),
-                          ptr(self.grad[lo:]), ptr(self.data[lo:]), n, cfg.lr, b1, b2, cfg.eps, wd, bc1, bc2,
+                          ptr(self.grad[lo:]), ptr(None if self.data is self.master else self.data[lo:]),
+                          n, cfg.lr, b1, b2, cfg.eps, wd, bc1, bc2,
                           ptr(ctrl), int(zero_grad), stream_ptr(self.device))
             return
         scale = 1.0 if ctrl is None else float(ctrl[0])
