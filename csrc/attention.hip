@@ -11,10 +11,12 @@
 //   the next MFMA's operand"); V^T fragments come from a row-major LDS tile via ds_read_b64_tr_b16
 //   (T10) in the matching permuted key order.  O^T keeps query on the lane, so the online-softmax
 //   rescale is a per-lane scalar multiply.
-// Backward (per workgroup: 128 keys = 4 waves x 32; query tiles of 32 staged in LDS):
-//   S and dP are computed with the KEY on the lane; their accumulators feed dV^T += dO^T.P and
-//   dK^T += Q^T.dS without leaving registers; only dS crosses LDS (for dQ = dS.K), and dQ is
-//   pre-summed over the 4 waves in LDS before one fp32 atomic per element per workgroup.
+// Backward = two atomic-free kernels (a first version that summed dQ with LDS + global fp32 atomics
+// ran at ~27 TFLOP/s, 47% of the step, rocprof):
+//   dK/dV: workgroup = 128 keys (key on the lane), double-buffered Q/dO tiles, S and dP
+//          accumulators feed dV^T += dO^T.P and dK^T += Q^T.dS without leaving registers;
+//   dQ:    workgroup = 128 queries (query on the lane, like the forward), S^T / dP^T recomputed,
+//          dQ^T += K^T.dS^T with dS^T as the B operand.  +2 recomputed products, zero atomics.
 #include "common.h"
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -190,18 +192,20 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
     delta[((size_t)b * H + hd) * T + t] = acc;
 }
 
+// ---------------------------------------------------------------------------- dK, dV (key-owned)
+// Workgroup = 128 keys (4 waves x 32, key on the MFMA lane); walks query tiles of 32 with a
+// double-buffered LDS pipeline: the next tile's Q / dO / lse / delta are loaded into registers
+// while the current tile computes, then written to the other buffer -> ONE barrier per tile.
+// Products per tile and wave: S = Q.K^T, dP = dO.V^T (row-read A, K/V fragments resident in
+// registers), dV^T += dO^T.P and dK^T += Q^T.dS (tr-read A, S/dP accumulators as B operands).
 template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
-                                                       const float* __restrict__ lse, const float* __restrict__ delta,
-                                                       float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int T, int H,
-                                                       float scale) {
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+                                                            const float* __restrict__ lse, const float* __restrict__ delta,
+                                                            bf16_t* __restrict__ dqkv, int T, int H, float scale) {
     constexpr int BK = 128, BQ = 32;
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[BK * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t dSs[4][32 * 32];
-    __shared__ float dQr[BQ * HD];
-    __shared__ float lse_s[BQ], delta_s[BQ];
+    __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
+    __shared__ float lse_s[2][BQ], delta_s[2][BQ];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
     const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
@@ -210,11 +214,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
     const bf16_t* kbase = qbase + H * HD;
     const bf16_t* vbase = qbase + 2 * H * HD;
     const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
-    const int kblk = blockIdx.x * BK;
-    const int k0 = kblk + 32 * w;
-    const int kj = k0 + r;
     const float* lse_row = lse + (size_t)bh * T;
     const float* delta_row = delta + (size_t)bh * T;
+    // heavy (long causal) key blocks first
+    const int kblk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * BK;
+    const int k0 = kblk + 32 * w;
+    const int kj = k0 + r;
 
     bf16x8_t kf[4], vf[4];
 #pragma unroll
@@ -222,46 +227,51 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
         kf[s] = as_bf16x8(*(const uint4*)(kbase + (size_t)kj * ldq + 16 * s + 8 * h));
         vf[s] = as_bf16x8(*(const uint4*)(vbase + (size_t)kj * ldq + 16 * s + 8 * h));
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-        *(uint4*)(Ks + row * HD + ch * 8) = *(const uint4*)(kbase + (size_t)(kblk + row) * ldq + ch * 8);
-    }
-    for (int e = tid; e < BQ * HD; e += 256) dQr[e] = 0.f;
-
     f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     const int q_start = CAUSAL ? kblk : 0;
+    const int srow = tid >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 tile per operand
 
+    // prologue: tile q_start -> buffer 0
+    *(uint4*)(Qs[0] + srow * HD + sch * 8) = *(const uint4*)(qbase + (size_t)(q_start + srow) * ldq + sch * 8);
+    *(uint4*)(dOs[0] + srow * HD + sch * 8) = *(const uint4*)(dobase + (size_t)(q_start + srow) * ldo + sch * 8);
+    if (tid < BQ) {
+        lse_s[0][tid] = lse_row[q_start + tid];
+        delta_s[0][tid] = delta_row[q_start + tid];
+    }
+    __syncthreads();
+
+    int buf = 0;
     for (int qt = q_start; qt < T; qt += BQ) {
-        {
-            const int row = tid >> 3, ch = tid & 7;  // 256 chunks = 32 rows x 8
-            *(uint4*)(Qs + row * HD + ch * 8) = *(const uint4*)(qbase + (size_t)(qt + row) * ldq + ch * 8);
-            *(uint4*)(dOs + row * HD + ch * 8) = *(const uint4*)(dobase + (size_t)(qt + row) * ldo + ch * 8);
+        const bool has_next = qt + BQ < T;
+        uint4 qn = make_uint4(0, 0, 0, 0), dn = make_uint4(0, 0, 0, 0);
+        float ln = 0.f, dln = 0.f;
+        if (has_next) {
+            qn = *(const uint4*)(qbase + (size_t)(qt + BQ + srow) * ldq + sch * 8);
+            dn = *(const uint4*)(dobase + (size_t)(qt + BQ + srow) * ldo + sch * 8);
             if (tid < BQ) {
-                lse_s[tid] = lse_row[qt + tid];
-                delta_s[tid] = delta_row[qt + tid];
+                ln = lse_row[qt + BQ + tid];
+                dln = delta_row[qt + BQ + tid];
             }
         }
-        __syncthreads();
-        const bool active = !CAUSAL || (qt + BQ - 1 >= k0);
-        if (active) {
+        const bf16_t* Qb = Qs[buf];
+        const bf16_t* dOb = dOs[buf];
+        if (!CAUSAL || qt + BQ - 1 >= k0) {
             f32x16 sacc = {}, dpacc = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qs + r * HD + 16 * s + 8 * h));
-                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOs + r * HD + 16 * s + 8 * h));
+                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qb + r * HD + 16 * s + 8 * h));
+                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOb + r * HD + 16 * s + 8 * h));
                 sacc = MFMA32(aq, kf[s], sacc);
                 dpacc = MFMA32(ad, vf[s], dpacc);
             }
-            // lane = key kj; reg i = query qt + ql(i)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                float p = __expf(sacc[i] * scale - lse_s[ql]);
+                float p = __expf(sacc[i] * scale - lse_s[buf][ql]);
                 if (CAUSAL && kj > qt + ql) p = 0.f;
                 sacc[i] = p;
-                dpacc[i] = p * (dpacc[i] - delta_s[ql]);
+                dpacc[i] = p * (dpacc[i] - delta_s[buf][ql]);
             }
             const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
             const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
@@ -270,53 +280,27 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
                 const int qr = 16 * s2 + 4 * h + tq;
                 const bf16x8_t pb = s2 == 0 ? pb0 : pb1;
                 const bf16x8_t dsb = s2 == 0 ? db0 : db1;
-                const bf16x8_t ado0 = tr_pair(dOs + qr * HD + tcol, dOs + (qr + 8) * HD + tcol);
-                const bf16x8_t ado1 = tr_pair(dOs + qr * HD + 32 + tcol, dOs + (qr + 8) * HD + 32 + tcol);
+                const bf16x8_t ado0 = tr_pair(dOb + qr * HD + tcol, dOb + (qr + 8) * HD + tcol);
+                const bf16x8_t ado1 = tr_pair(dOb + qr * HD + 32 + tcol, dOb + (qr + 8) * HD + 32 + tcol);
                 dv0 = MFMA32(ado0, pb, dv0);
                 dv1 = MFMA32(ado1, pb, dv1);
-                const bf16x8_t aq0 = tr_pair(Qs + qr * HD + tcol, Qs + (qr + 8) * HD + tcol);
-                const bf16x8_t aq1 = tr_pair(Qs + qr * HD + 32 + tcol, Qs + (qr + 8) * HD + 32 + tcol);
+                const bf16x8_t aq0 = tr_pair(Qb + qr * HD + tcol, Qb + (qr + 8) * HD + tcol);
+                const bf16x8_t aq1 = tr_pair(Qb + qr * HD + 32 + tcol, Qb + (qr + 8) * HD + 32 + tcol);
                 dk0 = MFMA32(aq0, dsb, dk0);
                 dk1 = MFMA32(aq1, dsb, dk1);
             }
-            bf16_t* dsw = dSs[w];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                dsw[ql * 32 + r] = f2bf(dpacc[i]);
+        }
+        if (has_next) {
+            *(uint4*)(Qs[buf ^ 1] + srow * HD + sch * 8) = qn;
+            *(uint4*)(dOs[buf ^ 1] + srow * HD + sch * 8) = dn;
+            if (tid < BQ) {
+                lse_s[buf ^ 1][tid] = ln;
+                delta_s[buf ^ 1][tid] = dln;
             }
         }
         __syncthreads();
-        if (active) {
-            f32x16 dq0 = {}, dq1 = {};
-            const bf16_t* dsw = dSs[w];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const bf16x8_t a = as_bf16x8(*(const uint4*)(dsw + r * 32 + 16 * s + 8 * h));
-                const int kr = 32 * w + 16 * s + 8 * h + tq;
-                const bf16x8_t b0 = tr_pair(Ks + kr * HD + tcol, Ks + (kr + 4) * HD + tcol);
-                const bf16x8_t b1 = tr_pair(Ks + kr * HD + 32 + tcol, Ks + (kr + 4) * HD + 32 + tcol);
-                dq0 = MFMA32(a, b0, dq0);
-                dq1 = MFMA32(a, b1, dq1);
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                atomicAdd(&dQr[ql * HD + r], dq0[i]);
-                atomicAdd(&dQr[ql * HD + 32 + r], dq1[i]);
-            }
-        }
-        __syncthreads();
-        for (int e = tid; e < BQ * HD; e += 256) {
-            const int ql = e >> 6, d = e & 63;
-            const float v = dQr[e];
-            if (v != 0.f) atomicAdd(dq_acc + (((size_t)b * T + qt + ql) * H + hd) * HD + d, v);
-            dQr[e] = 0.f;
-        }
-        // the staging writes of the next iteration are fenced by its __syncthreads before any read
-        __syncthreads();
+        buf ^= 1;
     }
-    // epilogue: lane = key kj; regs = d rows (i&3)+8(i>>2)+4h (+32 for tile 1)
     bf16_t* dkrow = dqkv + ((size_t)b * T + kj) * ldq + H * HD + hd * HD;
     bf16_t* dvrow = dkrow + H * HD;
 #pragma unroll
@@ -333,33 +317,125 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
     }
 }
 
-// dqkv[b,t,0,h,:] = bf16(dq_acc[b,t,h,:] * scale)
-__global__ __launch_bounds__(256) void attn_dq_finalize(const float* __restrict__ dq_acc, bf16_t* __restrict__ dqkv, int B,
-                                                        int T, int H, float scale) {
-    const size_t n4 = (size_t)B * T * H * HD / 4;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-        const float4 v = ((const float4*)dq_acc)[i];
-        const size_t e = i * 4;
-        const size_t bt = e / (H * HD), rem = e - bt * (H * HD);
-        float f[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
-        *(uint2*)(dqkv + bt * (3 * H * HD) + rem) = pack4(f);
+// ---------------------------------------------------------------------------- dQ (query-owned)
+// Mirrors the forward: workgroup = 128 queries (query on the lane), key tiles of 64 staged in LDS.
+// dP^T = V.dO^T and S^T = K.Q^T (row-read A), dS^T = P^T * (dP^T - delta) in registers, then
+// dQ^T += K^T.dS^T with K^T from the transposed read of a plain K image and dS^T as the B operand.
+// No atomics, no LDS round trip for dS.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          bf16_t* __restrict__ dqkv, int T, int H, float scale) {
+    constexpr int BM = 128, BN = 64;
+    __shared__ __attribute__((aligned(16))) bf16_t Kr[BN * HD];  // swizzled, row reads
+    __shared__ __attribute__((aligned(16))) bf16_t Kp[BN * HD];  // plain, transposed reads
+    __shared__ __attribute__((aligned(16))) bf16_t Vr[BN * HD];  // swizzled, row reads
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int ldq = 3 * H * HD, ldo = H * HD;
+    const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
+    const bf16_t* kbase = qbase + H * HD;
+    const bf16_t* vbase = qbase + 2 * H * HD;
+    const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
+    const int qblk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * BM;  // heavy blocks first
+    const int q0 = qblk + 32 * w;
+    const int qi = q0 + r;
+    const float lse_q = lse[(size_t)bh * T + qi] * 1.4426950408889634f;
+    const float dl_q = delta[(size_t)bh * T + qi];
+    const float sl2 = scale * 1.4426950408889634f;
+
+    bf16x8_t qf[4], df[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        qf[s] = as_bf16x8(*(const uint4*)(qbase + (size_t)qi * ldq + 16 * s + 8 * h));
+        df[s] = as_bf16x8(*(const uint4*)(dobase + (size_t)qi * ldo + 16 * s + 8 * h));
+    }
+    f32x16 dq0 = {}, dq1 = {};
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
+    int nkb = T / BN;
+    if (CAUSAL) {
+        const int lim = (qblk + BM + BN - 1) / BN;
+        nkb = lim < nkb ? lim : nkb;
+    }
+    for (int kb = 0; kb < nkb; ++kb) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+            const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
+            const uint4 kv = *(const uint4*)(kbase + goff);
+            const uint4 vv = *(const uint4*)(vbase + goff);
+            *(uint4*)(Kr + row * HD + ((ch ^ (row & 7)) * 8)) = kv;
+            *(uint4*)(Kp + row * HD + ch * 8) = kv;
+            *(uint4*)(Vr + row * HD + ((ch ^ (row & 7)) * 8)) = vv;
+        }
+        __syncthreads();
+        if (!CAUSAL || kb * BN <= q0 + 31) {
+            f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int r1 = 32 + r;
+                const int c0 = ((2 * s + h) ^ (r & 7)) * 8, c1 = ((2 * s + h) ^ (r1 & 7)) * 8;
+                const bf16x8_t ak0 = as_bf16x8(*(const uint4*)(Kr + r * HD + c0));
+                const bf16x8_t ak1 = as_bf16x8(*(const uint4*)(Kr + r1 * HD + c1));
+                const bf16x8_t av0 = as_bf16x8(*(const uint4*)(Vr + r * HD + c0));
+                const bf16x8_t av1 = as_bf16x8(*(const uint4*)(Vr + r1 * HD + c1));
+                s0 = MFMA32(ak0, qf[s], s0);
+                s1 = MFMA32(ak1, qf[s], s1);
+                p0 = MFMA32(av0, df[s], p0);
+                p1 = MFMA32(av1, df[s], p1);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
+                float e0 = exp2f(s0[i] * sl2 - lse_q), e1 = exp2f(s1[i] * sl2 - lse_q);
+                if (CAUSAL) {
+                    if (key0 > qi) e0 = 0.f;
+                    if (key0 + 32 > qi) e1 = 0.f;
+                }
+                s0[i] = e0 * (p0[i] - dl_q);  // dS^T
+                s1[i] = e1 * (p1[i] - dl_q);
+            }
+            const bf16x8_t d00 = cvt8(s0, 0), d01 = cvt8(s0, 8), d10 = cvt8(s1, 0), d11 = cvt8(s1, 8);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const bf16x8_t ds = t == 0 ? (s2 == 0 ? d00 : d01) : (s2 == 0 ? d10 : d11);
+                    const int kr = 32 * t + 16 * s2 + 4 * h + tq;
+                    const bf16x8_t a0 = tr_pair(Kp + kr * HD + tcol, Kp + (kr + 8) * HD + tcol);
+                    const bf16x8_t a1 = tr_pair(Kp + kr * HD + 32 + tcol, Kp + (kr + 8) * HD + 32 + tcol);
+                    dq0 = MFMA32(a0, ds, dq0);
+                    dq1 = MFMA32(a1, ds, dq1);
+                }
+        }
+        __syncthreads();
+    }
+    bf16_t* qrow = dqkv + ((size_t)b * T + qi) * ldq + hd * HD;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int d = 8 * g + 4 * h;
+        float a[4] = {dq0[4 * g] * scale, dq0[4 * g + 1] * scale, dq0[4 * g + 2] * scale, dq0[4 * g + 3] * scale};
+        *(uint2*)(qrow + d) = pack4(a);
+        float a2[4] = {dq1[4 * g] * scale, dq1[4 * g + 1] * scale, dq1[4 * g + 2] * scale, dq1[4 * g + 3] * scale};
+        *(uint2*)(qrow + 32 + d) = pack4(a2);
     }
 }
 
-TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* dq_acc,
+TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* unused,
                          float* delta, int B, int T, int H, int D, float scale, int causal, hipStream_t s) {
+    (void)unused;
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
-    hipMemsetAsync(dq_acc, 0, sizeof(float) * (size_t)B * T * H * HD, s);
     attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
     const dim3 grid(T / 128, B * H);
-    if (causal)
-        attn_bwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dq_acc,
-                                                   (bf16_t*)dqkv, T, H, scale);
-    else
-        attn_bwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (const bf16_t*)dout, lse, delta, dq_acc,
-                                                    (bf16_t*)dqkv, T, H, scale);
-    const size_t n4 = (size_t)B * T * H * HD / 4;
-    const int fg = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
-    attn_dq_finalize<<<fg, 256, 0, s>>>(dq_acc, (bf16_t*)dqkv, B, T, H, scale);
+    auto Q = (const bf16_t*)qkv;
+    auto dO = (const bf16_t*)dout;
+    auto dQKV = (bf16_t*)dqkv;
+    if (causal) {
+        attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+    } else {
+        attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+    }
     TDL_LAUNCH_CHECK();
 }

@@ -114,7 +114,7 @@ template <int VEC, int CH, int RPW>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                      const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
-                                                     float* __restrict__ dw_acc, float* __restrict__ db_acc, int M) {
+                                                     float* __restrict__ part, int M) {
     constexpr int N = 64 * VEC * CH;
     __shared__ float red[2][4][N];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -179,12 +179,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
             red[1][wid][col] = db[c][i];
         }
     __syncthreads();
+    // per-block partial sums with plain stores (the column sum over blocks runs in colsum_f32_kernel):
+    // hundreds of blocks atomically adding into the same N floats is the contended-atomic worst case
+    float* prow = part + (size_t)blockIdx.x * 2 * N;
     for (int col = threadIdx.x; col < N; col += 256) {
-        const float a = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
-        const float bb = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
-        atomicAdd(dw_acc + col, a);
-        atomicAdd(db_acc + col, bb);
+        prow[col] = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
+        prow[N + col] = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
     }
+}
+
+// acc[c] += sum_g part[g * ld + c]; grid (ceil(N/256), ceil(G/64)); <= ceil(G/64) atomics per column.
+__global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ part, int G, int N, int ld,
+                                                         float* __restrict__ acc) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= N) return;
+    const int g0 = blockIdx.y * 64, g1 = min(G, g0 + 64);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int g = g0;
+    for (; g + 4 <= g1; g += 4) {
+        s0 += part[(size_t)g * ld + col];
+        s1 += part[(size_t)(g + 1) * ld + col];
+        s2 += part[(size_t)(g + 2) * ld + col];
+        s3 += part[(size_t)(g + 3) * ld + col];
+    }
+    for (; g < g1; ++g) s0 += part[(size_t)g * ld + col];
+    const float s = (s0 + s1) + (s2 + s3);
+    if (gridDim.y == 1) acc[col] += s;
+    else atomicAdd(acc + col, s);
+}
+
+static inline void launch_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s) {
+    const dim3 grd((N + 255) / 256, (G + 63) / 64);
+    colsum_f32_kernel<<<grd, 256, 0, s>>>(part, G, N, ld, acc);
 }
 
 __global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
@@ -213,23 +239,31 @@ __global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__
 }
 
 TDL_API int tdl_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                              void* dx, float* dw_acc, float* db_acc, int M, int N, int unused, hipStream_t s) {
-    (void)unused;
+                              void* dx, float* dw_acc, float* db_acc, int M, int N, float* part, hipStream_t s) {
+    // part: workspace of tdl_layernorm_bwd_ws_floats(M, N) floats (per-block dgamma/dbeta partials)
     auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto DX = (bf16_t*)dx;
     constexpr int RPW = 2;
-    const dim3 blk(256), grd((M + 4 * RPW - 1) / (4 * RPW));
+    const int G = (M + 4 * RPW - 1) / (4 * RPW);
+    const dim3 blk(256), grd(G);
+    bool tiled = true;
     switch (N) {
-        case 256:  ln_bwd_kernel<4, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 512:  ln_bwd_kernel<8, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 768:  ln_bwd_kernel<4, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 1024: ln_bwd_kernel<8, 2, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 1280: ln_bwd_kernel<4, 5, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 1536: ln_bwd_kernel<8, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        case 2048: ln_bwd_kernel<8, 4, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M); break;
-        default: ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M, N); break;
+        case 256:  ln_bwd_kernel<4, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 512:  ln_bwd_kernel<8, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 768:  ln_bwd_kernel<4, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 1024: ln_bwd_kernel<8, 2, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 1280: ln_bwd_kernel<4, 5, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 1536: ln_bwd_kernel<8, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        case 2048: ln_bwd_kernel<8, 4, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
+        default: tiled = false; ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M, N); break;
+    }
+    if (tiled) {
+        launch_colsum_f32(part, G, N, 2 * N, dw_acc, s);
+        launch_colsum_f32(part + N, G, N, 2 * N, db_acc, s);
     }
     TDL_LAUNCH_CHECK();
 }
+
+TDL_API int64_t tdl_layernorm_bwd_ws_floats(int M, int N) { return (int64_t)2 * N * ((M + 7) / 8); }
 
 // ============================================================== bias + GELU(tanh)
 __device__ __forceinline__ float gelu_tanh(float u) {
@@ -272,7 +306,7 @@ TDL_API int tdl_bias_gelu_fwd(const void* x, const void* b, void* y, int M, int 
 template <int R>
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                             const bf16_t* __restrict__ b, bf16_t* __restrict__ dx,
-                                                            float* __restrict__ db_acc, int M, int N) {
+                                                            float* __restrict__ part, int M, int N) {
     const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
     if (col >= N) return;
     const int row0 = blockIdx.y * R;
@@ -280,34 +314,90 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const bf16_t* __rest
     if (b) unpack8(*(const uint4*)(b + col), bb);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    // issue every row's loads before any math: R x 32 B in flight per lane hides HBM latency
+    uint4 gq[R], xq[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = min(row0 + r, M - 1);
+        gq[r] = *(const uint4*)(dy + (size_t)row * N + col);
+        xq[r] = *(const uint4*)(x + (size_t)row * N + col);
+    }
+#pragma unroll
     for (int r = 0; r < R; ++r) {
         const int row = row0 + r;
         if (row >= M) break;
-        const size_t off = (size_t)row * N + col;
         float g[8], v[8];
-        unpack8(*(const uint4*)(dy + off), g);
-        unpack8(*(const uint4*)(x + off), v);
+        unpack8(gq[r], g);
+        unpack8(xq[r], v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float d = g[k] * gelu_tanh_grad(v[k] + bb[k]);
             v[k] = d;
             acc[k] += d;
         }
-        *(uint4*)(dx + off) = pack8(v);
+        *(uint4*)(dx + (size_t)row * N + col) = pack8(v);
     }
-    if (db_acc) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(db_acc + col + k, acc[k]);
+    if (part) {  // plain-stored per-row-block partial column sums
+        float4* p = (float4*)(part + (size_t)blockIdx.y * N + col);
+        p[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        p[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
     }
 }
 
 TDL_API int tdl_bias_gelu_bwd(const void* dy, const void* x, const void* b, void* dx, float* db_acc, int M, int N,
-                              int unused, hipStream_t s) {
-    (void)unused;
+                              float* part, hipStream_t s) {
+    // part: (ceil(M/16) * N) floats when db_acc is set
     constexpr int R = 16;
     const dim3 grd((N / 8 + 255) / 256, (M + R - 1) / R);
     bias_gelu_bwd_kernel<R><<<grd, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, (const bf16_t*)b, (bf16_t*)dx,
-                                                db_acc, M, N);
+                                                db_acc ? part : nullptr, M, N);
+    if (db_acc) launch_colsum_f32(part, (int)grd.y, N, N, db_acc, s);
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== bias gradient: acc[N] += sum_rows dy[M,N] (bf16)
+// Block = 4 waves; lane owns 8 consecutive columns of a 512-column tile; each wave sums a
+// 16-row strip with all loads issued up front, the 4 waves merge through LDS, then ONE fp32
+// atomic per column per block (replaces torch's .float() copy + reduce + add: 3 passes -> 1).
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ dy, float* __restrict__ acc_out,
+                                                          int M, int N) {
+    constexpr int RW = 16;
+    __shared__ float red[4][512];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = blockIdx.x * 512 + lane * 8;
+    const int row0 = blockIdx.y * (4 * RW) + w * RW;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (col < N) {
+        uint4 q[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int row = min(row0 + r, M - 1);
+            q[r] = *(const uint4*)(dy + (size_t)row * N + col);
+        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            if (row0 + r >= M) break;
+            float v[8];
+            unpack8(q[r], v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[w][lane * 8 + k] = acc[k];
+    __syncthreads();
+    for (int c = threadIdx.x; c < 512; c += 256) {
+        const int gc = blockIdx.x * 512 + c;
+        if (gc < N) acc_out[(size_t)blockIdx.y * N + gc] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    }
+}
+
+TDL_API int tdl_colsum_bf16(const void* dy, float* acc, int M, int N, float* part, hipStream_t s) {
+    // part: (ceil(M/64) * N) floats of per-block partials, then one short column-sum pass
+    if (N % 8) return (int)hipErrorInvalidValue;
+    const dim3 grd((N + 511) / 512, (M + 63) / 64);
+    colsum_bf16_kernel<<<grd, 256, 0, s>>>((const bf16_t*)dy, part, M, N);
+    launch_colsum_f32(part, (int)grd.y, N, N, acc, s);
     TDL_LAUNCH_CHECK();
 }
 

@@ -73,12 +73,14 @@ _P, _I, _L, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _SIGNATURES = {
     # norm_act.hip
     "tdl_layernorm_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
-    "tdl_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
+    "tdl_layernorm_bwd_ws_floats": [_I, _I],
     "tdl_bias_gelu_fwd": [_P, _P, _P, _I, _I, _P],
-    "tdl_bias_gelu_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_bias_gelu_bwd": [_P, _P, _P, _P, _P, _I, _I, _P, _P],
     "tdl_embedding_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "tdl_embedding_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "tdl_add_into_f32": [_P, _P, _L, _I, _P],
+    "tdl_colsum_bf16": [_P, _P, _I, _I, _P, _P],
     # xent.hip
     "tdl_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "tdl_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _F, _P],
@@ -106,7 +108,7 @@ def _declare(l: ctypes.CDLL):
         if fn is None:
             continue
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_int64 if name.endswith("_bytes") else ctypes.c_int
+        fn.restype = ctypes.c_int64 if name.endswith(("_bytes", "_floats")) else ctypes.c_int
 
 
 def call(name: str, *args):

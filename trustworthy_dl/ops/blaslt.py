@@ -128,8 +128,9 @@ def linear_bwd(x2: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], 
         dpre = torch.empty_like(pre)
         db_tmp = mg_b if mg_b is not None else (torch.zeros(N, dtype=torch.float32, device=dev)
                                                 if bias is not None else None)
-        _lib.call("tdl_bias_gelu_bwd", ptr(dy2), ptr(pre), None, ptr(dpre), ptr(db_tmp), M, N, 0,
-                  stream_ptr(dev))
+        from .layers import _scratch
+        _lib.call("tdl_bias_gelu_bwd", ptr(dy2), ptr(pre), None, ptr(dpre), ptr(db_tmp), M, N,
+                  ptr(_scratch(((M + 15) // 16) * N, dev)), stream_ptr(dev))
         dy2 = dpre
         bias_done = True
 

@@ -40,6 +40,11 @@ def _wants_main_grad(p: Optional[torch.Tensor]) -> bool:
     return p is not None and getattr(p, "main_grad", None) is not None
 
 
+def _scratch(n: int, device) -> torch.Tensor:
+    """fp32 workspace for per-block partial sums (stream-ordered caching allocator: free to reuse)."""
+    return torch.empty(max(n, 1), dtype=torch.float32, device=device)
+
+
 def _f32_acc(p: torch.Tensor) -> torch.Tensor:
     """fp32 buffer the kernels accumulate a param gradient into (main_grad or a fresh zero buffer)."""
     mg = getattr(p, "main_grad", None)
@@ -78,7 +83,8 @@ class _LayerNorm(torch.autograd.Function):
             dw = _f32_acc(weight)
             db = _f32_acc(bias)
             _lib.call("tdl_layernorm_bwd", ptr(dy2), ptr(x2), ptr(weight), ptr(mean), ptr(rstd), ptr(dx),
-                      ptr(dw), ptr(db), M, N, 0, stream_ptr(dy.device))
+                      ptr(dw), ptr(db), M, N, ptr(_scratch(2 * N * ((M + 7) // 8), dy.device)),
+                      stream_ptr(dy.device))
             gw = None if _wants_main_grad(weight) else dw.to(weight.dtype)
             gb = None if _wants_main_grad(bias) else db.to(bias.dtype)
             return dx.reshape(ctx.shape), gw, gb, None
@@ -105,14 +111,34 @@ def _gemm_backend(t: torch.Tensor) -> str:
 
 
 _MM_F32_OK = None
+_ADDMM_F32_OK = None
+
+
+def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
+    """bias grad = column sums of dy2 [M, N] (bf16), accumulated in fp32 by one native pass."""
+    if dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.shape[1] % 8 == 0:
+        acc = _f32_acc(bias)
+        M, N = dy2.shape
+        _lib.call("tdl_colsum_bf16", ptr(dy2), ptr(acc), M, N, ptr(_scratch(((M + 63) // 64) * N, dy2.device)),
+                  stream_ptr(dy2.device))
+        return None if _wants_main_grad(bias) else acc.to(bias.dtype)
+    return _accumulate(bias, dy2.float().sum(0))
 
 
 def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
     """param grad += a @ b, accumulating in fp32 into ``main_grad`` when present."""
-    global _MM_F32_OK
+    global _MM_F32_OK, _ADDMM_F32_OK
     mg = getattr(param, "main_grad", None)
     if mg is None or not a.is_cuda:
         return _accumulate(param, a @ b)
+    if _ADDMM_F32_OK is not False:
+        # beta=1 GEMM epilogue accumulating in place into the fp32 flat gradient (one pass)
+        try:
+            torch.ops.aten.addmm.dtype_out(mg, a, b, torch.float32, beta=1, alpha=1, out=mg)
+            _ADDMM_F32_OK = True
+            return None
+        except (RuntimeError, TypeError):
+            _ADDMM_F32_OK = False
     if _MM_F32_OK is not False:
         try:
             mg.add_(torch.mm(a, b, out_dtype=torch.float32).view(mg.shape))
@@ -183,11 +209,12 @@ class _Linear(torch.autograd.Function):
                 dpre = torch.empty_like(pre)
                 db = _f32_acc(bias)
                 _lib.call("tdl_bias_gelu_bwd", ptr(dy2), ptr(pre), ptr(bias), ptr(dpre), ptr(db),
-                          pre.shape[0], pre.shape[1], 0, stream_ptr(dy.device))
+                          pre.shape[0], pre.shape[1],
+                          ptr(_scratch(((pre.shape[0] + 15) // 16) * pre.shape[1], dy.device)), stream_ptr(dy.device))
                 dy2 = dpre
                 gb = None if _wants_main_grad(bias) else db.to(bias.dtype)
             else:
-                gb = _accumulate(bias, dy2.float().sum(0)) if bias is not None else None
+                gb = _bias_grad_into(bias, dy2) if bias is not None else None
             dx = torch.mm(dy2, weight.t()) if ctx.needs_input_grad[0] else None
             gw = _wgrad_into(weight, x2.t(), dy2)
         if dx is not None:
@@ -235,9 +262,8 @@ class _Attention(torch.autograd.Function):
         dout = dout.contiguous()
         if qkv.is_cuda:
             dqkv = torch.empty_like(qkv)
-            dq_acc = torch.empty(B, T, H, D, dtype=torch.float32, device=qkv.device)
             delta = torch.empty(B * H, T, dtype=torch.float32, device=qkv.device)
-            _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), ptr(dq_acc), ptr(delta),
+            _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), None, ptr(delta),
                       B, T, H, D, ctx.scale, int(ctx.causal), stream_ptr(qkv.device))
             return dqkv, None, None
         with torch.enable_grad():
