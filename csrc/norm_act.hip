@@ -188,28 +188,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
 }
 
-// acc[c] += sum_g part[g * ld + c]; grid (ceil(N/256), ceil(G/64)); <= ceil(G/64) atomics per column.
+// acc[c] += sum_g part[g * ld + c]; grid (ceil(N/256), ceil(G/CS)).  Each thread issues its CS
+// loads at once (latency, not bandwidth, bounds this pass) and adds with <= ceil(G/CS) atomics per column.
+constexpr int CS_ROWS = 16;
 __global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ part, int G, int N, int ld,
                                                          float* __restrict__ acc) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= N) return;
-    const int g0 = blockIdx.y * 64, g1 = min(G, g0 + 64);
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int g = g0;
-    for (; g + 4 <= g1; g += 4) {
-        s0 += part[(size_t)g * ld + col];
-        s1 += part[(size_t)(g + 1) * ld + col];
-        s2 += part[(size_t)(g + 2) * ld + col];
-        s3 += part[(size_t)(g + 3) * ld + col];
-    }
-    for (; g < g1; ++g) s0 += part[(size_t)g * ld + col];
-    const float s = (s0 + s1) + (s2 + s3);
-    if (gridDim.y == 1) acc[col] += s;
-    else atomicAdd(acc + col, s);
+    const int g0 = blockIdx.y * CS_ROWS;
+    float v[CS_ROWS];
+#pragma unroll
+    for (int i = 0; i < CS_ROWS; ++i) v[i] = (g0 + i < G) ? part[(size_t)(g0 + i) * ld + col] : 0.f;
+#pragma unroll
+    for (int w = CS_ROWS / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) v[i] += v[i + w];
+    if (gridDim.y == 1) acc[col] += v[0];
+    else atomicAdd(acc + col, v[0]);
 }
 
 static inline void launch_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s) {
-    const dim3 grd((N + 255) / 256, (G + 63) / 64);
+    const dim3 grd((N + 255) / 256, (G + CS_ROWS - 1) / CS_ROWS);
     colsum_f32_kernel<<<grd, 256, 0, s>>>(part, G, N, ld, acc);
 }
 
@@ -361,7 +360,7 @@ TDL_API int tdl_bias_gelu_bwd(const void* dy, const void* x, const void* b, void
 // atomic per column per block (replaces torch's .float() copy + reduce + add: 3 passes -> 1).
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ dy, float* __restrict__ acc_out,
                                                           int M, int N) {
-    constexpr int RW = 16;
+    constexpr int RW = 4;  // 16 rows per block: >= 512 blocks at M = 4096 even for N = 1024
     __shared__ float red[4][512];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int col = blockIdx.x * 512 + lane * 8;
@@ -393,9 +392,9 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restri
 }
 
 TDL_API int tdl_colsum_bf16(const void* dy, float* acc, int M, int N, float* part, hipStream_t s) {
-    // part: (ceil(M/64) * N) floats of per-block partials, then one short column-sum pass
+    // part: (ceil(M/16) * N) floats of per-block partials, then one short column-sum pass
     if (N % 8) return (int)hipErrorInvalidValue;
-    const dim3 grd((N + 511) / 512, (M + 63) / 64);
+    const dim3 grd((N + 511) / 512, (M + 15) / 16);
     colsum_bf16_kernel<<<grd, 256, 0, s>>>((const bf16_t*)dy, part, M, N);
     launch_colsum_f32(part, (int)grd.y, N, N, acc, s);
     TDL_LAUNCH_CHECK();

@@ -119,7 +119,7 @@ def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
     if dy2.is_cuda and dy2.dtype == torch.bfloat16 and dy2.shape[1] % 8 == 0:
         acc = _f32_acc(bias)
         M, N = dy2.shape
-        _lib.call("tdl_colsum_bf16", ptr(dy2), ptr(acc), M, N, ptr(_scratch(((M + 63) // 64) * N, dy2.device)),
+        _lib.call("tdl_colsum_bf16", ptr(dy2), ptr(acc), M, N, ptr(_scratch(((M + 15) // 16) * N, dy2.device)),
                   stream_ptr(dy2.device))
         return None if _wants_main_grad(bias) else acc.to(bias.dtype)
     return _accumulate(bias, dy2.float().sum(0))
