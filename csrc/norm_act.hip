@@ -7,6 +7,12 @@
 // bf16 weight-grad tensor and its separate accumulate kernel never exist.
 #include "common.h"
 
+template <int VEC, int CH>
+__device__ __forceinline__ void ln_vload(const bf16_t* p, float* v) {
+    if constexpr (VEC == 8) unpack8(*(const uint4*)p, v);
+    else unpack4(*(const uint2*)p, v);
+}
+
 // ============================================================== LayerNorm forward
 // One wave per row; every lane owns CH chunks of VEC contiguous columns
 // (N == 64 * VEC * CH), so the whole row lives in registers: two-pass mean/var, exact.
@@ -107,25 +113,135 @@ TDL_API int tdl_layernorm_fwd(const void* x, const void* w, const void* b, void*
     TDL_LAUNCH_CHECK();
 }
 
-// ============================================================== LayerNorm backward
-// 4 waves per block, each wave walks RPW rows; dgamma/dbeta are summed per lane over the
-// wave's rows, then across the 4 waves through LDS, then one fp32 atomic per column.
-template <int VEC, int CH, int RPW>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
-                                                     const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
-                                                     float* __restrict__ part, int M) {
+// ============================================================== residual add + bias + LayerNorm forward
+// Pre-LN block junction: y1 = x + z + bz (the residual stream after a projection whose GEMM ran
+// without bias), h = LN(y1), and optionally y1b = y1 + b2 (the next projection's bias pre-added,
+// so that projection's GEMM can accumulate onto y1b in place: y = y1b + f @ W).  LN statistics
+// are taken over the bf16-rounded y1 that is stored, i.e. exactly what LN backward re-reads.
+template <int VEC, int CH>
+__global__ __launch_bounds__(256) void add_bias_ln_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ z, const bf16_t* __restrict__ bz,
+    const bf16_t* __restrict__ b2, const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+    bf16_t* __restrict__ y1, bf16_t* __restrict__ y1b, bf16_t* __restrict__ h, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int M, float eps) {
     constexpr int N = 64 * VEC * CH;
-    __shared__ float red[2][4][N];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    float dw[CH][VEC], db[CH][VEC], wf[CH][VEC];
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const size_t off = (size_t)row * N;
+    float v[CH][VEC];
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
         const int col = (c * 64 + lane) * VEC;
-        if constexpr (VEC == 8) unpack8(*(const uint4*)(w + col), wf[c]);
-        else unpack4(*(const uint2*)(w + col), wf[c]);
+        float zv[VEC], bv[VEC];
+        ln_vload<VEC, CH>(x + off + col, v[c]);
+        ln_vload<VEC, CH>(z + off + col, zv);
+        ln_vload<VEC, CH>(bz + col, bv);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) v[c][i] = (v[c][i] + zv[i]) + bv[i];
+        if constexpr (VEC == 8) {
+            const uint4 q = pack8(v[c]);
+            *(uint4*)(y1 + off + col) = q;
+            unpack8(q, v[c]);
+        } else {
+            const uint2 q = pack4(v[c]);
+            *(uint2*)(y1 + off + col) = q;
+            unpack4(q, v[c]);
+        }
+        if (y1b) {
+            float o[VEC];
+            ln_vload<VEC, CH>(b2 + col, bv);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) o[i] = v[c][i] + bv[i];
+            if constexpr (VEC == 8) *(uint4*)(y1b + off + col) = pack8(o);
+            else *(uint2*)(y1b + off + col) = pack4(o);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) s += v[c][i];
+    const float mean = wave_sum(s) * (1.0f / N);
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+            const float d = v[c][i] - mean;
+            q += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(q) * (1.0f / N) + eps);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * VEC;
+        float wf[VEC], bf[VEC], o[VEC];
+        ln_vload<VEC, CH>(w + col, wf);
+        ln_vload<VEC, CH>(b + col, bf);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] = (v[c][i] - mean) * rstd * wf[i] + bf[i];
+        if constexpr (VEC == 8) *(uint4*)(h + off + col) = pack8(o);
+        else *(uint2*)(h + off + col) = pack4(o);
+    }
+    if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+    }
+}
+
+TDL_API int tdl_add_bias_ln_fwd(const void* x, const void* z, const void* bz, const void* b2, const void* w,
+                                const void* b, void* y1, void* y1b, void* h, float* mean, float* rstd, int M, int N,
+                                float eps, hipStream_t s) {
+    const dim3 blk(256), grd((M + 3) / 4);
+    auto X = (const bf16_t*)x; auto Z = (const bf16_t*)z; auto BZ = (const bf16_t*)bz; auto B2 = (const bf16_t*)b2;
+    auto W = (const bf16_t*)w; auto B = (const bf16_t*)b;
+    auto Y1 = (bf16_t*)y1; auto Y1B = (bf16_t*)y1b; auto H = (bf16_t*)h;
+    if (y1b && !b2) return (int)hipErrorInvalidValue;
+#define TDL_ABLN(V, C) add_bias_ln_fwd_kernel<V, C><<<grd, blk, 0, s>>>(X, Z, BZ, B2, W, B, Y1, Y1B, H, mean, rstd, M, eps)
+    switch (N) {
+        case 256:  TDL_ABLN(4, 1); break;
+        case 512:  TDL_ABLN(8, 1); break;
+        case 768:  TDL_ABLN(4, 3); break;
+        case 1024: TDL_ABLN(8, 2); break;
+        case 1280: TDL_ABLN(4, 5); break;
+        case 1536: TDL_ABLN(8, 3); break;
+        case 2048: TDL_ABLN(8, 4); break;
+        default: return (int)hipErrorInvalidValue;  // callers use the unfused path for other widths
+    }
+#undef TDL_ABLN
+    TDL_LAUNCH_CHECK();
+}
+
+// ============================================================== LayerNorm backward
+// 4 waves per block, each wave walks RPW rows; dgamma/dbeta are summed per lane over the
+// wave's rows, then across the 4 waves through LDS, then one fp32 atomic per column.
+//
+// Residual fusion (pre-LN transformer block, y = x + f(LN(x))): with ``dres`` non-null the kernel
+// writes dx = LN_bwd(dy) + dres, so the autograd "skip + branch" gradient add never runs.  With
+// SUMS it also emits per-block column partials of dres and of dx (the bias gradients of the two
+// projections that feed the residual stream), so those need no separate column-sum pass either.
+
+template <int VEC, int CH, int RPW, bool RES, bool SUMS>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                     const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+                                                     bf16_t* __restrict__ dx, float* __restrict__ part, int M) {
+    constexpr int N = 64 * VEC * CH;
+    constexpr int NS = SUMS ? 4 : 2;  // column partial sets: dgamma, dbeta [, sum dres, sum dx]
+    __shared__ float red[2][4][N];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float dw[CH][VEC], db[CH][VEC], wf[CH][VEC];
+    float sr[SUMS ? CH : 1][VEC], sx[SUMS ? CH : 1][VEC];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+        const int col = (c * 64 + lane) * VEC;
+        ln_vload<VEC, CH>(w + col, wf[c]);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) dw[c][i] = db[c][i] = 0.f;
+        if constexpr (SUMS) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) sr[c][i] = sx[c][i] = 0.f;
+        }
     }
     const int row0 = (blockIdx.x * 4 + wid) * RPW;
     for (int r = 0; r < RPW; ++r) {
@@ -158,6 +274,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                 s1 += g;
                 s2 += g * xh;
             }
+        float rv[CH][VEC];
+        if constexpr (RES) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c) ln_vload<VEC, CH>(dres + (size_t)row * N + (c * 64 + lane) * VEC, rv[c]);
+        }
         s1 = wave_sum(s1) * (1.0f / N);
         s2 = wave_sum(s2) * (1.0f / N);
 #pragma unroll
@@ -165,26 +286,52 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
             const int col = (c * 64 + lane) * VEC;
             float o[VEC];
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) o[i] = rs * (gv[c][i] - s1 - xv[c][i] * s2);
-            if constexpr (VEC == 8) *(uint4*)(dx + (size_t)row * N + col) = pack8(o);
-            else *(uint2*)(dx + (size_t)row * N + col) = pack4(o);
+            for (int i = 0; i < VEC; ++i) {
+                o[i] = rs * (gv[c][i] - s1 - xv[c][i] * s2);
+                if constexpr (RES) o[i] += rv[c][i];
+            }
+            if constexpr (VEC == 8) {
+                const uint4 q = pack8(o);
+                *(uint4*)(dx + (size_t)row * N + col) = q;
+                if constexpr (SUMS) unpack8(q, o);  // column sums of the bf16 values actually stored
+            } else {
+                const uint2 q = pack4(o);
+                *(uint2*)(dx + (size_t)row * N + col) = q;
+                if constexpr (SUMS) unpack4(q, o);
+            }
+            if constexpr (SUMS) {
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) {
+                    sr[c][i] += rv[c][i];
+                    sx[c][i] += o[i];
+                }
+            }
         }
     }
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-            const int col = (c * 64 + lane) * VEC + i;
-            red[0][wid][col] = dw[c][i];
-            red[1][wid][col] = db[c][i];
-        }
-    __syncthreads();
     // per-block partial sums with plain stores (the column sum over blocks runs in colsum_f32_kernel):
     // hundreds of blocks atomically adding into the same N floats is the contended-atomic worst case
-    float* prow = part + (size_t)blockIdx.x * 2 * N;
-    for (int col = threadIdx.x; col < N; col += 256) {
-        prow[col] = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
-        prow[N + col] = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
+    float* prow = part + (size_t)blockIdx.x * NS * N;
+#pragma unroll
+    for (int pass = 0; pass < NS / 2; ++pass) {
+        if (pass) __syncthreads();
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) {
+                const int col = (c * 64 + lane) * VEC + i;
+                if (pass == 0) {
+                    red[0][wid][col] = dw[c][i];
+                    red[1][wid][col] = db[c][i];
+                } else if constexpr (SUMS) {
+                    red[0][wid][col] = sr[c][i];
+                    red[1][wid][col] = sx[c][i];
+                }
+            }
+        __syncthreads();
+        for (int col = threadIdx.x; col < N; col += 256) {
+            prow[2 * pass * N + col] = red[0][0][col] + red[0][1][col] + red[0][2][col] + red[0][3][col];
+            prow[(2 * pass + 1) * N + col] = red[1][0][col] + red[1][1][col] + red[1][2][col] + red[1][3][col];
+        }
     }
 }
 
@@ -212,10 +359,33 @@ static inline void launch_colsum_f32(const float* part, int G, int N, int ld, fl
     colsum_f32_kernel<<<grd, 256, 0, s>>>(part, G, N, ld, acc);
 }
 
+// Several column-partial sets stored side by side in each partial row (set z at column offset z*N),
+// reduced into their own accumulators by one launch (grid.z = number of sets).
+struct AccPtrs { float* p[4]; };
+__global__ __launch_bounds__(256) void colsum_f32_multi_kernel(const float* __restrict__ part, int G, int N, int ld,
+                                                               AccPtrs accs) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    float* acc = accs.p[blockIdx.z];
+    if (col >= N || acc == nullptr) return;
+    const float* src = part + (size_t)blockIdx.z * N;
+    const int g0 = blockIdx.y * CS_ROWS;
+    float v[CS_ROWS];
+#pragma unroll
+    for (int i = 0; i < CS_ROWS; ++i) v[i] = (g0 + i < G) ? src[(size_t)(g0 + i) * ld + col] : 0.f;
+#pragma unroll
+    for (int w = CS_ROWS / 2; w > 0; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) v[i] += v[i + w];
+    if (gridDim.y == 1) acc[col] += v[0];
+    else atomicAdd(acc + col, v[0]);
+}
+
 __global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                       const bf16_t* __restrict__ w, const float* __restrict__ mean_in,
-                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ dx,
-                                                      float* __restrict__ dw_acc, float* __restrict__ db_acc, int M, int N) {
+                                                      const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+                                                      bf16_t* __restrict__ dx, float* __restrict__ dw_acc,
+                                                      float* __restrict__ db_acc, float* __restrict__ sres_acc,
+                                                      float* __restrict__ sdx_acc, int M, int N) {
     __shared__ float red[16];
     const int row = blockIdx.x;
     const float mu = mean_in[row], rs = rstd_in[row];
@@ -231,38 +401,66 @@ __global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__
     for (int i = threadIdx.x; i < N; i += 256) {
         const float xh = (bf2f(x[(size_t)row * N + i]) - mu) * rs;
         const float gy = bf2f(dy[(size_t)row * N + i]);
-        dx[(size_t)row * N + i] = f2bf(rs * (gy * bf2f(w[i]) - s1 - xh * s2));
+        const float r = dres ? bf2f(dres[(size_t)row * N + i]) : 0.f;
+        const bf16_t o = f2bf(rs * (gy * bf2f(w[i]) - s1 - xh * s2) + r);
+        dx[(size_t)row * N + i] = o;
         atomicAdd(dw_acc + i, gy * xh);
         atomicAdd(db_acc + i, gy);
+        if (sres_acc) atomicAdd(sres_acc + i, r);
+        if (sdx_acc) atomicAdd(sdx_acc + i, bf2f(o));
     }
 }
 
-TDL_API int tdl_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                              void* dx, float* dw_acc, float* db_acc, int M, int N, float* part, hipStream_t s) {
-    // part: workspace of tdl_layernorm_bwd_ws_floats(M, N) floats (per-block dgamma/dbeta partials)
-    auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto DX = (bf16_t*)dx;
+template <bool RES, bool SUMS>
+static void launch_ln_bwd(const bf16_t* DY, const bf16_t* X, const bf16_t* W, const float* mean, const float* rstd,
+                          const bf16_t* DR, bf16_t* DX, float* part, int M, int G, int N, bool& tiled, hipStream_t s) {
     constexpr int RPW = 2;
-    const int G = (M + 4 * RPW - 1) / (4 * RPW);
     const dim3 blk(256), grd(G);
-    bool tiled = true;
+    tiled = true;
     switch (N) {
-        case 256:  ln_bwd_kernel<4, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 512:  ln_bwd_kernel<8, 1, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 768:  ln_bwd_kernel<4, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 1024: ln_bwd_kernel<8, 2, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 1280: ln_bwd_kernel<4, 5, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 1536: ln_bwd_kernel<8, 3, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        case 2048: ln_bwd_kernel<8, 4, RPW><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DX, part, M); break;
-        default: tiled = false; ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DX, dw_acc, db_acc, M, N); break;
+        case 256:  ln_bwd_kernel<4, 1, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 512:  ln_bwd_kernel<8, 1, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 768:  ln_bwd_kernel<4, 3, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 1024: ln_bwd_kernel<8, 2, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 1280: ln_bwd_kernel<4, 5, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 1536: ln_bwd_kernel<8, 3, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        case 2048: ln_bwd_kernel<8, 4, RPW, RES, SUMS><<<grd, blk, 0, s>>>(DY, X, W, mean, rstd, DR, DX, part, M); break;
+        default: tiled = false; break;
     }
+}
+
+// dx = LN_bwd(dy) [+ dres]; dgamma/dbeta [+ colsum(dres), colsum(dx)] accumulated into fp32 buffers.
+// part: workspace of tdl_layernorm_bwd_ws_floats(M, N) floats (per-block column partials).
+TDL_API int tdl_layernorm_bwd_res(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                                  const void* dres, void* dx, float* dw_acc, float* db_acc, float* sres_acc,
+                                  float* sdx_acc, int M, int N, float* part, hipStream_t s) {
+    auto DY = (const bf16_t*)dy; auto X = (const bf16_t*)x; auto W = (const bf16_t*)w; auto DX = (bf16_t*)dx;
+    auto DR = (const bf16_t*)dres;
+    const bool sums = sres_acc != nullptr || sdx_acc != nullptr;
+    if (sums && !dres) return (int)hipErrorInvalidValue;
+    const int G = (M + 7) / 8;
+    bool tiled;
+    if (!dres) launch_ln_bwd<false, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+    else if (!sums) launch_ln_bwd<true, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+    else launch_ln_bwd<true, true>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
     if (tiled) {
-        launch_colsum_f32(part, G, N, 2 * N, dw_acc, s);
-        launch_colsum_f32(part + N, G, N, 2 * N, db_acc, s);
+        const int ns = sums ? 4 : 2;
+        AccPtrs a{{dw_acc, db_acc, sums ? sres_acc : nullptr, sums ? sdx_acc : nullptr}};
+        const dim3 grd((N + 255) / 256, (G + CS_ROWS - 1) / CS_ROWS, ns);
+        colsum_f32_multi_kernel<<<grd, 256, 0, s>>>(part, G, N, ns * N, a);
+    } else {
+        ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DR, DX, dw_acc, db_acc, sres_acc, sdx_acc, M, N);
     }
     TDL_LAUNCH_CHECK();
 }
 
-TDL_API int64_t tdl_layernorm_bwd_ws_floats(int M, int N) { return (int64_t)2 * N * ((M + 7) / 8); }
+TDL_API int tdl_layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                              void* dx, float* dw_acc, float* db_acc, int M, int N, float* part, hipStream_t s) {
+    return tdl_layernorm_bwd_res(dy, x, w, mean, rstd, nullptr, dx, dw_acc, db_acc, nullptr, nullptr, M, N, part, s);
+}
+
+// sized for the 4-set (residual + sums) variant
+TDL_API int64_t tdl_layernorm_bwd_ws_floats(int M, int N) { return (int64_t)4 * N * ((M + 7) / 8); }
 
 // ============================================================== bias + GELU(tanh)
 __device__ __forceinline__ float gelu_tanh(float u) {

@@ -43,6 +43,7 @@ class GPT2Config:
     layer_norm_epsilon: float = 1e-5
     initializer_range: float = 0.02
     pad_vocab_multiple: int = 64
+    fused_block: bool = True  # ops/block.py single-node block; False = op-by-op autograd
 
     @classmethod
     def from_size(cls, size: str = "small", **kw) -> "GPT2Config":
@@ -112,8 +113,11 @@ class GPT2Block(nn.Module):
         self.attn = GPT2Attention(cfg)
         self.ln_2 = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon)
         self.mlp = GPT2MLP(cfg)
+        self.fused = cfg.fused_block
 
     def forward(self, x):
+        if self.fused and ops.fused_block_enabled(x.shape[-1], x.device):
+            return ops.gpt2_block(x, self)  # one autograd node, residual adds fused (ops/block.py)
         x = x + self.attn(self.ln_1(x))
         return x + self.mlp(self.ln_2(x))
 

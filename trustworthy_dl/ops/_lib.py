@@ -75,6 +75,8 @@ _SIGNATURES = {
     "tdl_layernorm_fwd": [_P, _P, _P, _P, _P, _P, _I, _I, _F, _P],
     "tdl_layernorm_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
     "tdl_layernorm_bwd_ws_floats": [_I, _I],
+    "tdl_layernorm_bwd_res": [_P] * 11 + [_I, _I, _P, _P],
+    "tdl_add_bias_ln_fwd": [_P] * 11 + [_I, _I, _F, _P],
     "tdl_bias_gelu_fwd": [_P, _P, _P, _I, _I, _P],
     "tdl_bias_gelu_bwd": [_P, _P, _P, _P, _P, _I, _I, _P, _P],
     "tdl_embedding_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],

@@ -125,28 +125,37 @@ def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
     return _accumulate(bias, dy2.float().sum(0))
 
 
-def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
-    """param grad += a @ b, accumulating in fp32 into ``main_grad`` when present."""
+def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """acc (fp32, shape of a @ b) += a @ b in one GEMM pass where the torch build allows it."""
     global _MM_F32_OK, _ADDMM_F32_OK
-    mg = getattr(param, "main_grad", None)
-    if mg is None or not a.is_cuda:
-        return _accumulate(param, a @ b)
+    if not a.is_cuda:
+        acc.add_((a @ b).float().view(acc.shape))
+        return
     if _ADDMM_F32_OK is not False:
-        # beta=1 GEMM epilogue accumulating in place into the fp32 flat gradient (one pass)
+        # beta=1 GEMM epilogue accumulating in place into the fp32 buffer (one pass)
         try:
-            torch.ops.aten.addmm.dtype_out(mg, a, b, torch.float32, beta=1, alpha=1, out=mg)
+            torch.ops.aten.addmm.dtype_out(acc, a, b, torch.float32, beta=1, alpha=1, out=acc)
             _ADDMM_F32_OK = True
-            return None
+            return
         except (RuntimeError, TypeError):
             _ADDMM_F32_OK = False
     if _MM_F32_OK is not False:
         try:
-            mg.add_(torch.mm(a, b, out_dtype=torch.float32).view(mg.shape))
+            acc.add_(torch.mm(a, b, out_dtype=torch.float32).view(acc.shape))
             _MM_F32_OK = True
-            return None
+            return
         except (RuntimeError, TypeError):
             _MM_F32_OK = False
-    return _accumulate(param, torch.mm(a, b))
+    acc.add_(torch.mm(a, b).float().view(acc.shape))
+
+
+def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """param grad += a @ b, accumulating in fp32 into ``main_grad`` when present."""
+    mg = getattr(param, "main_grad", None)
+    if mg is None or not a.is_cuda:
+        return _accumulate(param, a @ b)
+    wgrad_acc(mg, a, b)
+    return None
 
 
 class _Linear(torch.autograd.Function):
@@ -227,28 +236,56 @@ def linear(x, weight, bias=None, act: Optional[str] = None):
 
 
 # ============================================================== causal self-attention on packed qkv
+def attn_fwd(qkv: torch.Tensor, n_head: int, causal: bool):
+    """qkv [B, T, 3*H*D] (contiguous) -> (out [B, T, H*D], lse [B*H, T] fp32, scale)."""
+    B, T, C3 = qkv.shape
+    D = C3 // (3 * n_head)
+    scale = 1.0 / math.sqrt(D)
+    if qkv.is_cuda:
+        if D != 64 or T % 128 != 0:
+            raise ValueError(f"native attention supports head_dim 64 and T % 128 == 0 (got D={D}, T={T})")
+        out = torch.empty(B, T, n_head * D, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(B * n_head, T, dtype=torch.float32, device=qkv.device)
+        _lib.call("tdl_attn_fwd", ptr(qkv), ptr(out), ptr(lse), None, B, T, n_head, D, scale, int(causal),
+                  stream_ptr(qkv.device))
+        return out, lse, scale
+    q, k, v = qkv.float().view(B, T, 3, n_head, D).permute(2, 0, 3, 1, 4)
+    att = (q @ k.transpose(-1, -2)) * scale
+    if causal:
+        att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1), float("-inf"))
+    lse = torch.logsumexp(att, -1).reshape(B * n_head, T)
+    out = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, n_head * D).to(qkv.dtype)
+    return out, lse, scale
+
+
+def attn_bwd(qkv, out, lse, dout, n_head: int, causal: bool, scale: float) -> torch.Tensor:
+    """Gradient w.r.t. the packed qkv (same layout as ``qkv``)."""
+    B, T, C3 = qkv.shape
+    H = n_head
+    D = C3 // (3 * H)
+    dout = dout.contiguous()
+    if qkv.is_cuda:
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(B * H, T, dtype=torch.float32, device=qkv.device)
+        _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), None, ptr(delta),
+                  B, T, H, D, scale, int(causal), stream_ptr(qkv.device))
+        return dqkv
+    with torch.enable_grad():
+        x = qkv.detach().float().requires_grad_(True)
+        q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+        att = (q @ k.transpose(-1, -2)) * scale
+        if causal:
+            att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1), float("-inf"))
+        o = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, H * D)
+        (g,) = torch.autograd.grad(o, x, dout.reshape(o.shape).float())
+    return g.to(qkv.dtype)
+
+
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, n_head, causal):
-        B, T, C3 = qkv.shape
-        D = C3 // (3 * n_head)
-        scale = 1.0 / math.sqrt(D)
         qkv = qkv.contiguous()
-        if qkv.is_cuda:
-            if D != 64 or T % 128 != 0:
-                raise ValueError(f"native attention supports head_dim 64 and T % 128 == 0 (got D={D}, T={T})")
-            out = torch.empty(B, T, n_head * D, dtype=qkv.dtype, device=qkv.device)
-            lse = torch.empty(B * n_head, T, dtype=torch.float32, device=qkv.device)
-            _lib.call("tdl_attn_fwd", ptr(qkv), ptr(out), ptr(lse), None, B, T, n_head, D, scale, int(causal),
-                      stream_ptr(qkv.device))
-        else:
-            q, k, v = qkv.float().view(B, T, 3, n_head, D).permute(2, 0, 3, 1, 4)
-            att = (q @ k.transpose(-1, -2)) * scale
-            if causal:
-                mask = torch.ones(T, T, dtype=torch.bool).triu(1)
-                att = att.masked_fill(mask, float("-inf"))
-            lse = torch.logsumexp(att, -1).reshape(B * n_head, T)
-            out = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, n_head * D).to(qkv.dtype)
+        out, lse, scale = attn_fwd(qkv, n_head, causal)
         ctx.save_for_backward(qkv, out, lse)
         ctx.n_head, ctx.causal, ctx.scale = n_head, causal, scale
         return out
@@ -256,25 +293,7 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        B, T, C3 = qkv.shape
-        H = ctx.n_head
-        D = C3 // (3 * H)
-        dout = dout.contiguous()
-        if qkv.is_cuda:
-            dqkv = torch.empty_like(qkv)
-            delta = torch.empty(B * H, T, dtype=torch.float32, device=qkv.device)
-            _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), None, ptr(delta),
-                      B, T, H, D, ctx.scale, int(ctx.causal), stream_ptr(qkv.device))
-            return dqkv, None, None
-        with torch.enable_grad():
-            x = qkv.detach().float().requires_grad_(True)
-            q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
-            att = (q @ k.transpose(-1, -2)) * ctx.scale
-            if ctx.causal:
-                att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1), float("-inf"))
-            o = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, H * D)
-            (g,) = torch.autograd.grad(o, x, dout.float())
-        return g.to(qkv.dtype), None, None
+        return attn_bwd(qkv, out, lse, dout, ctx.n_head, ctx.causal, ctx.scale), None, None
 
 
 def causal_attention(qkv: torch.Tensor, n_head: int, causal: bool = True) -> torch.Tensor:
