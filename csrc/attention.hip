@@ -47,19 +47,25 @@ __device__ __forceinline__ bf16x8_t cvt8(const f32x16& v, int base) {
 constexpr int HD = 64;
 
 // ============================================================================ forward
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Grid is (B*H, T/128) with the query block taken in REVERSE order of blockIdx.y: the dispatcher
+// walks x fastest, so every head's longest causal rows go out first (longest-processing-time-first
+// over the 256 CUs) instead of the short rows of head 0 followed by the long rows of head 0.
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                        float* __restrict__ lse, int T, int H, float scale_log2) {
     constexpr int BM = 128, BN = 64;
-    __shared__ __attribute__((aligned(16))) bf16_t Ks[BN * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t Vs[BN * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t Ks[2][BN * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t Vs[2][BN * HD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
     const bf16_t* vbase = qbase + 2 * H * HD;
-    const int q0 = blockIdx.x * BM + 32 * w;
+    const int qblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BM;
+    const int q0 = qblk + 32 * w;
     const int qi = q0 + r;
     const int qrow = qi < T ? qi : T - 1;
 
@@ -71,55 +77,79 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     float m = -1e30f, l = 0.f;
     int nkb = T / BN;
     if (CAUSAL) {
-        const int lim = (blockIdx.x * BM + BM + BN - 1) / BN;
+        const int lim = (qblk + BM + BN - 1) / BN;
         nkb = lim < nkb ? lim : nkb;
     }
     // tr-read lane geometry (16-lane groups): lane 4q+p supplies row q, cols 4p..4p+3
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
-
-    for (int kb = 0; kb < nkb; ++kb) {
+    // staging: 2 x 16 B of K and of V per thread per 64-key tile; the NEXT tile is loaded into
+    // registers while the current one computes (one barrier per tile, LDS double-buffered)
+    uint4 kreg[2], vreg[2];
+    auto gload = [&](int kb) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
             const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
-            const uint4 kv = *(const uint4*)(kbase + goff);
-            const uint4 vv = *(const uint4*)(vbase + goff);
-            *(uint4*)(Ks + row * HD + ((ch ^ (row & 7)) * 8)) = kv;
-            *(uint4*)(Vs + row * HD + ch * 8) = vv;
+            kreg[i] = *(const uint4*)(kbase + goff);
+            vreg[i] = *(const uint4*)(vbase + goff);
         }
-        __syncthreads();
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+            *(uint4*)(Ks[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = kreg[i];
+            *(uint4*)(Vs[buf] + row * HD + ch * 8) = vreg[i];
+        }
+    };
+    gload(0);
+    sstore(0);
+    __syncthreads();
+
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int buf = kb & 1;
+        const bool has_next = kb + 1 < nkb;
+        if (has_next) gload(kb + 1);
+        const bf16_t* K_ = Ks[buf];
+        const bf16_t* V_ = Vs[buf];
         const bool active = !CAUSAL || (kb * BN <= q0 + 31);
         if (active) {
             f32x16 s0 = {}, s1 = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int r1 = 32 + r;
-                const bf16x8_t a0 = as_bf16x8(*(const uint4*)(Ks + r * HD + (((2 * s + h) ^ (r & 7)) * 8)));
-                const bf16x8_t a1 = as_bf16x8(*(const uint4*)(Ks + r1 * HD + (((2 * s + h) ^ (r1 & 7)) * 8)));
+                const bf16x8_t a0 = as_bf16x8(*(const uint4*)(K_ + r * HD + (((2 * s + h) ^ (r & 7)) * 8)));
+                const bf16x8_t a1 = as_bf16x8(*(const uint4*)(K_ + r1 * HD + (((2 * s + h) ^ (r1 & 7)) * 8)));
                 s0 = MFMA32(a0, qf[s], s0);
                 s1 = MFMA32(a1, qf[s], s1);
             }
             float mx = -1e30f;
+            if (CAUSAL && kb * BN + BN - 1 > q0) {  // diagonal tile of this wave: mask keys > query
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
-                float v0 = s0[i] * scale_log2, v1 = s1[i] * scale_log2;
-                if (CAUSAL) {
-                    if (key0 > qi) v0 = -INFINITY;
-                    if (key0 + 32 > qi) v1 = -INFINITY;
+                for (int i = 0; i < 16; ++i) {
+                    const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const float v0 = key0 > qi ? -INFINITY : s0[i] * scale_log2;
+                    const float v1 = key0 + 32 > qi ? -INFINITY : s1[i] * scale_log2;
+                    s0[i] = v0;
+                    s1[i] = v1;
+                    mx = fmaxf(mx, fmaxf(v0, v1));
                 }
-                s0[i] = v0;
-                s1[i] = v1;
-                mx = fmaxf(mx, fmaxf(v0, v1));
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    s0[i] *= scale_log2;
+                    s1[i] *= scale_log2;
+                    mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+                }
             }
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
             const float mn = fmaxf(m, mx);
-            const float alpha = exp2f(m - mn);
+            const float alpha = fast_exp2(m - mn);
             float rs = 0.f;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                s0[i] = exp2f(s0[i] - mn);
-                s1[i] = exp2f(s1[i] - mn);
+                s0[i] = fast_exp2(s0[i] - mn);
+                s1[i] = fast_exp2(s1[i] - mn);
                 rs += s0[i] + s1[i];
             }
             rs += __shfl_xor(rs, 32, 64);
@@ -137,12 +167,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const bf16x8_t pf = t == 0 ? (s2 == 0 ? p00 : p01) : (s2 == 0 ? p10 : p11);
                     const int kr = 32 * t + 16 * s2 + 4 * h + tq;
-                    const bf16x8_t v0 = tr_pair(Vs + kr * HD + tcol, Vs + (kr + 8) * HD + tcol);
-                    const bf16x8_t v1 = tr_pair(Vs + kr * HD + 32 + tcol, Vs + (kr + 8) * HD + 32 + tcol);
+                    const bf16x8_t v0 = tr_pair(V_ + kr * HD + tcol, V_ + (kr + 8) * HD + tcol);
+                    const bf16x8_t v1 = tr_pair(V_ + kr * HD + 32 + tcol, V_ + (kr + 8) * HD + 32 + tcol);
                     o0 = MFMA32(v0, pf, o0);
                     o1 = MFMA32(v1, pf, o1);
                 }
         }
+        if (has_next) sstore(buf ^ 1);
         __syncthreads();
     }
     if (qi < T) {
@@ -164,7 +195,7 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
                          int causal, hipStream_t s) {
     (void)unused;
     if (D != HD || T % 64 != 0) return (int)hipErrorInvalidValue;
-    const dim3 grid((T + 127) / 128, B * H);
+    const dim3 grid(B * H, (T + 127) / 128);
     const float sl2 = scale * 1.4426950408889634f;
     if (causal) attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
     else attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
@@ -208,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     __shared__ float lse_s[2][BQ], delta_s[2][BQ];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD, ldo = H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
@@ -216,8 +247,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
     const float* lse_row = lse + (size_t)bh * T;
     const float* delta_row = delta + (size_t)bh * T;
-    // heavy (long causal) key blocks first
-    const int kblk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * BK;
+    // heavy (long causal) key blocks first, across all heads (grid (B*H, T/128), x fastest)
+    const int kblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BK;
     const int k0 = kblk + 32 * w;
     const int kj = k0 + r;
 
@@ -323,21 +354,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 // dQ^T += K^T.dS^T with K^T from the transposed read of a plain K image and dS^T as the B operand.
 // No atomics, no LDS round trip for dS.
 template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
                                                           bf16_t* __restrict__ dqkv, int T, int H, float scale) {
     constexpr int BM = 128, BN = 64;
-    __shared__ __attribute__((aligned(16))) bf16_t Kr[BN * HD];  // swizzled, row reads
-    __shared__ __attribute__((aligned(16))) bf16_t Kp[BN * HD];  // plain, transposed reads
-    __shared__ __attribute__((aligned(16))) bf16_t Vr[BN * HD];  // swizzled, row reads
+    __shared__ __attribute__((aligned(16))) bf16_t Kr[2][BN * HD];  // swizzled, row reads
+    __shared__ __attribute__((aligned(16))) bf16_t Kp[2][BN * HD];  // plain, transposed reads
+    __shared__ __attribute__((aligned(16))) bf16_t Vr[2][BN * HD];  // swizzled, row reads
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD, ldo = H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
     const bf16_t* vbase = qbase + 2 * H * HD;
     const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
-    const int qblk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * BM;  // heavy blocks first
+    const int qblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BM;  // heavy blocks first
     const int q0 = qblk + 32 * w;
     const int qi = q0 + r;
     const float lse_q = lse[(size_t)bh * T + qi] * 1.4426950408889634f;
@@ -357,43 +388,65 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
         const int lim = (qblk + BM + BN - 1) / BN;
         nkb = lim < nkb ? lim : nkb;
     }
-    for (int kb = 0; kb < nkb; ++kb) {
+    uint4 kreg[2], vreg[2];
+    auto gload = [&](int kb) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
             const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
-            const uint4 kv = *(const uint4*)(kbase + goff);
-            const uint4 vv = *(const uint4*)(vbase + goff);
-            *(uint4*)(Kr + row * HD + ((ch ^ (row & 7)) * 8)) = kv;
-            *(uint4*)(Kp + row * HD + ch * 8) = kv;
-            *(uint4*)(Vr + row * HD + ((ch ^ (row & 7)) * 8)) = vv;
+            kreg[i] = *(const uint4*)(kbase + goff);
+            vreg[i] = *(const uint4*)(vbase + goff);
         }
-        __syncthreads();
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+            *(uint4*)(Kr[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = kreg[i];
+            *(uint4*)(Kp[buf] + row * HD + ch * 8) = kreg[i];
+            *(uint4*)(Vr[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = vreg[i];
+        }
+    };
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int buf = kb & 1;
+        const bool has_next = kb + 1 < nkb;
+        if (has_next) gload(kb + 1);
+        const bf16_t* Kr_ = Kr[buf];
+        const bf16_t* Kp_ = Kp[buf];
+        const bf16_t* Vr_ = Vr[buf];
         if (!CAUSAL || kb * BN <= q0 + 31) {
             f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int r1 = 32 + r;
                 const int c0 = ((2 * s + h) ^ (r & 7)) * 8, c1 = ((2 * s + h) ^ (r1 & 7)) * 8;
-                const bf16x8_t ak0 = as_bf16x8(*(const uint4*)(Kr + r * HD + c0));
-                const bf16x8_t ak1 = as_bf16x8(*(const uint4*)(Kr + r1 * HD + c1));
-                const bf16x8_t av0 = as_bf16x8(*(const uint4*)(Vr + r * HD + c0));
-                const bf16x8_t av1 = as_bf16x8(*(const uint4*)(Vr + r1 * HD + c1));
+                const bf16x8_t ak0 = as_bf16x8(*(const uint4*)(Kr_ + r * HD + c0));
+                const bf16x8_t ak1 = as_bf16x8(*(const uint4*)(Kr_ + r1 * HD + c1));
+                const bf16x8_t av0 = as_bf16x8(*(const uint4*)(Vr_ + r * HD + c0));
+                const bf16x8_t av1 = as_bf16x8(*(const uint4*)(Vr_ + r1 * HD + c1));
                 s0 = MFMA32(ak0, qf[s], s0);
                 s1 = MFMA32(ak1, qf[s], s1);
                 p0 = MFMA32(av0, df[s], p0);
                 p1 = MFMA32(av1, df[s], p1);
             }
+            if (CAUSAL && kb * BN + BN - 1 > q0) {  // diagonal tile: mask keys > query
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
-                float e0 = exp2f(s0[i] * sl2 - lse_q), e1 = exp2f(s1[i] * sl2 - lse_q);
-                if (CAUSAL) {
-                    if (key0 > qi) e0 = 0.f;
-                    if (key0 + 32 > qi) e1 = 0.f;
+                for (int i = 0; i < 16; ++i) {
+                    const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const float e0 = key0 > qi ? 0.f : fast_exp2(s0[i] * sl2 - lse_q);
+                    const float e1 = key0 + 32 > qi ? 0.f : fast_exp2(s1[i] * sl2 - lse_q);
+                    s0[i] = e0 * (p0[i] - dl_q);  // dS^T
+                    s1[i] = e1 * (p1[i] - dl_q);
                 }
-                s0[i] = e0 * (p0[i] - dl_q);  // dS^T
-                s1[i] = e1 * (p1[i] - dl_q);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    s0[i] = fast_exp2(s0[i] * sl2 - lse_q) * (p0[i] - dl_q);
+                    s1[i] = fast_exp2(s1[i] * sl2 - lse_q) * (p1[i] - dl_q);
+                }
             }
             const bf16x8_t d00 = cvt8(s0, 0), d01 = cvt8(s0, 8), d10 = cvt8(s1, 0), d11 = cvt8(s1, 8);
 #pragma unroll
@@ -402,12 +455,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16_t* __restri
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const bf16x8_t ds = t == 0 ? (s2 == 0 ? d00 : d01) : (s2 == 0 ? d10 : d11);
                     const int kr = 32 * t + 16 * s2 + 4 * h + tq;
-                    const bf16x8_t a0 = tr_pair(Kp + kr * HD + tcol, Kp + (kr + 8) * HD + tcol);
-                    const bf16x8_t a1 = tr_pair(Kp + kr * HD + 32 + tcol, Kp + (kr + 8) * HD + 32 + tcol);
+                    const bf16x8_t a0 = tr_pair(Kp_ + kr * HD + tcol, Kp_ + (kr + 8) * HD + tcol);
+                    const bf16x8_t a1 = tr_pair(Kp_ + kr * HD + 32 + tcol, Kp_ + (kr + 8) * HD + 32 + tcol);
                     dq0 = MFMA32(a0, ds, dq0);
                     dq1 = MFMA32(a1, ds, dq1);
                 }
         }
+        if (has_next) sstore(buf ^ 1);
         __syncthreads();
     }
     bf16_t* qrow = dqkv + ((size_t)b * T + qi) * ldq + hd * HD;
@@ -426,7 +480,7 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     (void)unused;
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
     attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
-    const dim3 grid(T / 128, B * H);
+    const dim3 grid(B * H, T / 128);
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;
     auto dQKV = (bf16_t*)dqkv;
