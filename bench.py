@@ -31,6 +31,28 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# Measured single-GPU throughput of GPT-2-medium (k tokens/s, MI355X, r1 micro-batch sweep,
+# scripts/gpu_sweep_mbs.sh) per micro-batch size: larger micro-batches feed the GEMMs and the
+# attention kernels larger tiles.  Used only to choose the micro-batch size.
+_MBS_EFF = {4: 215.9, 8: 245.7, 16: 270.4, 32: 278.8}
+
+
+def choose_mbs(global_batch: int, stages: int) -> int:
+    """1F1B step time ~ (M + S - 1) micro-batch slots of mbs / eff(mbs) each (M = batch / mbs):
+    few big micro-batches run efficient kernels but leave a long fill/drain bubble."""
+    best, best_t = None, float("inf")
+    for mbs, eff in _MBS_EFF.items():
+        if global_batch % mbs:
+            continue
+        m = global_batch // mbs
+        if m < stages and stages > 1:
+            continue
+        t = (m + stages - 1) * mbs / eff
+        if t < best_t:
+            best, best_t = mbs, t
+    return best or 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -39,7 +61,8 @@ def main():
     ap.add_argument("--model", default="gpt2-medium")
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--batch-per-gpu", type=int, default=32)
-    ap.add_argument("--mbs", type=int, default=4, help="sequences per micro-batch")
+    ap.add_argument("--mbs", default="auto",
+                    help="sequences per micro-batch, or 'auto' (pipeline-bubble vs GEMM-efficiency model)")
     ap.add_argument("--no-verify", action="store_true", help="disable detection/verification (ablation)")
     ap.add_argument("--lr", type=float, default=5e-5)
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -66,7 +89,8 @@ def main():
 
     N = world
     global_batch = args.batch_per_gpu * N
-    M = global_batch // args.mbs
+    mbs = choose_mbs(global_batch, N) if args.mbs == "auto" else int(args.mbs)
+    M = global_batch // mbs
     model = get_model(args.model, seq_len=args.seq_len, seed=1234)
     verify = not args.no_verify
     cfg = EngineConfig(num_nodes=N, micro_batches=M, seq_len=args.seq_len,
@@ -114,7 +138,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic tokens, random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq_len,
-                       "micro_batch": args.mbs, "micro_batches": M, "parallelism": f"pp{N}",
+                       "micro_batch": mbs, "micro_batches": M, "parallelism": f"pp{N}",
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
                        "plan": engine.plan.describe(), "last_loss": engine.last_loss},
         }
