@@ -1,0 +1,492 @@
+// Implicit-GEMM convolutions for the VGG / ResNet blocks, NHWC bf16, fp32 accumulate,
+// gfx950 MFMA v_mfma_f32_32x32x16_bf16.  Replaces the MIOpen path the CNN stages used before.
+//
+// Layouts (torch channels_last == NHWC storage; weights [Cout][R][S][Cin] == KRSC, k = (r, s, c)
+// with c fastest).  Cin % 8 == 0 so one 16-byte vector is 8 channels of one tap (the Python side
+// pads the 3-channel stem input/weight to 8).
+//
+// conv_nt  — D[cout][m] = sum_k Wk[cout][k] * Act[m][k]   (both operands k-contiguous: "NT")
+//   forward : Act[m=(n,p,q)][k=(r,s,c)] = X [n][p*st-pad+r][q*st-pad+s][c]          (0 outside)
+//   dgrad   : Act[m=(n,h,w)][k=(r,s,k')] = dY[n][(h+pad-r)/st][(w+pad-s)/st][k']  (0 unless the
+//             division is exact and in range) with Wk = W permuted to [Cin][R][S][Cout]
+//   Workgroup tile BCO (cout: 64|128) x 128 (m), K step 64, 4 waves as 2 (cout) x 2 (m).  Both
+//   operands are register-staged (global -> VGPR prefetch of tile t+1 while tile t computes, then
+//   one LDS write + ONE barrier per K step), LDS rows of 128 B XOR-swizzled by (row>>1)&7 so the
+//   ds_read_b128 fragment reads of a 32-lane half hit 16 distinct 16-byte slots.  The weight tile
+//   is the MFMA A operand, so the accumulator has m on the lane and 4 consecutive output channels
+//   per register group: the epilogue writes 8-byte NHWC vectors.  Optional fused epilogue: per
+//   output-channel sum / sum-of-squares of the bf16-rounded outputs (BatchNorm batch statistics):
+//   one partial row per workgroup (registers -> shuffles -> LDS), summed by a small finalize pass
+//   (an earlier version issued per-wave same-address atomics: 4-8x slower forward, rocprof).
+// conv_wgrad — dW[cout][k] = sum_m dY[m][cout] * Act[m][k]   (reduction over output pixels)
+//   Both operands are m-major, so tiles are staged [32 m][cols] and read as MFMA fragments with
+//   the gfx950 transposing LDS read ds_read_b64_tr_b16 (rows padded to 320 B: conflict-free).
+//   Tile BCO x 128 (k), m step 32, split over m across grid.z; partial tiles are reduced into a
+//   [Cout][R][S][Cin] fp32 image (lane-contiguous atomics when split > 1) and added to the
+//   parameter's [Cout][Cin][R][S] gradient by one transpose pass (1x1: straight into it).
+#include "common.h"
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+
+namespace {
+
+__device__ __forceinline__ bf16x8_t as_bf16x8(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+
+__device__ __forceinline__ short4_t tr_read(const bf16_t* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
+}
+__device__ __forceinline__ bf16x8_t tr_pair(const bf16_t* p_lo, const bf16_t* p_hi) {
+    const short4_t a = tr_read(p_lo), b = tr_read(p_hi);
+    const short8_t c = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8_t, c);
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md T1): consecutive logical tiles land on the
+// same XCD (private L2), so the blocks that share an activation panel share its L2 lines.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+struct ConvDims {
+    int N, Hin, Win, Cin;   // gathered tensor (X for fwd/wgrad, dY for dgrad), NHWC
+    int P, Q, Cout;         // GEMM output: rows m = N*P*Q pixels, Cout channels (NHWC)
+    int R, S, stride, pad;  // filter geometry of the FORWARD convolution
+};
+
+constexpr int BM = 128;  // m (pixels) per workgroup
+constexpr int BK = 64;   // k per step
+
+// ============================================================================ conv_nt (fwd / dgrad)
+template <int BCO, bool TRANSPOSED, bool STATS>
+__global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restrict__ act, const bf16_t* __restrict__ wk,
+                                                         bf16_t* __restrict__ out, float* __restrict__ part,
+                                                         ConvDims d) {
+    constexpr int TCO = BCO / 64;   // 32-row cout tiles per wave (waves are 2 x 2)
+    constexpr int AROWS = BCO / 32; // weight rows staged per thread (BCO rows x 8 chunks / 256 threads)
+    __shared__ __attribute__((aligned(16))) bf16_t As[2][BCO * BK];
+    __shared__ __attribute__((aligned(16))) bf16_t Bs[2][BM * BK];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, lr = lane & 31;
+    const int wco = w >> 1, wm = w & 1;
+    const int M = d.N * d.P * d.Q;
+    const int K = d.R * d.S * d.Cin;
+    const int ntco = (d.Cout + BCO - 1) / BCO, ntm = (M + BM - 1) / BM;
+    const int wg = xcd_remap(blockIdx.x, ntco * ntm);
+    const int tco = wg % ntco, tm = wg / ntco;
+    const int co0 = tco * BCO, m0 = tm * BM;
+
+    // ---- per-thread staging geometry: rows srow + 32 i, 16-byte chunk sch of the 64-wide k step
+    const int srow = tid >> 3, sch = tid & 7;
+    const int PQ = d.P * d.Q;
+    int b_img[4], b_y[4], b_x[4];  // image offset, and spatial origin of each staged pixel row
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + srow + 32 * i;
+        if (m < M) {
+            const int n = m / PQ, pq = m - n * PQ, p = pq / d.Q, q = pq - p * d.Q;
+            b_img[i] = n;
+            b_y[i] = TRANSPOSED ? p + d.pad : p * d.stride - d.pad;
+            b_x[i] = TRANSPOSED ? q + d.pad : q * d.stride - d.pad;
+        } else {
+            b_img[i] = -1;
+            b_y[i] = b_x[i] = 0;
+        }
+    }
+    uint4 areg[AROWS], breg[4];
+    auto gload = [&](int k0) {
+        const int kk = k0 + 8 * sch;
+        const bool kin = kk < K;
+        int c = 0, r = 0, s = 0;
+        if (kin) {
+            const int rs = kk / d.Cin;
+            c = kk - rs * d.Cin;
+            r = rs / d.S;
+            s = rs - r * d.S;
+        }
+#pragma unroll
+        for (int i = 0; i < AROWS; ++i) {
+            const int co = co0 + srow + 32 * i;
+            areg[i] = (kin && co < d.Cout) ? *(const uint4*)(wk + (size_t)co * K + kk) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (kin && b_img[i] >= 0) {
+                int y, x;
+                bool ok;
+                if (TRANSPOSED) {
+                    const int ty = b_y[i] - r, tx = b_x[i] - s;
+                    y = ty / d.stride;
+                    x = tx / d.stride;
+                    ok = ty >= 0 && tx >= 0 && y * d.stride == ty && x * d.stride == tx && y < d.Hin && x < d.Win;
+                } else {
+                    y = b_y[i] + r;
+                    x = b_x[i] + s;
+                    ok = (unsigned)y < (unsigned)d.Hin && (unsigned)x < (unsigned)d.Win;
+                }
+                if (ok) v = *(const uint4*)(act + (((size_t)b_img[i] * d.Hin + y) * d.Win + x) * d.Cin + c);
+            }
+            breg[i] = v;
+        }
+    };
+    // LDS image: 64 bf16 (8 x 16-byte chunks) per row, chunk XOR-swizzled by (row >> 1) & 7
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AROWS; ++i) {
+            const int row = srow + 32 * i;
+            *(uint4*)(As[buf] + row * BK + ((sch ^ ((row >> 1) & 7)) << 3)) = areg[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = srow + 32 * i;
+            *(uint4*)(Bs[buf] + row * BK + ((sch ^ ((row >> 1) & 7)) << 3)) = breg[i];
+        }
+    };
+
+    f32x16 acc[TCO][2];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) acc[i][0] = acc[i][1] = f32x16{};
+
+    const int nk = (K + BK - 1) / BK;
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        const bool has_next = kt + 1 < nk;
+        if (has_next) gload((kt + 1) * BK);
+        const bf16_t* A_ = As[buf];
+        const bf16_t* B_ = Bs[buf];
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            const int ch = 2 * ks + h;
+            bf16x8_t af[TCO], bfr[2];
+#pragma unroll
+            for (int i = 0; i < TCO; ++i) {
+                const int row = wco * (BCO / 2) + 32 * i + lr;
+                af[i] = as_bf16x8(*(const uint4*)(A_ + row * BK + ((ch ^ ((row >> 1) & 7)) << 3)));
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = wm * 64 + 32 * j + lr;
+                bfr[j] = as_bf16x8(*(const uint4*)(B_ + row * BK + ((ch ^ ((row >> 1) & 7)) << 3)));
+            }
+#pragma unroll
+            for (int i = 0; i < TCO; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = MFMA32(af[i], bfr[j], acc[i][j]);
+        }
+        if (has_next) sstore(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane owns pixel m, registers 4g..4g+3 are channels co + 8g + 4h + 0..3.
+    // STATS: per-channel sum / sumsq of the stored (bf16-rounded) values, reduced over the wave's
+    // two pixel tiles in registers, over its 32 lanes by shuffles and over the two pixel-waves in
+    // LDS; each workgroup writes its own partial row part[tm][2 * Cout] (no atomics, no memset).
+    float* red = reinterpret_cast<float*>(As[0]);  // [2 (wm)][BCO][2], free after the K loop
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) {
+        const int cl = wco * (BCO / 2) + 32 * i;  // tile-local first channel of this MFMA tile
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int co = co0 + cl + 8 * g + 4 * h;
+            float sv[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int m = m0 + wm * 64 + 32 * j + lr;
+                const bool mok = m < M;
+                float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                const uint2 pk = pack4(v);
+                if (mok && co < d.Cout) *(uint2*)(out + (size_t)m * d.Cout + co) = pk;
+                if (STATS && mok) {
+                    float r[4];
+                    unpack4(pk, r);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        sv[e] += r[e];
+                        sq[e] += r[e] * r[e];
+                    }
+                }
+            }
+            if (STATS) {
+#pragma unroll
+                for (int o = 1; o < 32; o <<= 1)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        sv[e] += __shfl_xor(sv[e], o, 64);
+                        sq[e] += __shfl_xor(sq[e], o, 64);
+                    }
+                if (lr < 4) {
+                    const float s_ = lr == 0 ? sv[0] : lr == 1 ? sv[1] : lr == 2 ? sv[2] : sv[3];
+                    const float q_ = lr == 0 ? sq[0] : lr == 1 ? sq[1] : lr == 2 ? sq[2] : sq[3];
+                    const int c = cl + 8 * g + 4 * h + lr;
+                    red[(wm * BCO + c) * 2] = s_;
+                    red[(wm * BCO + c) * 2 + 1] = q_;
+                }
+            }
+        }
+    }
+    if (STATS) {
+        __syncthreads();
+        for (int c = tid; c < BCO; c += 256) {
+            const int co = co0 + c;
+            if (co < d.Cout) {
+                part[(size_t)tm * 2 * d.Cout + co] = red[c * 2] + red[(BCO + c) * 2];
+                part[(size_t)tm * 2 * d.Cout + d.Cout + co] = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
+            }
+        }
+    }
+}
+
+// stats[c] = sum over the ntm partial rows of part[r][c], c < 2*Cout (stats zeroed by the caller)
+__global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __restrict__ part, int rows, int cols,
+                                                             int rows_per_block, float* __restrict__ stats) {
+    __shared__ float red[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+    const int r0 = blockIdx.y * rows_per_block;
+    const int r1 = min(rows, r0 + rows_per_block);
+    float acc = 0.f;
+    if (c < cols)
+        for (int r = r0 + rg; r < r1; r += 4) acc += part[(size_t)r * cols + c];
+    red[rg][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (rg == 0 && c < cols) atomicAdd(stats + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                      red[3][threadIdx.x]);
+}
+
+// ============================================================================ conv_wgrad
+constexpr int WBM = 32;          // m rows per reduction step
+constexpr int WLD_PAD = 32;      // row padding (elements): 320-byte rows -> conflict-free tr reads
+
+template <int BCO>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                            float* __restrict__ dw, ConvDims d, int m_per_split,
+                                                            int mode) {
+    constexpr int TCO = BCO / 64;
+    constexpr int LDY = BCO + WLD_PAD, LDX = 128 + WLD_PAD;
+    constexpr int YCH = BCO / 8;        // 16-byte chunks per dY row
+    constexpr int YROWS = 256 / YCH;    // rows covered by one pass of 256 threads
+    __shared__ __attribute__((aligned(16))) bf16_t Ys[2][WBM * LDY];
+    __shared__ __attribute__((aligned(16))) bf16_t Xs[2][WBM * LDX];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, lr = lane & 31;
+    const int wco = w >> 1, wk = w & 1;
+    const int M = d.N * d.P * d.Q;
+    const int K = d.R * d.S * d.Cin;
+    const int ntco = (d.Cout + BCO - 1) / BCO, ntk = (K + 127) / 128;
+    const int wg = xcd_remap(blockIdx.x, ntco * ntk);
+    const int tco = wg % ntco, tk = wg / ntco;
+    const int co0 = tco * BCO, k0 = tk * 128;
+    const int mbeg = blockIdx.z * m_per_split;
+    const int mend = min(M, mbeg + m_per_split);
+    const int PQ = d.P * d.Q;
+
+    // X staging: thread -> (row xr + 16 i, chunk xc); its k chunk (r, s, c) is fixed for the block
+    const int xr = tid >> 4, xc = tid & 15;
+    const int kk = k0 + 8 * xc;
+    const bool kin = kk < K;
+    int kc = 0, kr = 0, ks = 0;
+    if (kin) {
+        const int rs = kk / d.Cin;
+        kc = kk - rs * d.Cin;
+        kr = rs / d.S;
+        ks = rs - kr * d.S;
+    }
+    // dY staging: thread -> (row yr + YROWS i, chunk yc)
+    const int yr = tid / YCH, yc = tid - yr * YCH;
+    uint4 yreg[WBM / YROWS], xreg[2];
+    auto gload = [&](int mb) {
+#pragma unroll
+        for (int i = 0; i < WBM / YROWS; ++i) {
+            const int m = mb + yr + YROWS * i;
+            const int co = co0 + 8 * yc;
+            yreg[i] = (m < mend && co < d.Cout) ? *(const uint4*)(dy + (size_t)m * d.Cout + co) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = mb + xr + 16 * i;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (kin && m < mend) {
+                const int n = m / PQ, pq = m - n * PQ, p = pq / d.Q, q = pq - p * d.Q;
+                const int y = p * d.stride - d.pad + kr, xx = q * d.stride - d.pad + ks;
+                if ((unsigned)y < (unsigned)d.Hin && (unsigned)xx < (unsigned)d.Win)
+                    v = *(const uint4*)(x + (((size_t)n * d.Hin + y) * d.Win + xx) * d.Cin + kc);
+            }
+            xreg[i] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < WBM / YROWS; ++i) *(uint4*)(Ys[buf] + (yr + YROWS * i) * LDY + 8 * yc) = yreg[i];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) *(uint4*)(Xs[buf] + (xr + 16 * i) * LDX + 8 * xc) = xreg[i];
+    };
+
+    f32x16 acc[TCO][2];
+#pragma unroll
+    for (int i = 0; i < TCO; ++i) acc[i][0] = acc[i][1] = f32x16{};
+    // transposed-read geometry: 16-lane group (gg = lane>>4 & 1 selects 16 columns), lane 4q+p
+    const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
+
+    if (mbeg < mend) {
+        gload(mbeg);
+        sstore(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int mb = mbeg; mb < mend; mb += WBM) {
+        const bool has_next = mb + WBM < mend;
+        if (has_next) gload(mb + WBM);
+        const bf16_t* Y_ = Ys[buf];
+        const bf16_t* X_ = Xs[buf];
+#pragma unroll
+        for (int st = 0; st < WBM / 16; ++st) {
+            const int rb = 16 * st + 8 * h + tq;  // element j<4: row rb+j... (same map for A and B)
+            bf16x8_t af[TCO], bfr[2];
+#pragma unroll
+            for (int i = 0; i < TCO; ++i) {
+                const int cb = wco * (BCO / 2) + 32 * i + tcol;
+                af[i] = tr_pair(Y_ + rb * LDY + cb, Y_ + (rb + 4) * LDY + cb);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int cb = wk * 64 + 32 * j + tcol;
+                bfr[j] = tr_pair(X_ + rb * LDX + cb, X_ + (rb + 4) * LDX + cb);
+            }
+#pragma unroll
+            for (int i = 0; i < TCO; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = MFMA32(af[i], bfr[j], acc[i][j]);
+        }
+        if (has_next) sstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // ---- epilogue: lane owns filter column k = (r, s, c); registers are output channels.
+    // dw is [Cout][K] (K = R*S*Cin, c fastest) so consecutive lanes hit consecutive addresses.
+    // mode 0: store, 1: +=, 2: fp32 atomic add (split reduction)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int k = k0 + wk * 64 + 32 * j + lr;
+        if (k >= K) continue;
+#pragma unroll
+        for (int i = 0; i < TCO; ++i) {
+            const int cb = co0 + wco * (BCO / 2) + 32 * i;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int co = cb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                if (co >= d.Cout) continue;
+                float* dst = dw + (size_t)co * K + k;
+                if (mode == 2) atomicAdd(dst, acc[i][j][reg]);
+                else if (mode == 1) *dst += acc[i][j][reg];
+                else *dst = acc[i][j][reg];
+            }
+        }
+    }
+}
+
+// dst[co][c][rs] += src[co][rs][c]   (KRSC fp32 workspace -> the parameter's [Cout][Cin][R][S] grad)
+__global__ __launch_bounds__(256) void krsc_to_kcrs_add_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                               int Cout, int RS, int Cin) {
+    const int64_t n = (int64_t)Cout * RS * Cin;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % Cin);
+        const int64_t t = i / Cin;
+        const int rs = (int)(t % RS);
+        const int64_t co = t / RS;
+        dst[(co * Cin + c) * RS + rs] += src[i];
+    }
+}
+
+bool dims_ok(const ConvDims& d) {
+    return d.Cin % 8 == 0 && d.Cout % 8 == 0 && d.N > 0 && d.P > 0 && d.Q > 0 && d.R > 0 && d.S > 0 && d.stride > 0 &&
+           (long long)d.N * d.Hin * d.Win * d.Cin < (1ll << 31) && (long long)d.N * d.P * d.Q * d.Cout < (1ll << 31);
+}
+
+}  // namespace
+
+// act: gathered NHWC tensor [N][Hin][Win][Cin]; wk: [Cout][R][S][Cin]; out: [N][P][Q][Cout].
+// transposed = 1 -> data-gradient mapping (act = dY, wk = W permuted to [Cin][R][S][Cout]).
+// stats: null, or fp32 [2 * Cout] = (per-channel sum, sum of squares) of out; then stats_ws must
+// hold tdl_conv_stats_ws_floats(...) floats (one partial row per 128-pixel tile).
+TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) { return (int64_t)((M + BM - 1) / BM) * 2 * Cout; }
+
+TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
+                        int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
+                        hipStream_t s) {
+    ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
+    if (!dims_ok(d)) return (int)hipErrorInvalidValue;
+    const int M = N * P * Q;
+    const bool st = stats != nullptr;
+    if (st && stats_ws == nullptr) return (int)hipErrorInvalidValue;
+    const bool big = Cout > 64;
+    const int ntm = (M + BM - 1) / BM;
+    const int nblk = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
+    auto A = (const bf16_t*)act;
+    auto W = (const bf16_t*)wk;
+    auto O = (bf16_t*)out;
+#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d)
+    if (big) {
+        if (transposed) { if (st) LAUNCH(128, true, true); else LAUNCH(128, true, false); }
+        else { if (st) LAUNCH(128, false, true); else LAUNCH(128, false, false); }
+    } else {
+        if (transposed) { if (st) LAUNCH(64, true, true); else LAUNCH(64, true, false); }
+        else { if (st) LAUNCH(64, false, true); else LAUNCH(64, false, false); }
+    }
+#undef LAUNCH
+    if (st) {
+        hipError_t e = hipMemsetAsync(stats, 0, sizeof(float) * 2 * Cout, s);
+        if (e != hipSuccess) return (int)e;
+        const int rpb = 64;
+        const dim3 g((2 * Cout + 63) / 64, (ntm + rpb - 1) / rpb);
+        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats);
+    }
+    TDL_LAUNCH_CHECK();
+}
+
+// dw (fp32 [Cout][Cin][R][S], accumulated) += sum_m dY[m][co] * im2col(X)[m][k].  For R*S > 1 the
+// kernel reduces into ws (fp32, Cout*R*S*Cin floats, [Cout][R][S][Cin]) and one pass adds it to dw.
+TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,
+                           int Q, int Cout, int R, int S, int stride, int pad, int num_cu, hipStream_t s) {
+    ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
+    if (!dims_ok(d)) return (int)hipErrorInvalidValue;
+    const int M = N * P * Q, K = R * S * Cin;
+    const bool big = Cout > 64;
+    const int bco = big ? 128 : 64;
+    const int tiles = ((Cout + bco - 1) / bco) * ((K + 127) / 128);
+    // split the pixel reduction until the grid holds ~2 workgroups per CU, each >= 16 steps
+    const int target = 2 * (num_cu > 0 ? num_cu : 256);
+    int split = (target + tiles - 1) / tiles;
+    const int max_split = (M + 16 * WBM - 1) / (16 * WBM);
+    if (split > max_split) split = max_split;
+    if (split < 1) split = 1;
+    int mps = (M + split - 1) / split;
+    mps = (mps + WBM - 1) / WBM * WBM;
+    split = (M + mps - 1) / mps;
+    const bool direct = R * S == 1;  // KRSC == KCRS: reduce straight into the gradient
+    if (!direct && ws == nullptr) return (int)hipErrorInvalidValue;
+    float* target_buf = direct ? dw : ws;
+    int mode = direct ? (split > 1 ? 2 : 1) : (split > 1 ? 2 : 0);
+    if (!direct && split > 1) {
+        hipError_t e = hipMemsetAsync(ws, 0, sizeof(float) * (size_t)Cout * K, s);
+        if (e != hipSuccess) return (int)e;
+    }
+    const dim3 grid(tiles, 1, split);
+    if (big) conv_wgrad_kernel<128><<<grid, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, target_buf, d, mps, mode);
+    else conv_wgrad_kernel<64><<<grid, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, target_buf, d, mps, mode);
+    if (!direct) {
+        const int64_t n = (int64_t)Cout * K;
+        int g = (int)((n + 255) / 256);
+        if (g > 2048) g = 2048;
+        krsc_to_kcrs_add_kernel<<<g, 256, 0, s>>>(ws, dw, Cout, R * S, Cin);
+    }
+    TDL_LAUNCH_CHECK();
+}

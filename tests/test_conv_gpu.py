@@ -1,0 +1,145 @@
+"""Numerics of the native NHWC conv / BN kernels (csrc/conv.hip, csrc/bn.hip) against PyTorch fp32
+references of the same ops on the same bf16-rounded inputs."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+# (N, C, H, W, Cout, R, stride, pad)
+SHAPES = [
+    (2, 16, 16, 16, 32, 3, 1, 1),
+    (2, 64, 14, 14, 128, 3, 2, 1),
+    (2, 64, 8, 8, 256, 1, 1, 0),
+    (2, 256, 8, 8, 512, 1, 2, 0),
+    (2, 3, 32, 32, 64, 7, 2, 3),     # image stem: channels padded to 8
+    (1, 24, 9, 7, 40, 3, 1, 1),      # ragged everything
+    (4, 64, 56, 56, 64, 3, 1, 1),    # many pixel tiles
+]
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+def _inputs(N, C, H, W, Cout, R, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, R, R, device="cuda", generator=g) * (2.0 / (C * R * R)) ** 0.5).to(torch.bfloat16)
+    return x, w
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_forward_and_stats(shape):
+    from trustworthy_dl.ops.conv import _Conv2dNHWC
+    N, C, H, W, Cout, R, st, pad = shape
+    x, w = _inputs(N, C, H, W, Cout, R)
+    y, stats = _Conv2dNHWC.apply(x, w, st, pad, True)
+    ref = F.conv2d(x.float(), w.float(), None, st, pad)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 1e-2
+    yb = y.float()
+    assert _rel(stats[:Cout], yb.sum((0, 2, 3))) < 1e-3
+    assert _rel(stats[Cout:], (yb * yb).sum((0, 2, 3))) < 1e-3
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_backward(shape):
+    from trustworthy_dl.ops.conv import conv2d
+    N, C, H, W, Cout, R, st, pad = shape
+    x, w = _inputs(N, C, H, W, Cout, R, seed=1)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    ref = F.conv2d(xr, wr, None, st, pad)
+    gy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16)
+    ref.backward(gy.float())
+    xn, wn = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv2d(xn, wn, st, pad)
+    y.backward(gy.contiguous(memory_format=torch.channels_last))
+    assert _rel(xn.grad, xr.grad) < 1e-2
+    assert _rel(wn.grad, wr.grad) < 1e-2
+
+
+def test_conv_wgrad_accumulates_into_main_grad():
+    from trustworthy_dl.ops.conv import conv2d
+    x, w = _inputs(2, 32, 12, 12, 64, 3, seed=2)
+    w = w.clone().requires_grad_(True)
+    w.main_grad = torch.full(w.shape, 0.5, dtype=torch.float32, device="cuda")
+    gy = torch.randn(2, 64, 12, 12, device="cuda").to(torch.bfloat16)
+    for _ in range(2):
+        conv2d(x, w, 1, 1).backward(gy)
+    assert w.grad is None
+    wr = w.detach().float().requires_grad_(True)
+    F.conv2d(x.float(), wr, None, 1, 1).backward(gy.float())
+    assert _rel(w.main_grad - 0.5, 2 * wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_conv_bn_act_train_matches_torch(relu, residual):
+    from trustworthy_dl.ops.conv import conv_bn_act
+    torch.manual_seed(0)
+    conv = nn.Conv2d(32, 64, 3, 2, 1, bias=False).cuda()
+    bn = nn.BatchNorm2d(64).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    conv_r, bn_r = nn.Conv2d(32, 64, 3, 2, 1, bias=False).cuda(), nn.BatchNorm2d(64).cuda()
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    conv.to(torch.bfloat16)
+    bn.weight.data = bn.weight.data.to(torch.bfloat16)
+    bn.bias.data = bn.bias.data.to(torch.bfloat16)
+    conv_r.weight.data.copy_(conv.weight.data.float())
+    bn_r.weight.data.copy_(bn.weight.data.float())
+    bn_r.bias.data.copy_(bn.bias.data.float())
+
+    x = torch.randn(4, 32, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(4, 64, 8, 8, device="cuda").to(torch.bfloat16) if residual else None
+    xn = x.clone().requires_grad_(True)
+    rn = res.clone().requires_grad_(True) if residual else None
+    out = conv_bn_act(xn, conv, bn, relu=relu, residual=rn)
+    xr = x.float().requires_grad_(True)
+    rr = res.float().requires_grad_(True) if residual else None
+    ref = bn_r(conv_r(xr))
+    if residual:
+        ref = ref + rr
+    if relu:
+        # the ReLU mask of the bf16 output decides near-zero pre-activations; use the same mask in
+        # the fp32 reference so mask flips at |pre| ~ bf16 ulp do not masquerade as kernel error
+        assert _rel(out, F.relu(ref)) < 2e-2
+        ref = ref * (out.detach() > 0).float()
+    assert _rel(out, ref) < 2e-2
+    gy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16)
+    out.backward(gy)
+    ref.backward(gy.float())
+    assert _rel(xn.grad, xr.grad) < 3e-2
+    assert _rel(conv.weight.grad, conv_r.weight.grad) < 3e-2
+    assert _rel(bn.weight.grad, bn_r.weight.grad) < 3e-2
+    assert _rel(bn.bias.grad, bn_r.bias.grad) < 3e-2
+    if residual:
+        assert _rel(rn.grad, rr.grad) < 2e-2
+    assert _rel(bn.running_mean, bn_r.running_mean) < 2e-2
+    assert _rel(bn.running_var, bn_r.running_var) < 2e-2
+
+
+def test_resnet_engine_step_native():
+    """A ResNet-32 pipeline step on the GPU goes through the native conv path (bf16) and matches
+    the CPU fp32 engine's first loss."""
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.flat import AdamWConfig
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    g = torch.Generator().manual_seed(3)
+    batch = {"input": torch.randn(16, 3, 32, 32, generator=g), "target": torch.randint(0, 10, (16,), generator=g)}
+    losses = {}
+    for dev in ("cpu", "cuda:0"):
+        m = get_model("resnet32", seed=5)
+        eng = PipelineEngine(m, EngineConfig(num_nodes=2, micro_batches=2, device=dev,
+                                             adamw=AdamWConfig(lr=1e-3), reassign=False))
+        eng.train_step(batch)
+        eng.train_step(batch)
+        eng.flush()
+        losses[dev] = eng.last_loss
+        if dev.startswith("cuda"):
+            assert eng.dtype == torch.bfloat16
+    assert losses["cuda:0"] == pytest.approx(losses["cpu"], rel=5e-2)

@@ -5,8 +5,10 @@ README.md:89-92 lists these model families; the reference's ``create_model_parti
 ``pipeline_layers()`` — a flat list of residual blocks / conv units with the classifier (+ loss)
 as the last layer — so the same partitioner and pipeline engine run them.  ResNet-32 is the CIFAR
 variant (6n+2, n=5; BasicBlocks of 16/32/64 channels), not in torchvision, built here.
-Convolutions run on MIOpen through torch (conv kernels are the next native milestone); BN/ReLU
-and the classifier cross-entropy use the same op layer as GPT-2.
+On GPU (bf16) every conv+BN(+residual)+ReLU unit runs the native NHWC implicit-GEMM MFMA conv
+kernels with fused batch statistics and the one-pass BN/act kernel (ops/conv.py, csrc/conv.hip,
+csrc/bn.hip); on CPU the same modules run through torch.  Parameter names are the torchvision ones
+(conv1/bn1/..., shortcut.0/shortcut.1), so state dicts are unchanged.
 """
 from __future__ import annotations
 
@@ -59,10 +61,9 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        out = self.bn2(self.conv2(out))
-        sc = x if self.shortcut is None else self.shortcut(x)
-        return F.relu(out + sc, inplace=True)
+        out = ops.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        sc = x if self.shortcut is None else ops.conv_bn_act(x, self.shortcut[0], self.shortcut[1], relu=False)
+        return ops.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=sc)
 
 
 class Bottleneck(nn.Module):
@@ -82,11 +83,10 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)), inplace=True)
-        out = F.relu(self.bn2(self.conv2(out)), inplace=True)
-        out = self.bn3(self.conv3(out))
-        sc = x if self.shortcut is None else self.shortcut(x)
-        return F.relu(out + sc, inplace=True)
+        out = ops.conv_bn_act(x, self.conv1, self.bn1, relu=True)
+        out = ops.conv_bn_act(out, self.conv2, self.bn2, relu=True)
+        sc = x if self.shortcut is None else ops.conv_bn_act(x, self.shortcut[0], self.shortcut[1], relu=False)
+        return ops.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=sc)
 
 
 class Stem(nn.Module):
@@ -100,7 +100,7 @@ class Stem(nn.Module):
         self.pool = imagenet
 
     def forward(self, x):
-        x = F.relu(self.bn(self.conv(x)), inplace=True)
+        x = ops.conv_bn_act(x, self.conv, self.bn, relu=True)
         return F.max_pool2d(x, 3, 2, 1) if self.pool else x
 
 
@@ -220,7 +220,7 @@ class ConvUnit(nn.Module):
         self.pool = pool
 
     def forward(self, x):
-        x = F.relu(self.bn(self.conv(x)), inplace=True)
+        x = ops.conv_bn_act(x, self.conv, self.bn, relu=True)
         return F.max_pool2d(x, 2) if self.pool else x
 
 

@@ -1,0 +1,197 @@
+"""Convolution + BatchNorm (+ residual) (+ ReLU) blocks for VGG / ResNet stages.
+
+GPU bf16 tensors run the native gfx950 kernels — implicit-GEMM MFMA convolutions
+(csrc/conv.hip: forward with fused per-channel batch statistics, data gradient, weight gradient
+accumulated into the parameter's fp32 ``main_grad``) and one-pass NHWC BatchNorm/residual/ReLU
+(csrc/bn.hip).  Activations are NHWC (torch ``channels_last``); weights keep the nn.Conv2d
+[Cout, Cin, R, S] parameter layout (so state dicts / checkpoints are unchanged) and are permuted
+to the kernel's [Cout][R][S][Cin] once per call (a weight-sized copy, tiny next to the GEMM).
+Input channel counts that are not a multiple of 8 (the 3-channel image stem) are zero-padded to 8.
+
+CPU (and fp32) tensors run the PyTorch modules themselves — the reference semantics the CPU/gloo
+tests and the layer-cost hooks see.  There is no silent fallback on a GPU: a bf16 CUDA conv that
+the kernels cannot serve raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import ptr, stream_ptr
+
+_NUM_CU = {}
+
+
+def _num_cu(dev: torch.device) -> int:
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    n = _NUM_CU.get(idx)
+    if n is None:
+        n = torch.cuda.get_device_properties(idx).multi_processor_count
+        _NUM_CU[idx] = n
+    return n
+
+
+def native_conv_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16
+
+
+def _out_hw(H: int, W: int, R: int, S: int, stride: int, pad: int):
+    return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
+
+
+def _pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
+    N, C, H, W = x.shape
+    xp = torch.empty((N, cp, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last).zero_()
+    xp[:, :C].copy_(x)
+    return xp
+
+
+class _Conv2dNHWC(torch.autograd.Function):
+    """y = conv2d(x, w) on NHWC bf16; also returns per-channel (sum, sumsq) of y when asked."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int, want_stats: bool):
+        N, C, H, W = x.shape
+        Cout, Cw, R, S = weight.shape
+        if Cw != C or Cout % 8 != 0:
+            raise ValueError(f"native conv: unsupported shapes x={tuple(x.shape)} w={tuple(weight.shape)}")
+        cp = (C + 7) // 8 * 8
+        xs = x.contiguous(memory_format=torch.channels_last)
+        wp = weight
+        if cp != C:
+            xs = _pad_channels(xs, cp)
+            wp = torch.zeros((Cout, cp, R, S), dtype=weight.dtype, device=weight.device)
+            wp[:, :C].copy_(weight)
+        wk = wp.permute(0, 2, 3, 1).contiguous()
+        P, Q = _out_hw(H, W, R, S, stride, pad)
+        y = torch.empty((N, Cout, P, Q), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        stats = ws = None
+        if want_stats:
+            stats = torch.empty(2 * Cout, dtype=torch.float32, device=x.device)
+            ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * P * Q, Cout)), dtype=torch.float32,
+                             device=x.device)
+        _lib.call("tdl_conv_nt", ptr(xs), ptr(wk), ptr(y), ptr(stats), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
+                  pad, 0, stream_ptr(x.device))
+        ctx.save_for_backward(xs, wp, weight)
+        ctx.geom = (N, C, cp, H, W, Cout, R, S, P, Q, stride, pad)
+        if stats is None:
+            stats = torch.zeros(0, dtype=torch.float32, device=x.device)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        xs, wp, weight = ctx.saved_tensors
+        N, C, cp, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if dy.dtype != xs.dtype:
+            dy = dy.to(xs.dtype)
+        dev = dy.device
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wd = wp.permute(1, 2, 3, 0).contiguous()  # [cp][R][S][Cout]
+            dxp = torch.empty((N, cp, H, W), dtype=dy.dtype, device=dev, memory_format=torch.channels_last)
+            _lib.call("tdl_conv_nt", ptr(dy), ptr(wd), ptr(dxp), None, None, N, P, Q, Cout, H, W, cp, R, S, stride,
+                      pad, 1, stream_ptr(dev))
+            dx = dxp if cp == C else dxp[:, :C]
+        gw = None
+        if ctx.needs_input_grad[1]:
+            mg = getattr(weight, "main_grad", None)
+            if mg is not None and cp == C and mg.is_contiguous():
+                acc = mg
+            else:
+                acc = torch.zeros((Cout, cp, R, S), dtype=torch.float32, device=dev)
+            ws = torch.empty(Cout * R * S * cp, dtype=torch.float32, device=dev) if R * S > 1 else None
+            _lib.call("tdl_conv_wgrad", ptr(dy), ptr(xs), ptr(acc), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
+                      pad, _num_cu(dev), stream_ptr(dev))
+            if acc is not mg:
+                g = acc if cp == C else acc[:, :C]
+                if mg is not None:
+                    mg.add_(g)
+                else:
+                    gw = g.to(weight.dtype)
+        return dx, gw, None, None, None
+
+
+class _BatchNormActNHWC(torch.autograd.Function):
+    """out = act(BN(y) (+ residual)) with batch statistics (training) from the conv epilogue."""
+
+    @staticmethod
+    def forward(ctx, y, stats, gamma, beta, residual, running_mean, running_var, training: bool,
+                momentum: float, eps: float, relu: bool):
+        N, C, H, W = y.shape
+        M = N * H * W
+        y = y.contiguous(memory_format=torch.channels_last)
+        res = None
+        if residual is not None:
+            res = residual.contiguous(memory_format=torch.channels_last)
+            if res.dtype != y.dtype:
+                res = res.to(y.dtype)
+        out = torch.empty_like(y, memory_format=torch.channels_last)
+        mean = torch.empty(C, dtype=torch.float32, device=y.device)
+        rstd = torch.empty_like(mean)
+        upd = training and running_mean is not None
+        _lib.call("tdl_bn_act_fwd", ptr(y), ptr(stats if training else None), ptr(running_mean), ptr(running_var),
+                  ptr(gamma), ptr(beta), ptr(res), ptr(out), ptr(mean), ptr(rstd),
+                  ptr(running_mean if upd else None), ptr(running_var if upd else None), M, C, float(eps),
+                  float(momentum), int(relu), stream_ptr(y.device))
+        ctx.save_for_backward(y, out, mean, rstd, gamma, beta)
+        ctx.cfg = (M, C, relu, residual is not None, training)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, out, mean, rstd, gamma, beta = ctx.saved_tensors
+        M, C, relu, has_res, training = ctx.cfg
+        if not training:
+            raise RuntimeError("native BatchNorm backward requires training mode (batch statistics)")
+        dev = dout.device
+        dout = dout.contiguous(memory_format=torch.channels_last)
+        if dout.dtype != y.dtype:
+            dout = dout.to(y.dtype)
+        dx = torch.empty_like(y, memory_format=torch.channels_last)
+        dres = torch.empty_like(y, memory_format=torch.channels_last) if has_res else None
+        sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
+        dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+        db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+        _lib.call("tdl_bn_act_bwd", ptr(dout), ptr(out), ptr(y), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums), ptr(dx),
+                  ptr(dres), ptr(dg), ptr(db), M, C, int(relu), stream_ptr(dev))
+        gg = None if mg_g is not None else dg.to(gamma.dtype)
+        gb = None if mg_b is not None else db.to(beta.dtype)
+        return dx, None, gg, gb, dres, None, None, None, None, None, None
+
+
+def _single(v) -> int:
+    return int(v if isinstance(v, int) else v[0])
+
+
+def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool = True,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(bn(conv(x)) (+ residual)).  Native NHWC kernels for CUDA bf16, the torch modules otherwise."""
+    if not native_conv_ok(x):
+        out = bn(conv(x))
+        if residual is not None:
+            out = out + residual
+        return F.relu(out) if relu else out
+    if conv.groups != 1 or _single(conv.dilation) != 1 or conv.bias is not None \
+            or conv.kernel_size[0] != conv.kernel_size[1] or conv.stride[0] != conv.stride[-1] \
+            or conv.padding[0] != conv.padding[-1]:
+        raise NotImplementedError(f"native conv: unsupported configuration {conv}")
+    training = bn.training
+    y, stats = _Conv2dNHWC.apply(x, conv.weight, _single(conv.stride), _single(conv.padding), training)
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    return _BatchNormActNHWC.apply(y, stats, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var,
+                                   training, momentum, bn.eps, relu)
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0) -> torch.Tensor:
+    """Plain convolution (no BN) on the native path for CUDA bf16 tensors."""
+    if native_conv_ok(x):
+        y, _ = _Conv2dNHWC.apply(x, weight, int(stride), int(padding), False)
+        return y
+    return F.conv2d(x, weight, None, stride, padding)

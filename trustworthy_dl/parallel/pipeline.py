@@ -118,10 +118,8 @@ class PipelineEngine:
             self.device = torch.device(cfg.device)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-        cd = cfg.compute_dtype
-        if cd == "auto" and getattr(model, "family", "") == "cnn":
-            cd = "fp32"  # conv nets: fp32 MIOpen path until the native implicit-GEMM convs land
-        self.dtype = _resolve_dtype(cd, self.device)
+        # conv nets run bf16 on the native NHWC implicit-GEMM kernels (ops/conv.py), like GPT-2
+        self.dtype = _resolve_dtype(cfg.compute_dtype, self.device)
 
         if hasattr(model, "config") and hasattr(model, "layer_costs") and getattr(model, "family", "") == "gpt2":
             self.costs = model.layer_costs(cfg.seq_len or model.config.n_positions)
