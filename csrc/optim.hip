@@ -76,3 +76,31 @@ TDL_API int tdl_fill_f32(float* p, int64_t n, float val, hipStream_t s) {
     fill_f32_kernel<<<(int)(work < 4096 ? (work > 0 ? work : 1) : 4096), 256, 0, s>>>(p, n, val);
     TDL_LAUNCH_CHECK();
 }
+
+// acc[i] += sum_s part[s * n + i]  — the reduction of a split-K weight-gradient GEMM whose S partial
+// products were written (fp32) by one batched GEMM; one streaming pass, float4-vectorised.
+__global__ __launch_bounds__(256) void splitk_reduce_add_kernel(float* __restrict__ acc, const float* __restrict__ part,
+                                                                int S, int64_t n4) {
+    const float4* p4 = (const float4*)part;
+    float4* a4 = (float4*)acc;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        float4 a = a4[i];
+        for (int s = 0; s < S; ++s) {
+            const float4 v = p4[(int64_t)s * n4 + i];
+            a.x += v.x;
+            a.y += v.y;
+            a.z += v.z;
+            a.w += v.w;
+        }
+        a4[i] = a;
+    }
+}
+
+TDL_API int tdl_splitk_reduce_add(float* acc, const float* part, int S, int64_t n, hipStream_t s) {
+    if (n % 4 != 0 || ((uintptr_t)acc & 15) || ((uintptr_t)part & 15)) return (int)hipErrorInvalidValue;
+    const int64_t n4 = n / 4;
+    int64_t g = (n4 + 255) / 256;
+    if (g > 4096) g = 4096;
+    splitk_reduce_add_kernel<<<(int)(g > 0 ? g : 1), 256, 0, s>>>(acc, part, S, n4);
+    TDL_LAUNCH_CHECK();
+}

@@ -358,3 +358,17 @@ def test_fused_gpt2_block_matches_fp32():
     for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
         assert p.grad is None, n
         assert _rel(p.main_grad.cpu(), q.grad) < 3e-2, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,K,N", [(32768, 1024, 1024), (16384, 1024, 3072), (8192, 1024, 1024)])
+def test_wgrad_splitk_accumulates(M, K, N):
+    from trustworthy_dl.ops.layers import wgrad_acc, wgrad_split
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    acc = torch.randn(K, N, device="cuda")
+    ref = acc + x.float().t() @ dy.float()
+    assert wgrad_split(M, K, N) > 1
+    wgrad_acc(acc, x.t(), dy)
+    assert float((acc - ref).norm() / ref.norm()) < 1e-3

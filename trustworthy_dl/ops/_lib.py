@@ -89,6 +89,7 @@ _SIGNATURES = {
     # optim.hip
     "tdl_adamw_flat": [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _F, _P, _I, _P],
     "tdl_fill_f32": [_P, _L, _F, _P],
+    "tdl_splitk_reduce_add": [_P, _P, _I, _L, _P],
     # stats.hip
     "tdl_tensor_stats": [_P, _I, _L, _P, _P, _I, _P],
     "tdl_grad_stats": [_P, _P, _P, _I, _P, _L, _F, _I, _P, _I, _I, _P],

@@ -125,11 +125,45 @@ def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
     return _accumulate(bias, dy2.float().sum(0))
 
 
+def wgrad_split(M: int, K: int, N: int) -> int:
+    """Split-K factor for a weight-gradient GEMM [K, M] @ [M, N] (reduction over M tokens).
+    A GPT-2 projection's gradient has only (K/256)(N/256) = 16..64 output tiles of hipBLASLt's
+    256x256 macro tile — a quarter of the 256 CUs or fewer — while M is 8k-32k deep; splitting M
+    into S batched products fills the chip (measured, scripts/bench_gemm.py on MI355X: o-proj
+    350 -> 813 TFLOP/s at M=32768 with S=8, qkv 660 -> 1027 with S=4)."""
+    tiles = max(1, (K // 256) * (N // 256))
+    if os.environ.get("TDL_WGRAD_SPLITK", "1") == "0":
+        return 1
+    if M >= 16384:
+        s = 8 if tiles <= 16 else (4 if tiles <= 64 else 1)
+    elif M >= 8192:
+        s = 4 if tiles <= 16 else 1
+    else:
+        s = 1
+    while s > 1 and (M % s or (M // s) % 64):
+        s //= 2
+    return s
+
+
 def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
-    """acc (fp32, shape of a @ b) += a @ b in one GEMM pass where the torch build allows it."""
+    """acc (fp32, shape of a @ b) += a @ b in one GEMM pass where the torch build allows it.
+
+    ``a`` is usually X^T (a transposed view of a row-major [M, K] activation): then the product
+    may be split along M into S fp32 partials by one batched GEMM and reduced into ``acc`` by one
+    native pass (wgrad_split)."""
     global _MM_F32_OK, _ADDMM_F32_OK
     if not a.is_cuda:
         acc.add_((a @ b).float().view(acc.shape))
+        return
+    K, M = a.shape
+    N = b.shape[1]
+    S = wgrad_split(M, K, N)
+    if S > 1 and a.t().is_contiguous() and b.is_contiguous() and acc.is_contiguous():
+        a3 = a.t().view(S, M // S, K).transpose(1, 2)
+        b3 = b.view(S, M // S, N)
+        part = torch.empty((S, K, N), dtype=torch.float32, device=acc.device)
+        torch.bmm(a3, b3, out_dtype=torch.float32, out=part)
+        _lib.call("tdl_splitk_reduce_add", ptr(acc), ptr(part), S, acc.numel(), stream_ptr(acc.device))
         return
     if _ADDMM_F32_OK is not False:
         # beta=1 GEMM epilogue accumulating in place into the fp32 buffer (one pass)
