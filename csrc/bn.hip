@@ -10,6 +10,10 @@
 
 namespace {
 
+// Backward reductions add into NREP replicas of the [2C] sums (replica = block % NREP): 16x less
+// same-address atomic contention than one copy; the dx kernel folds the replicas in LDS.
+constexpr int NREP = 16;
+
 // ---------------------------------------------------------------- forward
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ stats,
                                                          const float* __restrict__ run_mean, const float* __restrict__ run_var,
@@ -17,9 +21,13 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
                                                          const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
                                                          float* __restrict__ save_mean, float* __restrict__ save_rstd,
                                                          float* __restrict__ upd_mean, float* __restrict__ upd_var,
+                                                         float* __restrict__ zero_buf, int64_t zero_n,
                                                          int64_t M, int C, float eps, float momentum, int relu) {
     const int CV = C >> 3;
     const bool train = stats != nullptr;
+    // zero the backward's replicated reduction buffer here (saves a memset launch per BN layer)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += (int64_t)gridDim.x * blockDim.x)
+        zero_buf[i] = 0.f;
     const float invM = 1.f / (float)M;
     if (blockIdx.x == 0) {
         for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -43,6 +51,51 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
         }
     }
     const int64_t nvec = M * CV;
+    if ((blockDim.x % CV) == 0) {
+        // every thread of the grid-stride loop keeps the same 8 channels: fold BN into one
+        // per-channel scale/shift computed once (the per-element rsqrt made this pass ALU-bound)
+        const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int c0 = (int)(v0 % CV) * 8;
+        float sc[8], sh[8];
+        {
+            float g[8], b[8];
+            unpack8(*(const uint4*)(gamma + c0), g);
+            unpack8(*(const uint4*)(beta + c0), b);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int c = c0 + e;
+                float mean, var;
+                if (train) {
+                    mean = stats[c] * invM;
+                    var = fmaxf(stats[C + c] * invM - mean * mean, 0.f);
+                } else {
+                    mean = run_mean[c];
+                    var = run_var[c];
+                }
+                sc[e] = rsqrtf(var + eps) * g[e];
+                sh[e] = b[e] - mean * sc[e];
+            }
+        }
+        for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+            float xv[8];
+            unpack8(((const uint4*)x)[v], xv);
+            if (res) {
+                float rv[8];
+                unpack8(((const uint4*)res)[v], rv);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[e] = fmaf(xv[e], sc[e], sh[e]) + rv[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[e] = fmaf(xv[e], sc[e], sh[e]);
+            }
+            if (relu) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[e] = fmaxf(xv[e], 0.f);
+            }
+            ((uint4*)out)[v] = pack8(xv);
+        }
+        return;
+    }
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
         const int c0 = (int)(v % CV) * 8;
         float xv[8], g[8], b[8], rv[8];
@@ -93,21 +146,36 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
         }
         const int64_t rbeg = (int64_t)blockIdx.x * rows_per_block;
         const int64_t rend = rbeg + rows_per_block < M ? rbeg + rows_per_block : M;
-        for (int64_t r = rbeg + r0; r < rend; r += RPB) {
-            const int64_t v = r * CV + cv;
-            float dv[8], xv[8];
-            unpack8(((const uint4*)dout)[v], dv);
-            unpack8(((const uint4*)x)[v], xv);
-            if (relu) {
-                float ov[8];
-                unpack8(((const uint4*)out)[v], ov);
+        // 4 rows per iteration: 12 independent 16-byte loads in flight per thread (the loop is
+        // a pure HBM stream; one row at a time left it latency-bound at ~half the bandwidth)
+        constexpr int U = 4;
+        for (int64_t r = rbeg + r0; r < rend; r += U * RPB) {
+            uint4 dq[U], xq[U], oq[U];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) dv[e] = ov[e] > 0.f ? dv[e] : 0.f;
+            for (int u = 0; u < U; ++u) {
+                const int64_t rr = r + (int64_t)u * RPB;
+                const bool ok = rr < rend;
+                const int64_t v = (ok ? rr : r) * CV + cv;
+                dq[u] = ok ? ((const uint4*)dout)[v] : make_uint4(0, 0, 0, 0);
+                xq[u] = ((const uint4*)x)[v];
+                oq[u] = relu ? ((const uint4*)out)[v] : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                sg[e] += dv[e];
-                sgx[e] += dv[e] * (xv[e] - mu[e]) * rs[e];
+            for (int u = 0; u < U; ++u) {
+                float dv[8], xv[8];
+                unpack8(dq[u], dv);
+                unpack8(xq[u], xv);
+                if (relu) {
+                    float ov[8];
+                    unpack8(oq[u], ov);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) dv[e] = ov[e] > 0.f ? dv[e] : 0.f;
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    sg[e] += dv[e];
+                    sgx[e] += dv[e] * (xv[e] - mu[e]) * rs[e];
+                }
             }
         }
     }
@@ -127,8 +195,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            atomicAdd(sums + cv * 8 + e, sg[e]);
-            atomicAdd(sums + C + cv * 8 + e, sgx[e]);
+            float* rep = sums + (size_t)(blockIdx.x & (NREP - 1)) * 2 * C;
+            atomicAdd(rep + cv * 8 + e, sg[e]);
+            atomicAdd(rep + C + cv * 8 + e, sgx[e]);
         }
     }
 }
@@ -138,16 +207,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_dx_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, const bf16_t* __restrict__ gamma,
                                                             const float* __restrict__ sums, bf16_t* __restrict__ dx,
-                                                            bf16_t* __restrict__ dres, float* __restrict__ dgamma,
-                                                            float* __restrict__ dbeta, int64_t M, int C, int relu) {
+                                                            bf16_t* __restrict__ dres, int64_t M, int C, int relu) {
     const int CV = C >> 3;
     const float invM = 1.f / (float)M;
-    if (blockIdx.x == 0 && dgamma) {
-        for (int c = threadIdx.x; c < C; c += blockDim.x) {
-            dgamma[c] += sums[C + c];
-            dbeta[c] += sums[c];
-        }
-    }
     const int64_t nvec = M * CV;
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
         const int c0 = (int)(v % CV) * 8;
@@ -174,6 +236,21 @@ __global__ __launch_bounds__(256) void bn_act_bwd_dx_kernel(const bf16_t* __rest
     }
 }
 
+// sums[c] = sum over the NREP replicas (stored after them), and dgamma/dbeta += (one tiny pass)
+__global__ __launch_bounds__(256) void bn_fold_kernel(float* __restrict__ rep, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= 2 * C) return;
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) a += rep[(size_t)r * 2 * C + c];
+    rep[(size_t)NREP * 2 * C + c] = a;
+    if (dgamma) {
+        if (c < C) dbeta[c] += a;
+        else dgamma[c - C] += a;
+    }
+}
+
 int grid_for(int64_t nvec) {
     int64_t g = (nvec + 255) / 256;
     if (g > 4096) g = 4096;
@@ -182,39 +259,44 @@ int grid_for(int64_t nvec) {
 
 }  // namespace
 
+// Floats of the replicated backward-reduction buffer for C channels (allocated with the forward).
+TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1) * 2 * C; }
+
 // stats: [2C] (sum, sumsq) in training mode, or null to normalise with run_mean/run_var (eval).
 // save_mean/save_rstd: [C] or null.  upd_mean/upd_var: running buffers to update (train) or null.
+// bwd_ws: tdl_bn_bwd_ws_floats(C) floats zeroed here for the later backward (or null).
 TDL_API int tdl_bn_act_fwd(const void* x, const float* stats, const float* run_mean, const float* run_var,
                            const void* gamma, const void* beta, const void* res, void* out, float* save_mean,
-                           float* save_rstd, float* upd_mean, float* upd_var, int64_t M, int C, float eps,
-                           float momentum, int relu, hipStream_t s) {
+                           float* save_rstd, float* upd_mean, float* upd_var, float* bwd_ws, int64_t M, int C,
+                           float eps, float momentum, int relu, hipStream_t s) {
     if (C % 8 != 0) return (int)hipErrorInvalidValue;
     bn_act_fwd_kernel<<<grid_for(M * (C / 8)), 256, 0, s>>>(
         (const bf16_t*)x, stats, run_mean, run_var, (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)res,
-        (bf16_t*)out, save_mean, save_rstd, upd_mean, upd_var, M, C, eps, momentum, relu);
+        (bf16_t*)out, save_mean, save_rstd, upd_mean, upd_var, bwd_ws, bwd_ws ? (int64_t)NREP * 2 * C : 0, M, C, eps,
+        momentum, relu);
     TDL_LAUNCH_CHECK();
 }
 
-// sums: scratch [2C] (zeroed here).  dgamma/dbeta: fp32 accumulators (+=) or null.
+// sums: the forward's bwd_ws (zeroed there).  dgamma/dbeta: fp32 accumulators (+=) or null.
 TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
                            const void* gamma, float* sums, void* dx, void* dres, float* dgamma, float* dbeta, int64_t M,
                            int C, int relu, hipStream_t s) {
     if (C % 8 != 0) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, s);
-    if (e != hipSuccess) return (int)e;
     const int CV = C / 8;
     const int VPB = CV < 256 ? CV : 256;
     const int RPB = 256 / VPB;
     const int gy = (CV + VPB - 1) / VPB;
-    // ~4 waves of row work per CU across the grid, each block >= 8 row passes
-    int64_t rows_per_block = (M * gy + 1023) / 1024;
-    if (rows_per_block < 8 * RPB) rows_per_block = 8 * RPB;
+    // ~16 blocks per CU in total (the stream needs many loads in flight), >= one 4-row unrolled
+    // iteration per thread
+    int64_t rows_per_block = (M * gy + 4095) / 4096;
+    if (rows_per_block < 4 * RPB) rows_per_block = 4 * RPB;
     rows_per_block = (rows_per_block + RPB - 1) / RPB * RPB;
     const dim3 grid((unsigned)((M + rows_per_block - 1) / rows_per_block), gy);
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
                                                   sums, M, C, (int)rows_per_block, relu);
-    bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean,
-                                                          rstd, (const bf16_t*)gamma, sums, (bf16_t*)dx, (bf16_t*)dres,
-                                                          dgamma, dbeta, M, C, relu);
+    bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
+    bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
+        (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,
+        sums + (size_t)NREP * 2 * C, (bf16_t*)dx, (bf16_t*)dres, M, C, relu);
     TDL_LAUNCH_CHECK();
 }

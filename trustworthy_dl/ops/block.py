@@ -31,7 +31,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import ptr, stream_ptr
-from .layers import _f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, wgrad_acc
+from .layers import _f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, run_or_defer, wgrad_acc
 
 _FUSED_WIDTHS = (256, 512, 768, 1024, 1280, 1536, 2048)
 
@@ -176,25 +176,31 @@ class _GPT2BlockFn(torch.autograd.Function):
         dy2 = dy.reshape(B * T, C)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
+        # weight-gradient GEMMs only accumulate into main_grad: queue them when the engine defers
+        # them behind the input-gradient send (layers.defer_weight_grads); run inline otherwise
+        wdefer = run_or_defer if all(_wants_main_grad(p) for p in (w_qkv, b_qkv, w_o, w_fc, w_p)) else (lambda fn: fn())
         # MLP branch
-        wgrad_acc(g_wp, f.t(), dy2)
+        wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2))
         df = torch.mm(dy2, w_p.t())
         dpre = _bias_gelu_bwd(df, pre, b_fc, g_bfc)
         del df
-        wgrad_acc(g_wfc, h2.t(), dpre)
+        wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre))
         dh2 = torch.mm(dpre, w_fc.t())
         del dpre
         # dy1 = dy + LN2_bwd(dh2); bp grad = colsum(dy), bo grad = colsum(dy1) from the same pass
         dy1 = _ln_bwd(dh2, y1, ln2_w, mean2, rstd2, g_ln2w, g_ln2b, dres=dy2, sres_acc=g_bp, sdx_acc=g_bo)
         del dh2
         # attention branch
-        wgrad_acc(g_wo, o2.t(), dy1)
+        wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1))
         do = torch.mm(dy1, w_o.t())
         dqkv = attn_bwd(qkv.view(B, T, 3 * C), o2.view(B, T, C), lse, do.view(B, T, C), H, True, scale)
         del do
         dqkv2 = dqkv.view(B * T, 3 * C)
-        _colsum_into(g_bqkv, dqkv2)
-        wgrad_acc(g_wqkv, h1.t(), dqkv2)
+
+        def _qkv_grads(dqkv2=dqkv2):
+            _colsum_into(g_bqkv, dqkv2)
+            wgrad_acc(g_wqkv, h1.t(), dqkv2)
+        wdefer(_qkv_grads)
         dx = None
         if ctx.needs_input_grad[0]:
             dh1 = torch.mm(dqkv2, w_qkv.t())

@@ -135,10 +135,14 @@ class _BatchNormActNHWC(torch.autograd.Function):
         mean = torch.empty(C, dtype=torch.float32, device=y.device)
         rstd = torch.empty_like(mean)
         upd = training and running_mean is not None
+        # the backward's replicated reduction buffer, zeroed by this forward kernel
+        ws = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(C)), dtype=torch.float32, device=y.device) \
+            if training else None
         _lib.call("tdl_bn_act_fwd", ptr(y), ptr(stats if training else None), ptr(running_mean), ptr(running_var),
                   ptr(gamma), ptr(beta), ptr(res), ptr(out), ptr(mean), ptr(rstd),
-                  ptr(running_mean if upd else None), ptr(running_var if upd else None), M, C, float(eps),
+                  ptr(running_mean if upd else None), ptr(running_var if upd else None), ptr(ws), M, C, float(eps),
                   float(momentum), int(relu), stream_ptr(y.device))
+        ctx.ws = ws
         ctx.save_for_backward(y, out, mean, rstd, gamma, beta)
         ctx.cfg = (M, C, relu, residual is not None, training)
         return out
@@ -155,7 +159,7 @@ class _BatchNormActNHWC(torch.autograd.Function):
             dout = dout.to(y.dtype)
         dx = torch.empty_like(y, memory_format=torch.channels_last)
         dres = torch.empty_like(y, memory_format=torch.channels_last) if has_res else None
-        sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        sums = ctx.ws
         mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
         dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
         db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)

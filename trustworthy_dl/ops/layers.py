@@ -36,6 +36,46 @@ def _accumulate(param: Optional[torch.Tensor], grad: Optional[torch.Tensor]):
     return None
 
 
+# ---------------------------------------------------------------- deferred weight gradients
+# Inside ``defer_weight_grads()`` the fused backward ops queue their weight-gradient GEMMs (which
+# only accumulate into fp32 ``main_grad``) instead of running them: the pipeline engine computes a
+# stage's input gradient first, posts it to the previous stage, and only then runs the queued
+# weight-gradient work while the transfer (and the upstream stage's backward) proceeds — the
+# cooldown of a 1F1B schedule then advances one stage per B_input instead of per full backward
+# (the B/W split of zero-bubble pipeline schedules).
+_DEFER: Optional[list] = None
+
+
+class defer_weight_grads:
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+        self.pending: list = []
+
+    def __enter__(self):
+        global _DEFER
+        self._prev = _DEFER
+        if self.enabled:
+            _DEFER = self.pending
+        return self
+
+    def __exit__(self, *exc):
+        global _DEFER
+        _DEFER = self._prev
+        return False
+
+    def run(self):
+        pending, self.pending = self.pending, []
+        for fn in pending:
+            fn()
+
+
+def run_or_defer(fn) -> None:
+    if _DEFER is not None:
+        _DEFER.append(fn)
+    else:
+        fn()
+
+
 def _wants_main_grad(p: Optional[torch.Tensor]) -> bool:
     return p is not None and getattr(p, "main_grad", None) is not None
 
@@ -454,7 +494,11 @@ class _LinearT(torch.autograd.Function):
             dx, gw = blaslt.linear_t_bwd(x2, weight, dy2, ctx.needs_input_grad[0])
         else:
             dx = (dy2 @ weight) if ctx.needs_input_grad[0] else None
-            gw = _wgrad_into(weight, dy2.t(), x2)
+            if _wants_main_grad(weight):
+                run_or_defer(lambda: _wgrad_into(weight, dy2.t(), x2))
+                gw = None
+            else:
+                gw = _wgrad_into(weight, dy2.t(), x2)
         return (dx.reshape(ctx.shape) if dx is not None else None), gw
 
 

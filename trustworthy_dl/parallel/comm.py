@@ -43,6 +43,14 @@ class P2PComm:
                  recv_prev: Optional[Tuple[torch.Size, torch.dtype]] = None,
                  recv_next: Optional[Tuple[torch.Size, torch.dtype]] = None):
         """One grouped exchange. Returns (tensor_from_prev, tensor_from_next)."""
+        return self.wait(self.post(send_next, send_prev, recv_prev, recv_next))
+
+    def post(self, send_next: Optional[torch.Tensor] = None, send_prev: Optional[torch.Tensor] = None,
+             recv_prev: Optional[Tuple[torch.Size, torch.dtype]] = None,
+             recv_next: Optional[Tuple[torch.Size, torch.dtype]] = None):
+        """Issue a grouped exchange without waiting: work enqueued on the compute stream between
+        ``post`` and ``wait`` (e.g. deferred weight gradients) overlaps the transfer instead of
+        queueing behind the receive.  The sends read their tensors as of the ``post`` call."""
         ops, from_prev, from_next = [], None, None
         if send_next is not None and self.next is not None:
             t = send_next.contiguous()
@@ -58,7 +66,17 @@ class P2PComm:
         if recv_next is not None and self.next is not None:
             from_next = torch.empty(recv_next[0], dtype=recv_next[1], device=self.device)
             ops.append(dist.P2POp(dist.irecv, from_next, self.next, self.group))
-        self._run(ops)
+        t0 = time.perf_counter()
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        self.wait_seconds += time.perf_counter() - t0
+        return reqs, from_prev, from_next
+
+    def wait(self, handle):
+        reqs, from_prev, from_next = handle
+        t0 = time.perf_counter()
+        for r in reqs:
+            r.wait()
+        self.wait_seconds += time.perf_counter() - t0
         return from_prev, from_next
 
 

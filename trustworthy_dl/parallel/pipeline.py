@@ -35,6 +35,7 @@ import torch.nn as nn
 from ..core.trust_manager import (METRIC_NAMES, NodeStatus, STATUS_CODES, STATUS_FROM_CODE, TrustManager)
 from ..security import stage_verifier as SV
 from ..ops import stats as dstats
+from ..ops.layers import defer_weight_grads
 from .comm import P2PComm, all_gather_rows, batched_transfer
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
@@ -63,6 +64,7 @@ class EngineConfig:
     min_stages: int = 1
     output_check: str = "first"          # which micro-batch output is monitored: first|none
     compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
+    defer_wgrad: bool = True             # B/W split: weight grads run after dx is posted upstream
     seed: int = 0
 
 
@@ -319,12 +321,22 @@ class PipelineEngine:
                     torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
             return y
 
+        defer_w = self.cfg.defer_wgrad and not first
+
         def bwd(x, y, dy):
-            if last:
-                y.backward()
-            else:
-                torch.autograd.backward(y, dy)
-            return None if first else x.grad
+            """Input-gradient backward; the weight-gradient GEMMs are queued (ops.layers
+            .defer_weight_grads) and run by the caller AFTER dx has been posted upstream."""
+            with defer_weight_grads(defer_w) as dw:
+                if last:
+                    y.backward()
+                else:
+                    torch.autograd.backward(y, dy)
+            return (None if first else x.grad), dw
+
+        def send_dx_then_w(dx, dw, recv_prev=None):
+            h = comm.post(send_prev=dx, recv_prev=recv_prev)
+            dw.run()  # overlaps the transfer and the upstream stage's backward
+            return comm.wait(h)[0]
 
         for i in range(warm):
             x = get_input(i)
@@ -343,23 +355,26 @@ class PipelineEngine:
             in_q.append(x)
             out_q.append(y)
             x0, y0 = in_q.popleft(), out_q.popleft()
-            dx = bwd(x0, y0, dy)
+            dx, dw = bwd(x0, y0, dy)
             if j == rem - 1:
                 if not first:
-                    comm.exchange(send_prev=dx)
+                    send_dx_then_w(dx, dw)
+                dw.run()
             else:
                 if first:
+                    dw.run()
                     x = get_input(i + 1)
                 else:
-                    x, _ = comm.exchange(send_prev=dx, recv_prev=(in_shape, act_dtype))
+                    x = send_dx_then_w(dx, dw, recv_prev=(in_shape, act_dtype))
         for _ in range(warm):
             x0, y0 = in_q.popleft(), out_q.popleft()
             dy = None
             if not last:
                 _, dy = comm.exchange(recv_next=(out_shape, act_dtype))
-            dx = bwd(x0, y0, dy)
+            dx, dw = bwd(x0, y0, dy)
             if not first:
-                comm.exchange(send_prev=dx)
+                send_dx_then_w(dx, dw)
+            dw.run()
         self._comm_wait = comm.wait_seconds - waited0
         return total[0]
 
