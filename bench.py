@@ -65,6 +65,8 @@ def main():
                     help="sequences per micro-batch, or 'auto' (pipeline-bubble vs GEMM-efficiency model)")
     ap.add_argument("--no-verify", action="store_true", help="disable detection/verification (ablation)")
     ap.add_argument("--lr", type=float, default=5e-5)
+    ap.add_argument("--dp", type=int, default=1,
+                    help="data-parallel pipeline replicas (default 1: the headline is MP = N stages)")
     ap.add_argument("--profile-steps", type=int, default=0)
     args = ap.parse_args()
 
@@ -88,12 +90,15 @@ def main():
     from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
 
     N = world
+    dp = max(1, args.dp)
+    stages = N // dp
     global_batch = args.batch_per_gpu * N
-    mbs = choose_mbs(global_batch, N) if args.mbs == "auto" else int(args.mbs)
-    M = global_batch // mbs
+    per_replica = global_batch // dp
+    mbs = choose_mbs(per_replica, stages) if args.mbs == "auto" else int(args.mbs)
+    M = per_replica // mbs
     model = get_model(args.model, seq_len=args.seq_len, seed=1234)
     verify = not args.no_verify
-    cfg = EngineConfig(num_nodes=N, micro_batches=M, seq_len=args.seq_len,
+    cfg = EngineConfig(num_nodes=N, micro_batches=M, seq_len=args.seq_len, data_parallel=dp,
                        adamw=AdamWConfig(lr=args.lr, weight_decay=0.01, max_grad_norm=1.0),
                        attack_detection=verify, gradient_verification=verify, quarantine=verify,
                        reassign=False)
@@ -138,7 +143,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic tokens, random-init weights",
             "config": {"model": args.model, "global_batch": global_batch, "seq_len": args.seq_len,
-                       "micro_batch": mbs, "micro_batches": M, "parallelism": f"pp{N}",
+                       "micro_batch": mbs, "micro_batches": M,
+                       "parallelism": f"pp{stages}" + (f"xdp{dp}" if dp > 1 else ""),
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
                        "plan": engine.plan.describe(), "last_loss": engine.last_loss},
         }

@@ -44,7 +44,9 @@ class TrainingConfig:
     reassignment_enabled: bool = True
     quarantine_enabled: bool = True
     trust_decay_per_step: float = 0.01
-    parallelism: str = "model"
+    parallelism: str = "model"           # "model" (pipeline) | "hybrid" (pipeline x data-parallel replicas)
+    data_parallel: int = 1                # pipeline replicas (world size = stages x replicas)
+    defer_wgrad: bool = True              # B/W split in the 1F1B schedule
     num_classes: Optional[int] = None
     image_size: Optional[int] = None
     batches_per_epoch: Optional[int] = None
@@ -97,6 +99,8 @@ def load_config(path: str, overrides: Optional[Dict[str, Any]] = None):
         tc["parallelism"] = ds["parallelism"]
     if "micro_batches" in ds:
         tc["micro_batches"] = ds["micro_batches"]
+    if "data_parallel" in ds:
+        tc["data_parallel"] = int(ds["data_parallel"])
     sec = raw.get("security", {}) or {}
     mapping = {"trust_threshold": "trust_threshold", "attack_detection": "attack_detection_enabled",
                "gradient_verification": "gradient_verification_enabled", "reassignment": "reassignment_enabled",
@@ -119,7 +123,8 @@ def dump_config(cfg: TrainingConfig, attack: Optional[AttackSection], path: str)
         "model": {"name": d.pop("model_name"), "size": d.pop("model_size")},
         "training": {k: d.pop(k) for k in ("batch_size", "learning_rate", "num_epochs", "seq_len",
                                            "micro_batches", "dataset_name")},
-        "distributed": {"num_nodes": d.pop("num_nodes"), "parallelism": d.pop("parallelism")},
+        "distributed": {"num_nodes": d.pop("num_nodes"), "parallelism": d.pop("parallelism"),
+                        "data_parallel": d.pop("data_parallel")},
         "security": {"trust_threshold": d.pop("trust_threshold"),
                      "attack_detection": d.pop("attack_detection_enabled"),
                      "gradient_verification": d.pop("gradient_verification_enabled")},

@@ -65,6 +65,10 @@ class EngineConfig:
     output_check: str = "first"          # which micro-batch output is monitored: first|none
     compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
     defer_wgrad: bool = True             # B/W split: weight grads run after dx is posted upstream
+    data_parallel: int = 1               # pipeline replicas (distributed): world = stages x replicas
+    robust_aggregation: bool = True      # DP: flagged / outlier replicas are left out of the gradient mean
+    outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
+    param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     seed: int = 0
 
 
@@ -90,6 +94,14 @@ class PipelineEngine:
         self.rank = dist.get_rank() if self.distributed else 0
         self.world = dist.get_world_size() if self.distributed else 1
         self.num_nodes = self.world if self.distributed else cfg.num_nodes
+        # data parallelism over pipeline replicas: rank = replica * pp + stage position
+        self.dp = max(1, int(cfg.data_parallel)) if self.distributed else 1
+        if self.world % self.dp:
+            raise ValueError(f"world size {self.world} not divisible by data_parallel={self.dp}")
+        self.pp = self.world // self.dp if self.distributed else cfg.num_nodes
+        self.replica = self.rank // self.pp if self.distributed else 0
+        self.dp_group = None
+        self.dp_audits: List[Dict] = []
         self.trust = trust_manager or TrustManager(self.num_nodes, cfg.trust_threshold)
         self.trust.resize(self.num_nodes)
         self.attacker = attacker
@@ -129,8 +141,9 @@ class PipelineEngine:
             self.costs = model.layer_costs()
         else:
             self.costs = [1.0] * self.num_layers
-        n_stages = min(self.num_nodes, self.num_layers)
-        self.plan = make_plan(self.costs, list(range(n_stages)), 0, cfg.balanced_partition)
+        n_stages = min(self.pp, self.num_layers)
+        base = self.replica * self.pp
+        self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
         self._init_trust_state()
         self._build()
         logger.info("PipelineEngine[%s] plan: %s", "dist" if self.distributed else "local", self.plan.describe())
@@ -170,12 +183,21 @@ class PipelineEngine:
         prev = self.plan.ranks[s - 1] if s is not None and s > 0 else None
         nxt = self.plan.ranks[s + 1] if s is not None and s + 1 < self.plan.num_stages else None
         self.comm = P2PComm(prev, nxt, self.device)
-        # tied parameters living on different ranks need a gradient all-reduce group
-        members = sorted({self.plan.owner_of_layer(li) for grp in self.ties for li, _ in grp})
-        self.tie_members = members if len(members) > 1 else []
-        if self.tie_members:
-            # new_group is collective over the whole world
-            self.tie_group = dist.new_group(ranks=self.tie_members)
+        # tied parameters living on different ranks need a gradient all-reduce group (one per
+        # replica; new_group is collective over the whole world, so every rank creates them all)
+        base = self.replica * self.pp
+        local = sorted({self.plan.owner_of_layer(li) - base for grp in self.ties for li, _ in grp})
+        self.tie_members = [base + r for r in local] if len(local) > 1 else []
+        if len(local) > 1:
+            for d in range(self.dp):
+                g = dist.new_group(ranks=[d * self.pp + r for r in local])
+                if d == self.replica:
+                    self.tie_group = g
+        if self.dp > 1 and self.dp_group is None:
+            for pos in range(self.pp):
+                g = dist.new_group(ranks=[d * self.pp + pos for d in range(self.dp)])
+                if pos == self.rank % self.pp:
+                    self.dp_group = g
 
     def _init_trust_state(self):
         N = self.num_nodes
@@ -218,8 +240,11 @@ class PipelineEngine:
             batch = self.attacker.apply_attacks(batch, self.global_step)
             truth.update(getattr(self.attacker, "last_batch_truth", {}) or {})
         M = self.cfg.micro_batches
-        inputs = split_micro(batch["input"], M)
-        targets = split_micro(batch["target"], M)
+        inp, tgt = batch["input"], batch["target"]
+        if self.dp > 1:
+            inp, tgt = inp.chunk(self.dp, 0)[self.replica], tgt.chunk(self.dp, 0)[self.replica]
+        inputs = split_micro(inp, M)
+        targets = split_micro(tgt, M)
         if self.distributed:
             loss = self._run_1f1b(inputs, targets, truth)
         else:
@@ -455,9 +480,12 @@ class PipelineEngine:
             D = torch.zeros(N, SV.DIGEST, dtype=torch.float32, device=self.device)
             for node, d in rows:
                 D[node].copy_(d.to(self.device))
-        # global gradient norm for clipping (sum of per-stage sumsq), trust update on identical data
-        total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
-        present_nodes = list(self.plan.ranks)
+        if self.dp > 1:
+            total_sumsq = self._dp_aggregate(D)
+        else:
+            # global gradient norm for clipping (sum of per-stage sumsq), trust update on identical data
+            total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
+        present_nodes = self.all_ranks()
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
         raw = torch.maximum(D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG]).to(torch.int32)
         # a single flag quarantines that step's update; k consecutive flags compromise the node
@@ -479,6 +507,8 @@ class PipelineEngine:
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
             st.flat.adamw_step(self.cfg.adamw, ctrl=st.verifier.ctrl)
+        if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
+            self._audit_params()
         # queue the host report (pinned, non-blocking)
         rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float()])
         if rep.is_cuda:
@@ -489,6 +519,103 @@ class PipelineEngine:
         else:
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
+
+    # ================================================================== data parallelism (pipeline replicas)
+    def all_ranks(self) -> List[int]:
+        """Every rank holding a stage: the plan's ranks in each replica."""
+        if self.dp == 1:
+            return list(self.plan.ranks)
+        base = self.replica * self.pp
+        return [d * self.pp + (r - base) for d in range(self.dp) for r in self.plan.ranks]
+
+    def last_ranks(self) -> List[int]:
+        base = self.replica * self.pp
+        return [d * self.pp + (self.plan.ranks[-1] - base) for d in range(self.dp)]
+
+    def _dp_group_ranks(self) -> List[int]:
+        pos = self.rank % self.pp
+        return [d * self.pp + pos for d in range(self.dp)]
+
+    def _dp_aggregate(self, D: torch.Tensor) -> torch.Tensor:
+        """Byzantine-robust gradient mean across this stage's replicas, all on device.
+
+        A replica is left out when its own verifier flagged the gradient, it produced non-finite
+        values, its node is COMPROMISED, or (>= 3 replicas) its gradient norm is an outlier
+        against the replicas' median.  Each rank scales its flat gradient by ok / n_ok and the
+        replicas all-reduce (sum) -> mean of the trusted replicas; if none is trusted the step is
+        skipped on every replica (weights stay identical).  Returns the global sum of squares of the
+        aggregated gradient (for clipping), from one extra scalar all-reduce."""
+        st = self.my_stage()
+        ranks = self._dp_group_ranks()
+        idx = torch.tensor(ranks, dtype=torch.long, device=self.device)
+        rows = D[idx]
+        bad = torch.maximum(rows[:, SV.D_GRAD_FLAG], (rows[:, SV.D_NONFINITE] > 0).float())
+        bad = torch.maximum(bad, (self.t_status[idx] == STATUS_CODES[NodeStatus.COMPROMISED]).float())
+        if len(ranks) >= 3:
+            norms = rows[:, SV.D_GRAD_L2]
+            med = norms.median()
+            ratio = norms / torch.clamp(med, min=1e-30)
+            tau = float(self.cfg.outlier_ratio)
+            bad = torch.maximum(bad, ((ratio > tau) | (ratio < 1.0 / tau)).float())
+        if not self.cfg.robust_aggregation:
+            bad = torch.zeros_like(bad)
+        ok = 1.0 - bad
+        n_ok = ok.sum()
+        me = ranks.index(self.rank)
+        w = ok[me] / torch.clamp(n_ok, min=1.0)
+        if st is not None:
+            st.flat.grad.mul_(w)
+            dist.all_reduce(st.flat.grad, group=self.dp_group)
+            st.verifier.ctrl[1:2].copy_((n_ok < 0.5).float().reshape(1))
+            sq = (st.flat.grad * st.flat.grad).sum().reshape(1)
+        else:
+            sq = torch.zeros(1, device=self.device)
+        self._dp_excluded = bad
+        dist.all_reduce(sq)
+        return (sq / self.dp).reshape(())
+
+    @torch.no_grad()
+    def _audit_params(self):
+        """Cross-replica weight audit: replicas must hold bit-identical fp32 master weights.  A
+        replica whose digest (float64 sum, sum of squares) differs from the majority of its stage
+        position was tampered with (parameter perturbation / model poisoning): every rank sees the
+        same all-gathered digests, so every rank records it and marks the node compromised in the
+        device trust state identically; the stage's replicas then re-synchronise (fp32 master and
+        AdamW moments broadcast from a majority member).  One small host read every few steps."""
+        st = self.my_stage()
+        if st is not None:
+            m = st.flat.master.double()
+            dg = torch.stack([m.sum(), (m * m).sum()])
+        else:
+            dg = torch.zeros(2, dtype=torch.float64, device=self.device)
+        G = all_gather_rows(dg, self.world).cpu()
+        my_pos = self.rank % self.pp
+        for pos in range(self.pp):
+            ranks = [d * self.pp + pos for d in range(self.dp)]
+            rows = [tuple(G[r].tolist()) for r in ranks]
+            counts: Dict[tuple, int] = {}
+            for r in rows:
+                counts[r] = counts.get(r, 0) + 1
+            majority, votes = max(counts.items(), key=lambda kv: kv[1])
+            divergent = [ranks[i] for i, r in enumerate(rows) if r != majority]
+            if not divergent:
+                continue
+            src = ranks[rows.index(majority)] if votes * 2 > len(ranks) else None
+            rec = {"step": self.global_step, "timestamp": time.time(), "attack_type": "model_poisoning",
+                   "divergent_nodes": divergent, "resync_from": src, "stage_position": pos}
+            self.dp_audits.append(rec)
+            logger.warning("parameter audit: replicas %s diverge from the majority (resync from %s)", divergent, src)
+            for n in divergent:
+                self.attack_history.append({"node_id": n, "timestamp": rec["timestamp"], "step": self.global_step,
+                                            "attack_type": "model_poisoning", "ground_truth": None})
+                self.trust.mark_compromised(n, "model_poisoning")
+                self.t_values[n] = 0.1
+                self.t_status[n] = STATUS_CODES[NodeStatus.COMPROMISED]
+            if pos == my_pos and src is not None and st is not None:
+                for buf in st.flat.optimizer_state_tensors():
+                    dist.broadcast(buf, src, group=self.dp_group)
+                if st.flat.data is not st.flat.master:
+                    st.flat.data.copy_(st.flat.master)
 
     # ================================================================== host-side report processing
     def flush(self) -> Optional[float]:
@@ -507,10 +634,9 @@ class PipelineEngine:
         D = host[: N * SV.DIGEST].view(N, SV.DIGEST).tolist()
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
         statuses = [int(v) for v in host[N * SV.DIGEST + N:].tolist()]
-        present = set(self.plan.ranks)
-        loss_rows = [r[SV.D_LOSS] for n, r in enumerate(D) if n in present and r[SV.D_PRESENT] > 0]
-        last_node = self.plan.ranks[-1]
-        self.last_loss = D[last_node][SV.D_LOSS] if D[last_node][SV.D_PRESENT] > 0 else None
+        present = set(self.all_ranks())
+        lasts = [n for n in self.last_ranks() if D[n][SV.D_PRESENT] > 0]
+        self.last_loss = sum(D[n][SV.D_LOSS] for n in lasts) / len(lasts) if lasts else None
         detections = []
         for n in range(N):
             row = D[n]
@@ -575,6 +701,11 @@ class PipelineEngine:
     def reassign(self, compromised: Sequence[int], step: Optional[int] = None):
         """Exclude ``compromised`` nodes and re-partition every layer over the remaining trusted
         ones, migrating weights + optimizer state (distributed_trainer.py:324-380, made real)."""
+        if self.dp > 1:
+            # replicas keep identical layouts; a compromised replica member is excluded from the
+            # gradient mean (robust aggregation) and re-synchronised by the parameter audit instead
+            logger.warning("DP=%d: nodes %s excluded from aggregation (no re-shard)", self.dp, list(compromised))
+            return
         attempts = sum(1 for r in self.reassignment_history if set(r["from_nodes"]) & set(compromised))
         if attempts >= self.cfg.max_reassignment_attempts:
             logger.warning("max reassignment attempts reached for %s", compromised)
@@ -695,7 +826,10 @@ class PipelineEngine:
     def eval_step(self, batch: Dict[str, torch.Tensor]) -> float:
         """Forward-only loss over the global batch (no detector side effects: reference A21 fixed)."""
         M = self.cfg.micro_batches
-        inputs, targets = split_micro(batch["input"], M), split_micro(batch["target"], M)
+        inp, tgt = batch["input"], batch["target"]
+        if self.dp > 1:
+            inp, tgt = inp.chunk(self.dp, 0)[self.replica], tgt.chunk(self.dp, 0)[self.replica]
+        inputs, targets = split_micro(inp, M), split_micro(tgt, M)
         total = torch.zeros((), dtype=torch.float32, device=self.device)
         if not self.distributed:
             for i in range(M):
@@ -720,7 +854,7 @@ class PipelineEngine:
                 else:
                     self.comm.exchange(send_next=y)
         dist.all_reduce(total)
-        return float(total)
+        return float(total) / self.dp
 
     # ================================================================== checkpoint state
     def stage_state_dicts(self) -> Dict[int, Dict[str, torch.Tensor]]:
