@@ -7,6 +7,10 @@ loader yields *synthetic* data of the right shape (documented in the batch's ``"
 flag): deterministic per (seed, split, index).  A local directory of ``.npy`` token shards or
 a torchvision-style CIFAR folder can be plugged in through ``data_dir``.
 Batches are dicts ``{"input": Tensor, "target": Tensor}`` (distributed_trainer.py:395, 398).
+
+``native=True`` (language modelling) switches to the C++ loader (runtime/native.py,
+csrc/runtime/token_loader.cpp): worker threads fill a pinned ring from a memory-mapped raw token
+file (``token_file``, uint16/uint32) or synthetic ids, ahead of the training loop.
 """
 from __future__ import annotations
 
@@ -79,10 +83,16 @@ class SyntheticImages:
 
 def get_dataloader(dataset_name: str, split: str = "train", batch_size: int = 32, seq_len: int = 1024,
                    num_batches: Optional[int] = None, seed: int = 0, data_dir: Optional[str] = None,
-                   vocab_size: int = 50257, pin_memory: bool = False):
+                   vocab_size: int = 50257, pin_memory: bool = False, native: bool = False,
+                   token_file: Optional[str] = None, token_bytes: int = 2, rank: int = 0, world: int = 1):
     name = dataset_name.lower()
     nb = num_batches if num_batches is not None else (100 if split == "train" else 10)
     if "text" in name or name in ("openwebtext", "wikitext", "tokens", "lm"):
+        if native or token_file:
+            from ..runtime.native import NativeTokenLoader
+            return NativeTokenLoader(batch_size, seq_len, path=token_file, vocab_size=vocab_size,
+                                     token_bytes=token_bytes, seed=seed + (0 if split == "train" else 10_000),
+                                     num_batches=nb, rank=rank, world=world, pin_memory=pin_memory or None)
         return SyntheticLanguageModeling(batch_size, seq_len, vocab_size, nb, seed, split, data_dir, pin_memory)
     if name in ("cifar10", "cifar-10", "cifar"):
         return SyntheticImages(batch_size, 32, 10, nb, seed, split, pin_memory)
