@@ -393,6 +393,7 @@ class DistributedTrainer:
     def cleanup(self):
         if self.engine is not None:
             self.engine.flush()
+            self.engine.close()
         if self._owns_pg and dist.is_initialized():
             dist.destroy_process_group()
         logger.info("Distributed training cleanup completed")

@@ -69,6 +69,9 @@ class EngineConfig:
     robust_aggregation: bool = True      # DP: flagged / outlier replicas are left out of the gradient mean
     outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
+    heartbeat_interval: float = 0.0      # distributed: seconds between heartbeats (0 = watchdog off)
+    heartbeat_timeout: float = 30.0      # silence after which a peer is OFFLINE
+    abort_on_offline: bool = False       # fail fast so an elastic launcher restarts from a checkpoint
     seed: int = 0
 
 
@@ -146,6 +149,13 @@ class PipelineEngine:
         self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
         self._init_trust_state()
         self._build()
+        self.heartbeat = None
+        self.node_events: List[Dict] = []
+        if self.distributed and cfg.heartbeat_interval > 0:
+            from ..runtime.heartbeat import HeartbeatMonitor
+            store = dist.distributed_c10d._get_default_store()
+            self.heartbeat = HeartbeatMonitor(store, self.rank, self.world, cfg.heartbeat_interval,
+                                              cfg.heartbeat_timeout, abort_on_offline=cfg.abort_on_offline).start()
         logger.info("PipelineEngine[%s] plan: %s", "dist" if self.distributed else "local", self.plan.describe())
 
     # ================================================================== construction
@@ -475,7 +485,11 @@ class PipelineEngine:
             rows.append((node, d))
         if self.distributed:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
+            if self.heartbeat is not None:
+                mine[SV.D_OFFLINE_MASK] = float(sum(1 << n for n in self.heartbeat.offline() if n < 24))
             D = all_gather_rows(mine, self.world)
+            if self.heartbeat is not None:
+                self._apply_offline(D)
         else:
             D = torch.zeros(N, SV.DIGEST, dtype=torch.float32, device=self.device)
             for node, d in rows:
@@ -519,6 +533,27 @@ class PipelineEngine:
         else:
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
+
+    # ================================================================== heartbeat -> OFFLINE
+    def _apply_offline(self, D: torch.Tensor):
+        """A node is OFFLINE while any rank's watchdog reports it silent (union of the all-gathered
+        bitmasks, identical on every rank); a node no rank reports any more goes RECOVERING.
+        Device-side, so every rank's trust state moves identically without a host sync."""
+        N = self.num_nodes
+        bits = D[:, SV.D_OFFLINE_MASK].to(torch.int64)
+        shifts = torch.arange(N, device=self.device, dtype=torch.int64)
+        off = ((bits[:, None] >> shifts[None, :]) & 1).amax(0).to(torch.bool)
+        OFF = STATUS_CODES[NodeStatus.OFFLINE]
+        was_off = self.t_status == OFF
+        self.t_status.copy_(torch.where(off, torch.full_like(self.t_status, OFF),
+                                        torch.where(was_off, torch.full_like(self.t_status,
+                                                                             STATUS_CODES[NodeStatus.RECOVERING]),
+                                                    self.t_status)))
+
+    def close(self):
+        if self.heartbeat is not None:
+            self.heartbeat.stop()
+            self.heartbeat = None
 
     # ================================================================== data parallelism (pipeline replicas)
     def all_ranks(self) -> List[int]:
@@ -680,6 +715,11 @@ class PipelineEngine:
                 "trust_scores": {i: values[i] for i in range(N)},
                 "detections": detections, "grad_norm": [D[n][SV.D_GRAD_L2] for n in range(N)],
                 "step_time": self._step_time})
+        OFF = STATUS_CODES[NodeStatus.OFFLINE]
+        for n in range(N):
+            if (statuses[n] == OFF) != (prev_status.get(n) == NodeStatus.OFFLINE):
+                self.node_events.append({"node_id": n, "step": step, "timestamp": time.time(),
+                                         "event": "offline" if statuses[n] == OFF else "online"})
         newly = [n for n in range(N) if n in present and statuses[n] == STATUS_CODES[NodeStatus.COMPROMISED]
                  and prev_status.get(n) != NodeStatus.COMPROMISED]
         newly += [n for n in range(N) if n in present and statuses[n] == STATUS_CODES[NodeStatus.COMPROMISED]
