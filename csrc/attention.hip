@@ -19,6 +19,16 @@
 //          dQ^T += K^T.dS^T with dS^T as the B operand.  +2 recomputed products, zero atomics.
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
+// Block-order mode: default = every head's block y dispatched together across heads (LPT over the
+// whole grid); TDL_ATTN_MAP=xcd -> one head's blocks back to back on one XCD (head_xcd_map).
+static int attn_nbh_arg(int nbh) {
+    const char* e = std::getenv("TDL_ATTN_MAP");
+    return (e && std::strcmp(e, "xcd") == 0) ? -nbh : nbh;
+}
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
@@ -46,25 +56,46 @@ __device__ __forceinline__ bf16x8_t cvt8(const f32x16& v, int base) {
 
 constexpr int HD = 64;
 
+// Workgroup -> (batch*head, block) with the nb blocks of one head on ONE XCD, dispatched back to
+// back (heaviest causal block first): the dispatcher sends workgroup L to XCD L % 8, so L = 8 j + x
+// puts stream position j of XCD x on head 8 (j / nb) + x.  The head's K/V (fwd, dQ) or Q/dO (dK/dV)
+// tiles are then fetched into that XCD's L2 once and shared by its co-resident workgroups — the
+// earlier (B*H, T/128) grid streamed every head's K/V from HBM once per q-block wave.
+__device__ __forceinline__ void head_xcd_map(int L, int nbh, int nb, bool causal, int& bh, int& blk) {
+    const bool per_xcd = nbh < 0;  // sign carries the mapping mode (host: TDL_ATTN_MAP=xcd)
+    nbh = per_xcd ? -nbh : nbh;
+    if (per_xcd && (nbh & 7) == 0) {
+        const int xcd = L & 7, j = L >> 3;
+        const int hq = j % nb;
+        bh = (j / nb) * 8 + xcd;
+        blk = causal ? nb - 1 - hq : hq;
+    } else {
+        bh = L % nbh;
+        const int y = L / nbh;
+        blk = causal ? nb - 1 - y : y;
+    }
+}
+
 // ============================================================================ forward
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// Grid is (B*H, T/128) with the query block taken in REVERSE order of blockIdx.y: the dispatcher
-// walks x fastest, so every head's longest causal rows go out first (longest-processing-time-first
-// over the 256 CUs) instead of the short rows of head 0 followed by the long rows of head 0.
+// 1-D grid of B*H*(T/128) workgroups mapped by head_xcd_map: one head's query blocks run back to
+// back on one XCD, longest causal rows first (longest-processing-time-first inside each head).
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                       float* __restrict__ lse, int T, int H, float scale_log2) {
+                                                       float* __restrict__ lse, int T, int H, int nbh, float scale_log2) {
     constexpr int BM = 128, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][BN * HD];
     __shared__ __attribute__((aligned(16))) bf16_t Vs[2][BN * HD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
+    int bh, qb;
+    head_xcd_map(blockIdx.x, nbh, T / BM, CAUSAL, bh, qb);
+    const int b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
     const bf16_t* vbase = qbase + 2 * H * HD;
-    const int qblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BM;
+    const int qblk = qb * BM;
     const int q0 = qblk + 32 * w;
     const int qi = q0 + r;
     const int qrow = qi < T ? qi : T - 1;
@@ -123,43 +154,46 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                 s0 = MFMA32(a0, qf[s], s0);
                 s1 = MFMA32(a1, qf[s], s1);
             }
-            float mx = -1e30f;
+            // row max on the raw scores (scale > 0 commutes with max); the scale folds into the
+            // exponent's fma: p = exp2(s * scale_log2 - m) -> one fma + one v_exp per score
+            float mx = -INFINITY;
             if (CAUSAL && kb * BN + BN - 1 > q0) {  // diagonal tile of this wave: mask keys > query
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const float v0 = key0 > qi ? -INFINITY : s0[i] * scale_log2;
-                    const float v1 = key0 + 32 > qi ? -INFINITY : s1[i] * scale_log2;
+                    const float v0 = key0 > qi ? -INFINITY : s0[i];
+                    const float v1 = key0 + 32 > qi ? -INFINITY : s1[i];
                     s0[i] = v0;
                     s1[i] = v1;
                     mx = fmaxf(mx, fmaxf(v0, v1));
                 }
             } else {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    s0[i] *= scale_log2;
-                    s1[i] *= scale_log2;
-                    mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
-                }
+                for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
             }
             mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float mn = fmaxf(m, mx);
-            const float alpha = fast_exp2(m - mn);
+            const float mn = fmaxf(m, mx * scale_log2);
+            // exact skip of the O / l rescale when no row of the wave raised its running max
+            // (alpha == 1 for every lane): the common case once the first tiles have been seen
+            if (__any(mn > m)) {
+                const float alpha = fast_exp2(m - mn);
+                l *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    o0[i] *= alpha;
+                    o1[i] *= alpha;
+                }
+            }
             float rs = 0.f;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                s0[i] = fast_exp2(s0[i] - mn);
-                s1[i] = fast_exp2(s1[i] - mn);
+                s0[i] = fast_exp2(fmaf(s0[i], scale_log2, -mn));
+                s1[i] = fast_exp2(fmaf(s1[i], scale_log2, -mn));
                 rs += s0[i] + s1[i];
             }
             rs += __shfl_xor(rs, 32, 64);
-            l = l * alpha + rs;
+            l += rs;
             m = mn;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                o0[i] *= alpha;
-                o1[i] *= alpha;
-            }
             const bf16x8_t p00 = cvt8(s0, 0), p01 = cvt8(s0, 8), p10 = cvt8(s1, 0), p11 = cvt8(s1, 8);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -195,10 +229,11 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
                          int causal, hipStream_t s) {
     (void)unused;
     if (D != HD || T % 64 != 0) return (int)hipErrorInvalidValue;
-    const dim3 grid(B * H, (T + 127) / 128);
+    if (T % 128 != 0) return (int)hipErrorInvalidValue;
+    const int grid = B * H * (T / 128);
     const float sl2 = scale * 1.4426950408889634f;
-    if (causal) attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
-    else attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, sl2);
+    if (causal) attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, attn_nbh_arg(B * H), sl2);
+    else attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16_t*)qkv, (bf16_t*)out, lse, T, H, attn_nbh_arg(B * H), sl2);
     TDL_LAUNCH_CHECK();
 }
 
@@ -232,14 +267,18 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
-                                                            bf16_t* __restrict__ dqkv, int T, int H, float scale) {
+                                                            bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
     constexpr int BK = 128, BQ = 32;
     __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
     __shared__ float lse_s[2][BQ], delta_s[2][BQ];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
+    int bh, kbi;
+    // causal dK/dV: key block 0 sees every query -> it is the heavy one; reverse the LPT order
+    head_xcd_map(blockIdx.x, nbh, T / BK, CAUSAL, bh, kbi);
+    if (CAUSAL) kbi = T / BK - 1 - kbi;
+    const int b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD, ldo = H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
@@ -247,8 +286,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
     const float* lse_row = lse + (size_t)bh * T;
     const float* delta_row = delta + (size_t)bh * T;
-    // heavy (long causal) key blocks first, across all heads (grid (B*H, T/128), x fastest)
-    const int kblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BK;
+    const int kblk = kbi * BK;
     const int k0 = kblk + 32 * w;
     const int kj = k0 + r;
 
@@ -356,19 +394,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          bf16_t* __restrict__ dqkv, int T, int H, float scale) {
+                                                          bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
     constexpr int BM = 128, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Kr[2][BN * HD];  // swizzled, row reads
     __shared__ __attribute__((aligned(16))) bf16_t Kp[2][BN * HD];  // plain, transposed reads
     __shared__ __attribute__((aligned(16))) bf16_t Vr[2][BN * HD];  // swizzled, row reads
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
-    const int bh = blockIdx.x, b = bh / H, hd = bh - b * H;
+    int bh, qb;
+    head_xcd_map(blockIdx.x, nbh, T / BM, CAUSAL, bh, qb);  // heavy (late) query blocks first
+    const int b = bh / H, hd = bh - b * H;
     const int ldq = 3 * H * HD, ldo = H * HD;
     const bf16_t* qbase = qkv + (size_t)b * T * ldq + hd * HD;
     const bf16_t* kbase = qbase + H * HD;
     const bf16_t* vbase = qbase + 2 * H * HD;
     const bf16_t* dobase = dout + (size_t)b * T * ldo + hd * HD;
-    const int qblk = (CAUSAL ? (gridDim.y - 1 - blockIdx.y) : blockIdx.y) * BM;  // heavy blocks first
+    const int qblk = qb * BM;
     const int q0 = qblk + 32 * w;
     const int qi = q0 + r;
     const float lse_q = lse[(size_t)bh * T + qi] * 1.4426950408889634f;
@@ -480,16 +520,16 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     (void)unused;
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
     attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
-    const dim3 grid(B * H, T / 128);
+    const int grid = B * H * (T / 128);
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;
     auto dQKV = (bf16_t*)dqkv;
     if (causal) {
-        attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
-        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+        attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
+        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
     } else {
-        attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
-        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, scale);
+        attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
+        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
     }
     TDL_LAUNCH_CHECK();
 }
