@@ -566,3 +566,70 @@ TDL_API int tdl_kl_div_softmax(const float* a, const float* b, int R, int C, flo
     kl_kernel<<<R, 256, 0, s>>>(a, b, R, C, out);
     TDL_LAUNCH_CHECK();
 }
+
+// ============================================================================ parameter integrity
+// Deterministic checksum of a bf16 weight buffer: (sum, sum of squares, position-weighted sum) in
+// fp64.  Element -> block assignment, per-thread order and both reduction trees are fixed, so bit-
+// identical data gives a bit-identical checksum: the engine compares the checksum of a stage's
+// compute weights taken right after its optimizer step with the one taken before the next update —
+// any write outside the optimizer (parameter perturbation, memory corruption) shows up.
+namespace {
+constexpr int CK_BLOCKS = 512;
+
+__global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __restrict__ x, int64_t n,
+                                                               int64_t per_block, double* __restrict__ part) {
+    __shared__ double red[3][4];
+    const int64_t beg = (int64_t)blockIdx.x * per_block;
+    const int64_t end = beg + per_block < n ? beg + per_block : n;
+    double s = 0.0, q = 0.0, w = 0.0;
+    for (int64_t i = beg + threadIdx.x * 8; i < end; i += 256 * 8) {
+        float f[8];
+        if (i + 8 <= end) {
+            unpack8(*(const uint4*)(x + i), f);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = i + e < end ? bf2f(x[i + e]) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const double v = (double)f[e];
+            s += v;
+            q += v * v;
+            w += v * (double)((i + e) % 1021 + 1);
+        }
+    }
+    s = wave_sum_d(s);
+    q = wave_sum_d(q);
+    w = wave_sum_d(w);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wid] = s;
+        red[1][wid] = q;
+        red[2][wid] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const double* r = red[threadIdx.x];
+        part[(int64_t)blockIdx.x * 3 + threadIdx.x] = ((r[0] + r[1]) + r[2]) + r[3];
+    }
+}
+
+__global__ void checksum_final_kernel(const double* __restrict__ part, int nb, double* __restrict__ out) {
+    if (threadIdx.x < 3) {
+        double a = 0.0;
+        for (int b = 0; b < nb; ++b) a += part[b * 3 + threadIdx.x];
+        out[threadIdx.x] = a;
+    }
+}
+}  // namespace
+
+// out: 3 doubles; ws: 3 * 512 doubles.  n bf16 elements, 16-byte aligned base.
+TDL_API int tdl_checksum_bf16(const void* x, int64_t n, double* ws, double* out, hipStream_t s) {
+    if (((uintptr_t)x & 15) != 0) return (int)hipErrorInvalidValue;
+    int64_t per_block = (n + CK_BLOCKS - 1) / CK_BLOCKS;
+    per_block = (per_block + 7) / 8 * 8;
+    const int nb = (int)((n + per_block - 1) / per_block);
+    checksum_partial_kernel<<<nb > 0 ? nb : 1, 256, 0, s>>>((const bf16_t*)x, n, per_block, ws);
+    checksum_final_kernel<<<1, 64, 0, s>>>(ws, nb > 0 ? nb : 1, out);
+    TDL_LAUNCH_CHECK();
+}

@@ -140,3 +140,28 @@ def test_trainer_facade_checkpoint_roundtrip(tmp_path):
     assert tr2.global_step == 8
     assert tr2.engine.eval_step(batch) == pytest.approx(ref, rel=1e-6)
     assert tr2.trust_manager.get_trust_score(0) == pytest.approx(tr.trust_manager.get_trust_score(0))
+
+
+def test_parameter_tampering_caught_by_integrity_checksum():
+    atk = AdversarialAttacker(AttackConfig(["model_poisoning"], target_nodes=[1], intensity=0.05, start_step=12,
+                                           end_step=14))
+    atk.activate_attacks()
+    eng = _engine(nodes=3, attacker=atk, reassign=False)
+    for b in _batches(18):
+        eng.train_step(b)
+    eng.flush()
+    hits = [r for r in eng.attack_history if r["attack_type"] == "model_poisoning"]
+    assert sorted({r["step"] for r in hits}) == [12, 13, 14] and {r["node_id"] for r in hits} == {1}
+    m = atk.detection_metrics()
+    assert m["recall"] == 1.0 and m["precision"] == 1.0
+
+
+def test_byzantine_blame_goes_to_the_earliest_stage_only():
+    atk = AdversarialAttacker(AttackConfig(["byzantine"], target_nodes=[0], intensity=0.5, start_step=20))
+    atk.activate_attacks()
+    eng = _engine(nodes=3, attacker=atk, reassign=False)
+    for b in _batches(26):
+        eng.train_step(b)
+    eng.flush()
+    blamed = {r["node_id"] for r in eng.attack_history if r["step"] >= 20}
+    assert blamed == {0}   # downstream output echoes and upstream gradient echoes are not blamed

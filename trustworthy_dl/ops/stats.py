@@ -281,3 +281,19 @@ def cosine_gram(xs: List[torch.Tensor]) -> torch.Tensor:
     nrm = X.norm(dim=1).clamp(min=1e-30)
     G = X @ X.t()
     return G / (nrm[:, None] * nrm[None, :])
+
+
+def checksum(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Deterministic (sum, sum of squares, position-weighted sum) of a flat buffer, float64 [3].
+    Bit-identical data -> bit-identical result (fixed reduction order; csrc/stats.hip)."""
+    x = x.reshape(-1)
+    if out is None:
+        out = torch.empty(3, dtype=torch.float64, device=x.device)
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.data_ptr() % 16 == 0:
+        ws = torch.empty(3 * 512, dtype=torch.float64, device=x.device)
+        _lib.call("tdl_checksum_bf16", ptr(x), x.numel(), ptr(ws), ptr(out), stream_ptr(x.device))
+        return out
+    v = x.double()
+    w = (torch.arange(v.numel(), dtype=torch.float64, device=v.device) % 1021) + 1
+    out.copy_(torch.stack([v.sum(), (v * v).sum(), (v * w).sum()]))
+    return out

@@ -69,6 +69,8 @@ class EngineConfig:
     robust_aggregation: bool = True      # DP: flagged / outlier replicas are left out of the gradient mean
     outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
+    param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
+    attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     heartbeat_interval: float = 0.0      # distributed: seconds between heartbeats (0 = watchdog off)
     heartbeat_timeout: float = 30.0      # silence after which a peer is OFFLINE
     abort_on_offline: bool = False       # fail fast so an elastic launcher restarts from a checkpoint
@@ -482,6 +484,8 @@ class PipelineEngine:
             hm = self._host_metric_row(node)
             d = st.verifier.finish_step(st.flat.grad, loss if st.computes_loss else None, hm,
                                         truth.get(node, False), st.stage_id)
+            if self.cfg.param_integrity:
+                d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].copy_(self._integrity_flag(st))
             rows.append((node, d))
         if self.distributed:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
@@ -501,7 +505,8 @@ class PipelineEngine:
             total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
         present_nodes = self.all_ranks()
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
-        raw = torch.maximum(D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG]).to(torch.int32)
+        blame = self._attribute(D)
+        raw = blame.to(torch.int32)
         # a single flag quarantines that step's update; k consecutive flags compromise the node
         self.t_flagrun.copy_((self.t_flagrun + 1) * raw)
         flags = (self.t_flagrun >= max(1, self.cfg.compromise_after)).to(torch.int32)
@@ -521,10 +526,12 @@ class PipelineEngine:
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
             st.flat.adamw_step(self.cfg.adamw, ctrl=st.verifier.ctrl)
+            if self.cfg.param_integrity:
+                st.param_checksum = dstats.checksum(st.flat.data, getattr(st, "param_checksum", None))
         if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
             self._audit_params()
         # queue the host report (pinned, non-blocking)
-        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float()])
+        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float(), blame.float()])
         if rep.is_cuda:
             host = torch.empty(rep.shape, dtype=rep.dtype, pin_memory=True)
             host.copy_(rep, non_blocking=True)
@@ -533,6 +540,46 @@ class PipelineEngine:
         else:
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
+
+    # ================================================================== integrity + attribution
+    @torch.no_grad()
+    def _integrity_flag(self, st: Stage) -> torch.Tensor:
+        """1.0 when the stage's compute weights differ from the checksum taken right after its last
+        optimizer step (a write outside the optimizer), else 0.0 — device-side, no sync."""
+        cur = dstats.checksum(st.flat.data)
+        ref = getattr(st, "param_checksum", None)
+        if ref is None:  # first step / freshly (re)built or reloaded stage: nothing to compare yet
+            st.param_checksum = cur
+            return torch.zeros(1, dtype=torch.float32, device=st.device)
+        return (cur != ref).any().float().reshape(1)
+
+    def _replica_orders(self) -> List[torch.Tensor]:
+        key = (self.plan.version, self.dp)
+        if getattr(self, "_orders_key", None) != key:
+            base = self.replica * self.pp
+            self._orders = [torch.tensor([d * self.pp + (r - base) for r in self.plan.ranks], dtype=torch.long,
+                                         device=self.device) for d in range(self.dp)]
+            self._orders_key = key
+        return self._orders
+
+    def _attribute(self, D: torch.Tensor) -> torch.Tensor:
+        """Per-node blame for this step, identical on every rank (device, from the all-gathered D).
+
+        In a pipeline an anomaly echoes: tampered activations of stage s make every later stage's
+        output (and, through backward, every stage's gradients) look anomalous too.  Blame goes to
+        (a) any stage whose weights failed the integrity check, (b) the EARLIEST stage of each
+        pipeline replica with an output anomaly, and (c) gradient anomalies only when the replica
+        shows no output / integrity evidence (gradient poisoning does not propagate)."""
+        of, gf, pf = D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG], D[:, SV.D_PARAM_FLAG]
+        if not self.cfg.attribute_flags:
+            return torch.maximum(torch.maximum(of, gf), pf)
+        blame = torch.zeros_like(of)
+        for idx in self._replica_orders():
+            o, g, p = of[idx], gf[idx], pf[idx]
+            first = o * (torch.cumsum(o, 0) == 1).float()
+            evidence = torch.maximum(o.max(), p.max())
+            blame[idx] = torch.maximum(torch.maximum(p, first), g * (1.0 - evidence))
+        return blame
 
     # ================================================================== heartbeat -> OFFLINE
     def _apply_offline(self, D: torch.Tensor):
@@ -651,6 +698,7 @@ class PipelineEngine:
                     dist.broadcast(buf, src, group=self.dp_group)
                 if st.flat.data is not st.flat.master:
                     st.flat.data.copy_(st.flat.master)
+                st.param_checksum = None
 
     # ================================================================== host-side report processing
     def flush(self) -> Optional[float]:
@@ -668,7 +716,8 @@ class PipelineEngine:
         N = self.num_nodes
         D = host[: N * SV.DIGEST].view(N, SV.DIGEST).tolist()
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
-        statuses = [int(v) for v in host[N * SV.DIGEST + N:].tolist()]
+        statuses = [int(v) for v in host[N * SV.DIGEST + N:N * SV.DIGEST + 2 * N].tolist()]
+        blamed = [v > 0 for v in host[N * SV.DIGEST + 2 * N:].tolist()]
         present = set(self.all_ranks())
         lasts = [n for n in self.last_ranks() if D[n][SV.D_PRESENT] > 0]
         self.last_loss = sum(D[n][SV.D_LOSS] for n in lasts) / len(lasts) if lasts else None
@@ -679,8 +728,10 @@ class PipelineEngine:
                 continue
             gt = bool(row[SV.D_ATTACK_TRUTH] > 0)
             out_flag, grad_flag = row[SV.D_OUT_FLAG] > 0, row[SV.D_GRAD_FLAG] > 0
-            if out_flag or grad_flag:
-                kind = "gradient_poisoning" if grad_flag else "output_anomaly"
+            param_flag = row[SV.D_PARAM_FLAG] > 0
+            flagged = blamed[n]
+            if flagged:
+                kind = "model_poisoning" if param_flag else ("output_anomaly" if out_flag else "gradient_poisoning")
                 rec = {"node_id": n, "timestamp": time.time(), "step": step, "attack_type": kind,
                        "output_stats": {"mean": row[SV.D_OUT_MEAN], "std": row[SV.D_OUT_STD],
                                         "z": row[SV.D_OUT_Z]},
@@ -694,15 +745,15 @@ class PipelineEngine:
                 detections.append(n)
             if self.detector is not None:
                 ds = self.detector.detection_stats
-                flagged = out_flag or grad_flag
                 if flagged:
                     ds["total_detections"] += 1
-                    ds["attack_types"]["gradient_poisoning" if grad_flag else "byzantine"] += 1
+                    k = "model_poisoning" if param_flag else ("byzantine" if out_flag else "gradient_poisoning")
+                    ds["attack_types"][k] = ds["attack_types"].get(k, 0) + 1
                 key = ("true_positives" if gt else "false_positives") if flagged else \
                       ("false_negatives" if gt else "true_negatives")
                 ds[key] += 1
             if self.attacker is not None and hasattr(self.attacker, "record_detection"):
-                self.attacker.record_detection(n, step, out_flag or grad_flag, gt)
+                self.attacker.record_detection(n, step, flagged, gt)
         metrics = [row[SV.D_METRICS:SV.D_METRICS + 6] for row in D]
         prev_status = {n: self.trust.get_node_status(n) for n in range(N)}
         self.trust.ingest_device_update([values[n] for n in range(N)], [statuses[n] for n in range(N)], metrics,
@@ -940,3 +991,4 @@ class PipelineEngine:
                         b.copy_(model_sd[node][n])
             if verifier_sd and node in verifier_sd:
                 st.verifier.load_state_dict(verifier_sd[node])
+            st.param_checksum = None  # weights legitimately replaced

@@ -29,6 +29,7 @@ D_METRICS = 5  # 6 trust metrics: output_deviation, gradient_consistency, latenc
 D_GRAD_SUMSQ, D_OUT_MEAN, D_OUT_STD, D_GRAD_L2, D_NONFINITE, D_GRAD_COS = 11, 12, 13, 14, 15, 16
 D_ATTACK_TRUTH, D_PRESENT, D_STAGE, D_OUT_CONF, D_GRAD_CONF = 17, 18, 19, 20, 21
 D_OFFLINE_MASK = 22  # bitmask of the peers this rank's heartbeat watchdog sees offline
+D_PARAM_FLAG = 23    # compute weights changed outside the optimizer (integrity checksum mismatch)
 DIGEST = 24
 
 

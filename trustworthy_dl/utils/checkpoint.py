@@ -95,7 +95,9 @@ def load_checkpoint(trainer, path: str):
     e = trainer.engine
     ck = consolidate(path)
     saved_plan = PlacementPlan.from_list(ck["plan"])
-    if saved_plan.ranks != e.plan.ranks or saved_plan.ranges != e.plan.ranges:
+    # with data-parallel replicas the manifest holds replica 0's plan; replicas share its layout
+    same_ranks = saved_plan.ranks == e.plan.ranks or getattr(e, "dp", 1) > 1
+    if not same_ranks or saved_plan.ranges != e.plan.ranges:
         if all(r < e.num_nodes for r in saved_plan.ranks):
             e.plan = saved_plan
             e._build()
