@@ -372,3 +372,18 @@ def test_wgrad_splitk_accumulates(M, K, N):
     assert wgrad_split(M, K, N) > 1
     wgrad_acc(acc, x.t(), dy)
     assert float((acc - ref).norm() / ref.norm()) < 1e-3
+
+
+@pytest.mark.gpu
+def test_weight_checksum_deterministic_and_sensitive():
+    from trustworthy_dl.ops.stats import checksum
+    x = torch.randn(3_000_001, device="cuda").to(torch.bfloat16)
+    a, b = checksum(x).clone(), checksum(x).clone()
+    assert torch.equal(a, b)  # bit-identical on identical data
+    v = x.double().cpu()
+    w = (torch.arange(v.numel(), dtype=torch.float64) % 1021) + 1
+    ref = torch.stack([v.sum(), (v * v).sum(), (v * w).sum()])
+    assert torch.allclose(a.cpu(), ref, rtol=1e-9, atol=1e-6)
+    y = x.clone()
+    y[1_234_567] = (y[1_234_567].float() * 1.01).to(torch.bfloat16)  # one weight nudged
+    assert not torch.equal(checksum(y), a)

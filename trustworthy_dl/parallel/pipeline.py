@@ -71,6 +71,7 @@ class EngineConfig:
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
+    pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
     heartbeat_interval: float = 0.0      # distributed: seconds between heartbeats (0 = watchdog off)
     heartbeat_timeout: float = 30.0      # silence after which a peer is OFFLINE
     abort_on_offline: bool = False       # fail fast so an elastic launcher restarts from a checkpoint
@@ -153,6 +154,7 @@ class PipelineEngine:
         self._build()
         self.heartbeat = None
         self.node_events: List[Dict] = []
+        self.quarantine_on_evidence = cfg.quarantine and cfg.pipeline_quarantine
         if self.distributed and cfg.heartbeat_interval > 0:
             from ..runtime.heartbeat import HeartbeatMonitor
             store = dist.distributed_c10d._get_default_store()
@@ -498,14 +500,20 @@ class PipelineEngine:
             D = torch.zeros(N, SV.DIGEST, dtype=torch.float32, device=self.device)
             for node, d in rows:
                 D[node].copy_(d.to(self.device))
+        blame, evidence = self._attribute(D)
+        if self.quarantine_on_evidence:
+            # a tampered forward (output anomaly / failed integrity check anywhere in the pipeline)
+            # taints every gradient of the step: skip the update on all of the replica's stages, so
+            # the damage does not echo into the next step's outputs
+            for node, st in self.stages.items():
+                st.verifier.ctrl[1:2].copy_(torch.maximum(st.verifier.ctrl[1:2], evidence[node:node + 1].to(st.device)))
         if self.dp > 1:
-            total_sumsq = self._dp_aggregate(D)
+            total_sumsq = self._dp_aggregate(D, evidence)
         else:
             # global gradient norm for clipping (sum of per-stage sumsq), trust update on identical data
             total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
         present_nodes = self.all_ranks()
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
-        blame = self._attribute(D)
         raw = blame.to(torch.int32)
         # a single flag quarantines that step's update; k consecutive flags compromise the node
         self.t_flagrun.copy_((self.t_flagrun + 1) * raw)
@@ -563,7 +571,8 @@ class PipelineEngine:
         return self._orders
 
     def _attribute(self, D: torch.Tensor) -> torch.Tensor:
-        """Per-node blame for this step, identical on every rank (device, from the all-gathered D).
+        """Per-node (blame, evidence) for this step, identical on every rank (device, from the
+        all-gathered D); ``evidence[n]`` = 1 when n's pipeline replica saw a tampered forward.
 
         In a pipeline an anomaly echoes: tampered activations of stage s make every later stage's
         output (and, through backward, every stage's gradients) look anomalous too.  Blame goes to
@@ -571,15 +580,18 @@ class PipelineEngine:
         pipeline replica with an output anomaly, and (c) gradient anomalies only when the replica
         shows no output / integrity evidence (gradient poisoning does not propagate)."""
         of, gf, pf = D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG], D[:, SV.D_PARAM_FLAG]
-        if not self.cfg.attribute_flags:
-            return torch.maximum(torch.maximum(of, gf), pf)
         blame = torch.zeros_like(of)
+        evidence = torch.zeros_like(of)
         for idx in self._replica_orders():
             o, g, p = of[idx], gf[idx], pf[idx]
-            first = o * (torch.cumsum(o, 0) == 1).float()
-            evidence = torch.maximum(o.max(), p.max())
-            blame[idx] = torch.maximum(torch.maximum(p, first), g * (1.0 - evidence))
-        return blame
+            ev = torch.maximum(o.max(), p.max())
+            if self.cfg.attribute_flags:
+                first = o * (torch.cumsum(o, 0) == 1).float()
+                blame[idx] = torch.maximum(torch.maximum(p, first), g * (1.0 - ev))
+            else:
+                blame[idx] = torch.maximum(torch.maximum(o, g), p)
+            evidence[idx] = ev.expand(idx.numel())
+        return blame, evidence
 
     # ================================================================== heartbeat -> OFFLINE
     def _apply_offline(self, D: torch.Tensor):
@@ -618,7 +630,7 @@ class PipelineEngine:
         pos = self.rank % self.pp
         return [d * self.pp + pos for d in range(self.dp)]
 
-    def _dp_aggregate(self, D: torch.Tensor) -> torch.Tensor:
+    def _dp_aggregate(self, D: torch.Tensor, evidence: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Byzantine-robust gradient mean across this stage's replicas, all on device.
 
         A replica is left out when its own verifier flagged the gradient, it produced non-finite
@@ -633,6 +645,8 @@ class PipelineEngine:
         rows = D[idx]
         bad = torch.maximum(rows[:, SV.D_GRAD_FLAG], (rows[:, SV.D_NONFINITE] > 0).float())
         bad = torch.maximum(bad, (self.t_status[idx] == STATUS_CODES[NodeStatus.COMPROMISED]).float())
+        if evidence is not None:
+            bad = torch.maximum(bad, evidence[idx])  # the replica's forward was tampered
         if len(ranks) >= 3:
             norms = rows[:, SV.D_GRAD_L2]
             med = norms.median()
