@@ -72,6 +72,8 @@ class EngineConfig:
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
+    p2p_mode: str = "async"              # "async": per-direction communicators + receives posted a phase
+                                         # ahead; "grouped": one batch_isend_irecv per exchange
     heartbeat_interval: float = 0.0      # distributed: seconds between heartbeats (0 = watchdog off)
     heartbeat_timeout: float = 30.0      # silence after which a peer is OFFLINE
     abort_on_offline: bool = False       # fail fast so an elastic launcher restarts from a checkpoint
@@ -197,6 +199,11 @@ class PipelineEngine:
         prev = self.plan.ranks[s - 1] if s is not None and s > 0 else None
         nxt = self.plan.ranks[s + 1] if s is not None and s + 1 < self.plan.num_stages else None
         self.comm = P2PComm(prev, nxt, self.device)
+        if self.cfg.p2p_mode == "async" and getattr(self, "_dir_groups", None) is None:
+            # one communicator for activations (stage s -> s+1), one for activation gradients
+            # (s+1 -> s): each carries one-way, in-order traffic per neighbour pair
+            everyone = list(range(self.world))
+            self._dir_groups = (dist.new_group(ranks=everyone), dist.new_group(ranks=everyone))
         # tied parameters living on different ranks need a gradient all-reduce group (one per
         # replica; new_group is collective over the whole world, so every rank creates them all)
         base = self.replica * self.pp
@@ -316,6 +323,8 @@ class PipelineEngine:
 
     # ------------------------------------------------------------------ distributed 1F1B schedule
     def _run_1f1b(self, inputs, targets, truth) -> Optional[torch.Tensor]:
+        if self.cfg.p2p_mode == "async":
+            return self._run_1f1b_async(inputs, targets, truth)
         st = self.my_stage()
         if st is None:
             return None
@@ -415,6 +424,132 @@ class PipelineEngine:
                 send_dx_then_w(dx, dw)
             dw.run()
         self._comm_wait = comm.wait_seconds - waited0
+        return total[0]
+
+    def _run_1f1b_async(self, inputs, targets, truth) -> Optional[torch.Tensor]:
+        """1F1B with latency-hiding point-to-point transfers.
+
+        Activations travel on one process group and activation gradients on another, so every
+        communicator carries one-way traffic per neighbour pair in issue order (deadlock-free for
+        any interleaving of the two directions).  Each receive is posted one compute phase ahead
+        of its use — the next input before this stage's backward, the next output gradient before
+        its forward — so the xGMI transfer overlaps compute instead of adding a full transfer
+        latency to every pipeline hop (the grouped exchange serialises send and receive behind
+        both neighbours' compute).  On each direction's stream a send is always issued before the
+        next receive, so a ready send never queues behind a pending receive.  The compute stream
+        never waits for a send; all sends are drained at the end of the step.  Weight gradients
+        (B/W split) run after the input gradient is posted."""
+        st = self.my_stage()
+        if st is None:
+            return None
+        node = self.rank
+        M = len(inputs)
+        S = self.plan.num_stages
+        s = st.stage_id
+        first, last = s == 0, s == S - 1
+        self._attack_params(node, st, truth)
+        in_shape, out_shape = self._boundary_shapes(st, inputs[0])
+        act_pg, grad_pg = self._dir_groups
+        prev, nxt = self.comm.prev, self.comm.next
+        dt = self.dtype
+        warm = min(S - s - 1, M)
+        rem = M - warm
+        in_q: deque = deque()
+        out_q: deque = deque()
+        sends: List = []
+        total = [None]
+        waited = [0.0]
+        defer_w = self.cfg.defer_wgrad and not first
+
+        def post_recv(shape, src, group):
+            buf = torch.empty(shape, dtype=dt, device=st.device)
+            return dist.irecv(buf, src, group=group), buf
+
+        def take(h):
+            t0 = time.perf_counter()
+            h[0].wait()
+            waited[0] += time.perf_counter() - t0
+            return h[1]
+
+        def post_x(i):
+            return None if first or i >= M else post_recv(in_shape, prev, act_pg)
+
+        def post_dy(i):
+            return None if last or i >= M else post_recv(out_shape, nxt, grad_pg)
+
+        def send(t, dst, group):
+            sends.append(dist.isend(t.contiguous(), dst, group=group))
+            if len(sends) > 8:  # drop finished sends (their tensors are released)
+                sends[:] = [w for w in sends if not w.is_completed()]
+
+        def fwd(i, x):
+            if not first:
+                x.requires_grad_(True)
+            labels = targets[i].to(st.device, non_blocking=True) if last else None
+            y, mon = st.forward(x, labels)
+            if last:
+                y = y / M
+                total[0] = y.detach() if total[0] is None else total[0] + y.detach()
+            else:
+                y = self._attack_output(node, y, truth)
+                if i == 0:
+                    mon = y
+            if i == 0 and mon is not None and self.cfg.output_check != "none":
+                st.verifier.observe_output(mon)
+                if last and st.verifier.side is not None:
+                    torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
+            return y
+
+        def bwd(x, y, dy):
+            with defer_weight_grads(defer_w) as dw:
+                if last:
+                    y.backward()
+                else:
+                    torch.autograd.backward(y, dy)
+            return (None if first else x.grad), dw
+
+        def input_of(i, h):
+            return self._stage_input(inputs[i], st) if first else take(h)
+
+        x_h = post_x(0)
+        for i in range(warm):                      # warm > 0 implies not last
+            x = input_of(i, x_h)
+            y = fwd(i, x)
+            send(y, nxt, act_pg)
+            x_h = post_x(i + 1)
+            in_q.append(x)
+            out_q.append(y)
+        for j in range(rem):
+            i = warm + j
+            x = input_of(i, x_h)
+            dy_h = post_dy(j)                      # arrives while this forward runs
+            y = fwd(i, x)
+            if not last:
+                send(y, nxt, act_pg)
+            x_h = post_x(i + 1)                    # arrives while the backward below runs
+            in_q.append(x)
+            out_q.append(y)
+            x0, y0 = in_q.popleft(), out_q.popleft()
+            dy = None if last else take(dy_h)
+            dx, dw = bwd(x0, y0, dy)
+            if not first:
+                send(dx, prev, grad_pg)
+            dw.run()
+        dy_h = post_dy(rem) if warm > 0 else None
+        for c in range(warm):
+            b = rem + c
+            dy = take(dy_h)
+            x0, y0 = in_q.popleft(), out_q.popleft()
+            dx, dw = bwd(x0, y0, dy)
+            if not first:
+                send(dx, prev, grad_pg)
+            dy_h = post_dy(b + 1)                  # after the send: no send queues behind it
+            dw.run()
+        t0 = time.perf_counter()
+        for w in sends:
+            w.wait()
+        waited[0] += time.perf_counter() - t0
+        self._comm_wait = waited[0]
         return total[0]
 
     def _boundary_shapes(self, st: Stage, sample_in: torch.Tensor):
