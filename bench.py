@@ -31,14 +31,17 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# Measured single-GPU throughput of GPT-2-medium (k tokens/s, MI355X, r1 micro-batch sweep,
-# scripts/gpu_sweep_mbs.sh) per micro-batch size: larger micro-batches feed the GEMMs and the
-# attention kernels larger tiles.  Used only to choose the micro-batch size.
-_MBS_EFF = {4: 215.9, 8: 245.7, 16: 270.4, 32: 278.8}
+# Measured single-GPU throughput of GPT-2-medium (k tokens/s, MI355X, scripts/gpu_sweep_mbs.sh after
+# the split-K weight gradients and attention changes) per micro-batch size: larger micro-batches feed
+# the GEMMs and the attention kernels larger tiles.  Used only to choose the micro-batch size.
+_MBS_EFF = {4: 224.9, 8: 276.8, 16: 325.7, 32: 335.1}
+# fill/drain slot cost relative to a steady-state slot: with the B/W split the drain advances one
+# stage per (F + B_input) ~ 2/3 of a full (F + B_input + W) slot
+_BUBBLE_WEIGHT = 2.0 / 3.0
 
 
 def choose_mbs(global_batch: int, stages: int) -> int:
-    """1F1B step time ~ (M + S - 1) micro-batch slots of mbs / eff(mbs) each (M = batch / mbs):
+    """1F1B step time ~ (M + w (S - 1)) micro-batch slots of mbs / eff(mbs) each (M = batch / mbs):
     few big micro-batches run efficient kernels but leave a long fill/drain bubble."""
     best, best_t = None, float("inf")
     for mbs, eff in _MBS_EFF.items():
@@ -47,7 +50,7 @@ def choose_mbs(global_batch: int, stages: int) -> int:
         m = global_batch // mbs
         if m < stages and stages > 1:
             continue
-        t = (m + stages - 1) * mbs / eff
+        t = (m + _BUBBLE_WEIGHT * (stages - 1)) * mbs / eff
         if t < best_t:
             best, best_t = mbs, t
     return best or 1
