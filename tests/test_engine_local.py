@@ -165,3 +165,66 @@ def test_byzantine_blame_goes_to_the_earliest_stage_only():
     eng.flush()
     blamed = {r["node_id"] for r in eng.attack_history if r["step"] >= 20}
     assert blamed == {0}   # downstream output echoes and upstream gradient echoes are not blamed
+
+
+def test_half_block_pair_on_one_stage_runs_fused_and_matches():
+    eng = _engine(nodes=3, reassign=False, layer_granularity="half")
+    from trustworthy_dl.models.gpt2 import FusedHalfPair
+    assert any(isinstance(r, FusedHalfPair) for st in eng.stages.values() for r in st._runners())
+    ref = _engine(nodes=3, reassign=False, layer_granularity="block")
+    for b in _batches(3):
+        eng.train_step(b)
+        ref.train_step(b)
+        eng.flush()
+        ref.flush()
+        assert eng.last_loss == pytest.approx(ref.last_loss, rel=1e-4, abs=1e-5)
+
+
+def test_half_block_granularity_matches_block_granularity():
+    """Attention / MLP halves as pipeline units compute the same function and updates as whole
+    blocks; a stage holding both halves of a block runs them as one fused pair."""
+    losses = {}
+    for g in ("block", "half"):
+        eng = _engine(nodes=4, reassign=False, layer_granularity=g)
+        assert eng.granularity == g
+        if g == "half":
+            # stage boundaries inside blocks: embed+attn0 | mlp0+attn1 | mlp1 | head
+            assert eng.num_layers == 2 * 2 + 2
+            assert eng.plan.ranges == [(0, 2), (2, 4), (4, 5), (5, 6)]
+        losses[g] = []
+        for b in _batches(4):
+            eng.train_step(b)
+            eng.flush()
+            losses[g].append(eng.last_loss)
+    assert losses["block"] == pytest.approx(losses["half"], rel=1e-4, abs=1e-5)
+
+
+def test_auto_granularity_prefers_half_blocks_for_gpt2_medium_8_stages():
+    m = get_model("gpt2-medium")
+    for g, want in (("block", 0.80), ("half", 0.93)):
+        m.set_pipeline_granularity(g)
+        costs = m.layer_costs(1024)
+        parts = balanced_partition(costs, 8)
+        per = [sum(costs[a:b]) for a, b in parts]
+        assert sum(per) / 8 / max(per) > want
+    m.set_pipeline_granularity("block")
+
+
+def test_checkpoint_restores_half_block_layout(tmp_path):
+    """A checkpoint written with half-block units loads into a job configured for whole blocks:
+    the manifest's granularity is adopted so its plan's layer indices keep their meaning."""
+    from trustworthy_dl import DistributedTrainer
+    kw = dict(model_name="gpt2-tiny", num_nodes=4, seq_len=32, micro_batches=2, batch_size=8,
+              checkpoint_dir=str(tmp_path), device="cpu")
+    tr = DistributedTrainer(checkpoint_interval=0, batches_per_epoch=2, layer_granularity="half", **kw)
+    tr.train(dataset="openwebtext", epochs=1)
+    assert tr.engine.granularity == "half"
+    path = tr.save_checkpoint()
+    batch = next(_batches(1, seed=5))
+    ref = tr.engine.eval_step(batch)
+    tr2 = DistributedTrainer(layer_granularity="block", **kw)
+    tr2.create_model_partitions()
+    assert tr2.engine.granularity == "block"
+    tr2.load_checkpoint(path)
+    assert tr2.engine.granularity == "half" and tr2.engine.plan.ranges == tr.engine.plan.ranges
+    assert tr2.engine.eval_step(batch) == pytest.approx(ref, rel=1e-6)

@@ -305,6 +305,28 @@ def test_gpt2_engine_step_matches_cpu():
     assert abs(losses["cpu"] - losses["cuda:0"]) < 0.05 * losses["cpu"], losses
 
 
+def test_gpt2_half_block_stages_match_block_stages_on_gpu():
+    """Stage boundaries inside blocks (unpaired attention / MLP halves, bf16 native kernels) give
+    the same training trajectory as whole-block stages."""
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    torch.manual_seed(0)
+    ids = torch.randint(0, 50257, (4, 129))
+    batch = {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+    losses = {}
+    for g in ("block", "half"):
+        m = get_model("gpt2-mini", seq_len=128, seed=3)
+        eng = PipelineEngine(m, EngineConfig(num_nodes=4, micro_batches=2, seq_len=128, device="cuda:0",
+                                             layer_granularity=g, reassign=False))
+        if g == "half":
+            assert any((b - a) % 2 for a, b in eng.plan.ranges[1:-1]), eng.plan.ranges
+        for _ in range(4):
+            eng.train_step(batch)
+        eng.flush()
+        losses[g] = eng.last_loss
+    assert abs(losses["block"] - losses["half"]) < 0.02 * losses["block"], losses
+
+
 @pytest.mark.parametrize("N", [1024, 768])
 def test_add_bias_ln_and_residual_ln_bwd(N):
     """tdl_add_bias_ln_fwd and the residual/colsum variant of LN backward vs fp32 torch."""

@@ -47,6 +47,7 @@ class TrainingConfig:
     parallelism: str = "model"           # "model" (pipeline) | "hybrid" (pipeline x data-parallel replicas)
     data_parallel: int = 1                # pipeline replicas (world size = stages x replicas)
     defer_wgrad: bool = True              # B/W split in the 1F1B schedule
+    layer_granularity: str = "auto"       # pipeline units: "block" | "half" (GPT-2 attn/MLP) | "auto"
     num_classes: Optional[int] = None
     image_size: Optional[int] = None
     batches_per_epoch: Optional[int] = None
@@ -101,6 +102,8 @@ def load_config(path: str, overrides: Optional[Dict[str, Any]] = None):
         tc["micro_batches"] = ds["micro_batches"]
     if "data_parallel" in ds:
         tc["data_parallel"] = int(ds["data_parallel"])
+    if "layer_granularity" in ds:
+        tc["layer_granularity"] = str(ds["layer_granularity"])
     sec = raw.get("security", {}) or {}
     mapping = {"trust_threshold": "trust_threshold", "attack_detection": "attack_detection_enabled",
                "gradient_verification": "gradient_verification_enabled", "reassignment": "reassignment_enabled",
@@ -124,7 +127,8 @@ def dump_config(cfg: TrainingConfig, attack: Optional[AttackSection], path: str)
         "training": {k: d.pop(k) for k in ("batch_size", "learning_rate", "num_epochs", "seq_len",
                                            "micro_batches", "dataset_name")},
         "distributed": {"num_nodes": d.pop("num_nodes"), "parallelism": d.pop("parallelism"),
-                        "data_parallel": d.pop("data_parallel")},
+                        "data_parallel": d.pop("data_parallel"),
+                        "layer_granularity": d.pop("layer_granularity")},
         "security": {"trust_threshold": d.pop("trust_threshold"),
                      "attack_detection": d.pop("attack_detection_enabled"),
                      "gradient_verification": d.pop("gradient_verification_enabled")},

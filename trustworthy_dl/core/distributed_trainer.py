@@ -130,7 +130,8 @@ class DistributedTrainer:
             quarantine=c.quarantine_enabled, verifier=dict(c.verifier), trust_threshold=c.trust_threshold,
             trust_decay_per_step=c.trust_decay_per_step, reassign=c.reassignment_enabled,
             max_reassignment_attempts=c.max_reassignment_attempts, seed=c.seed,
-            data_parallel=c.data_parallel, defer_wgrad=c.defer_wgrad)
+            data_parallel=c.data_parallel, defer_wgrad=c.defer_wgrad,
+            layer_granularity=c.layer_granularity)
 
     def create_model_partitions(self, model_name: Optional[str] = None) -> Dict[int, torch.nn.Module]:
         """Build the model, plan a cost-balanced partition over the nodes and instantiate the stages

@@ -122,6 +122,50 @@ class GPT2Block(nn.Module):
         return x + self.mlp(self.ln_2(x))
 
 
+class GPT2HalfBlock(nn.Module):
+    """One residual half of a GPT2Block as its own pipeline unit: ``x + attn(ln_1(x))`` (part
+    "attn") or ``x + mlp(ln_2(x))`` (part "mlp").  Shares the block's submodules, so parameter
+    names inside the unit are the block's own (``ln_1.weight``, ``mlp.c_fc.weight`` ...).
+
+    With half-block granularity a stage boundary may fall between a block's attention and MLP,
+    which halves the partition granule (an MLP is ~0.6 of a block): an 8-stage GPT-2-medium split
+    otherwise leaves whole-block stages of 4 against an ideal of ~3.5.  Both halves of a block on
+    one stage still run as the single fused block op (parallel/stage.py pairs them)."""
+
+    def __init__(self, block: GPT2Block, part: str, index: int):
+        super().__init__()
+        if part not in ("attn", "mlp"):
+            raise ValueError(part)
+        self.part = part
+        self.block_index = index
+        self.fused = block.fused
+        if part == "attn":
+            self.ln_1, self.attn = block.ln_1, block.attn
+        else:
+            self.ln_2, self.mlp = block.ln_2, block.mlp
+
+    def forward(self, x):
+        if self.part == "attn":
+            return x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class FusedHalfPair:
+    """Runs an (attn, mlp) pair of GPT2HalfBlock units of the same block as one fused block op.
+    Not an nn.Module: it only borrows the two units' submodules (no parameter is registered twice)."""
+
+    def __init__(self, attn_half: GPT2HalfBlock, mlp_half: GPT2HalfBlock):
+        self.ln_1, self.attn = attn_half.ln_1, attn_half.attn
+        self.ln_2, self.mlp = mlp_half.ln_2, mlp_half.mlp
+        self._halves = (attn_half, mlp_half)
+        self.fused = attn_half.fused
+
+    def __call__(self, x):
+        if self.fused and ops.fused_block_enabled(x.shape[-1], x.device):
+            return ops.gpt2_block(x, self)
+        return self._halves[1](self._halves[0](x))
+
+
 class GPT2Embedding(nn.Module):
     """wte (padded vocab) + wpe; first pipeline layer. Input: token ids [B, T]."""
     takes_tokens = True
@@ -181,7 +225,15 @@ class GPT2LMHeadModel(nn.Module):
         self.config = cfg
         self.transformer = _Transformer(cfg)
         self.head = GPT2Head(cfg, wte=self.transformer.embed.wte)
+        self.granularity = "block"
+        self._halves: Optional[List[GPT2HalfBlock]] = None  # plain list: not registered twice
         self.reset_parameters(seed)
+
+    def set_pipeline_granularity(self, granularity: str) -> None:
+        """``"block"``: pipeline units are whole blocks; ``"half"``: attention and MLP halves."""
+        if granularity not in ("block", "half"):
+            raise ValueError(f"granularity must be 'block' or 'half', got {granularity!r}")
+        self.granularity = granularity
 
     def reset_parameters(self, seed: Optional[int] = 0):
         """GPT-2 init (normal 0.02; residual projections scaled by 1/sqrt(2L)); deterministic per seed."""
@@ -199,16 +251,33 @@ class GPT2LMHeadModel(nn.Module):
             self.transformer.embed.wte[self.config.vocab_size:].zero_()
 
     def pipeline_layers(self) -> List[nn.Module]:
+        if self.granularity == "half":
+            if self._halves is None:
+                self._halves = [GPT2HalfBlock(b, part, i) for i, b in enumerate(self.transformer.h)
+                                for part in ("attn", "mlp")]
+            return [self.transformer.embed, *self._halves, self.head]
         return [self.transformer.embed, *self.transformer.h, self.head]
 
+    # time per token of each unit relative to 24 n^2 dense-GEMM FLOPs: the attention core and the
+    # pointwise kernels run far from the GEMM rate, the LM head GEMMs close to it.  Calibrated on
+    # MI355X from per-unit fwd+bwd timings of GPT-2-medium at T=1024 (scripts/time_units.py,
+    # profiles/r1_gpt2m_unit_times.jsonl): attn half 0.527, MLP half 0.532, LM head 2.71-2.86 and
+    # embedding 0.13 block-times.
+    _ATTN_CORE_WEIGHT = 2.25     # causal attention FLOPs (4 T n) run at < half the GEMM rate
+    _POINTWISE_PER_BLOCK = 0.12  # LayerNorms, bias-GELU, residual adds: fraction of the block GEMMs
+    _EMBED_PER_BLOCK = 0.13      # gather fwd + wte/wpe scatter-add bwd
+
     def layer_costs(self, seq_len: int) -> List[float]:
-        """Relative fwd+bwd FLOPs per pipeline layer (per token)."""
+        """Relative fwd+bwd time per pipeline unit (per token)."""
         c = self.config
         n, T = c.n_embd, seq_len
-        block = 24 * n * n + 4 * T * n  # dense + causal attention
+        pw = self._POINTWISE_PER_BLOCK * 24 * n * n
+        attn = 8 * n * n + self._ATTN_CORE_WEIGHT * 4 * T * n + 0.4 * pw  # qkv + proj GEMMs + core
+        mlp = 16 * n * n + 0.6 * pw                                         # fc + proj GEMMs + GELU
         head = 2 * n * c.padded_vocab + 10 * c.padded_vocab  # LM head GEMM + softmax/CE passes
-        embed = 0.02 * block
-        return [embed] + [float(block)] * c.n_layer + [float(head)]
+        embed = self._EMBED_PER_BLOCK * (attn + mlp)
+        units = [attn, mlp] if self.granularity == "half" else [attn + mlp]
+        return [embed] + [float(u) for u in units] * c.n_layer + [float(head)]
 
     def forward(self, ids, labels=None):
         h = self.transformer.embed(ids)

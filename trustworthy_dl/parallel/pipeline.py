@@ -72,6 +72,8 @@ class EngineConfig:
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
+    layer_granularity: str = "auto"      # "block" | "half" (GPT-2 attention / MLP halves as pipeline
+                                         # units) | "auto": half when it lowers the slowest stage
     p2p_mode: str = "async"              # "async": per-direction communicators + receives posted a phase
                                          # ahead; "grouped": one batch_isend_irecv per exchange
     heartbeat_interval: float = 0.0      # distributed: seconds between heartbeats (0 = watchdog off)
@@ -121,6 +123,7 @@ class PipelineEngine:
         self.reassignment_history: List[Dict] = []
         self.excluded: List[int] = []
         self.state_flags = {"under_attack": False}
+        self.granularity = self._choose_granularity(model, cfg)
         self.layers = model.pipeline_layers()
         self.num_layers = len(self.layers)
         self.ties = tied_groups(model)
@@ -143,12 +146,7 @@ class PipelineEngine:
         # conv nets run bf16 on the native NHWC implicit-GEMM kernels (ops/conv.py), like GPT-2
         self.dtype = _resolve_dtype(cfg.compute_dtype, self.device)
 
-        if hasattr(model, "config") and hasattr(model, "layer_costs") and getattr(model, "family", "") == "gpt2":
-            self.costs = model.layer_costs(cfg.seq_len or model.config.n_positions)
-        elif hasattr(model, "layer_costs"):
-            self.costs = model.layer_costs()
-        else:
-            self.costs = [1.0] * self.num_layers
+        self.costs = self._model_costs(model, cfg)
         n_stages = min(self.pp, self.num_layers)
         base = self.replica * self.pp
         self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
@@ -165,6 +163,45 @@ class PipelineEngine:
         logger.info("PipelineEngine[%s] plan: %s", "dist" if self.distributed else "local", self.plan.describe())
 
     # ================================================================== construction
+    def _model_costs(self, model: nn.Module, cfg: EngineConfig) -> List[float]:
+        if hasattr(model, "config") and hasattr(model, "layer_costs") and getattr(model, "family", "") == "gpt2":
+            return model.layer_costs(cfg.seq_len or model.config.n_positions)
+        if hasattr(model, "layer_costs"):
+            return model.layer_costs()
+        return [1.0] * len(model.pipeline_layers())
+
+    def _choose_granularity(self, model: nn.Module, cfg: EngineConfig) -> str:
+        """Pick the pipeline unit size for models that offer several (GPT-2 blocks or halves):
+        ``auto`` takes half blocks only when that lowers the slowest stage's cost by > 2%."""
+        if not hasattr(model, "set_pipeline_granularity"):
+            return "block"
+        want = cfg.layer_granularity
+        if want == "auto":
+            best = {}
+            for g in ("block", "half"):
+                model.set_pipeline_granularity(g)
+                costs = self._model_costs(model, cfg)
+                n = min(self.pp, len(costs))
+                rngs = make_plan(costs, list(range(n)), 0, cfg.balanced_partition).ranges
+                best[g] = max(sum(costs[a:b]) for a, b in rngs)
+            want = "half" if best["half"] < 0.98 * best["block"] else "block"
+        model.set_pipeline_granularity(want)
+        return want
+
+    def set_granularity(self, granularity: str) -> None:
+        """Switch the pipeline unit size (e.g. to match a checkpoint); the caller then installs a
+        plan over the new unit list and rebuilds (stage weights are reloaded by the caller)."""
+        if not hasattr(self.model, "set_pipeline_granularity"):
+            if granularity != "block":
+                raise ValueError(f"{type(self.model).__name__} has only whole-layer pipeline units")
+            return
+        self.model.set_pipeline_granularity(granularity)
+        self.granularity = granularity
+        self.layers = self.model.pipeline_layers()
+        self.num_layers = len(self.layers)
+        self.ties = tied_groups(self.model)
+        self.costs = self._model_costs(self.model, self.cfg)
+
     def _stage_device(self, node: int) -> torch.device:
         if self.distributed or self.device.type != "cuda":
             return self.device

@@ -68,9 +68,30 @@ class Stage:
     def is_first(self) -> bool:
         return self.layer_range[0] == 0
 
+    def _runners(self) -> List:
+        """Callables over the stage's layers: an adjacent (attn, mlp) half-block pair of the same
+        block runs as one fused block (models/gpt2.py FusedHalfPair)."""
+        r = getattr(self, "_runner_cache", None)
+        if r is not None:
+            return r
+        from ..models.gpt2 import FusedHalfPair, GPT2HalfBlock
+        layers, out, i = list(self.module), [], 0
+        while i < len(layers):
+            a = layers[i]
+            b = layers[i + 1] if i + 1 < len(layers) else None
+            if (isinstance(a, GPT2HalfBlock) and isinstance(b, GPT2HalfBlock) and a.part == "attn"
+                    and b.part == "mlp" and a.block_index == b.block_index):
+                out.append(FusedHalfPair(a, b))
+                i += 2
+            else:
+                out.append(a)
+                i += 1
+        self._runner_cache = out
+        return out
+
     def forward(self, x, labels=None):
         """Returns (output, monitored_activation).  Loss stages return the (scalar) loss."""
-        layers = list(self.module)
+        layers = self._runners()
         for layer in layers[:-1]:
             x = layer(x)
         last = layers[-1]

@@ -41,6 +41,7 @@ def _base_dict(trainer) -> Dict:
         "attack_history": _jsonable(e.attack_history),
         "reassignment_history": _jsonable(e.reassignment_history),
         "plan": e.plan.to_list(),
+        "granularity": getattr(e, "granularity", "block"),
         "trust_manager": _jsonable(trainer.trust_manager.state_dict()),
         "device_trust": e.trust_state(),
         "detector": _jsonable(trainer.attack_detector.state_dict()),
@@ -95,6 +96,9 @@ def load_checkpoint(trainer, path: str):
     e = trainer.engine
     ck = consolidate(path)
     saved_plan = PlacementPlan.from_list(ck["plan"])
+    g = ck.get("granularity", "block")
+    if g != getattr(e, "granularity", "block"):
+        e.set_granularity(g)  # layer indices of the saved plan refer to that unit size
     # with data-parallel replicas the manifest holds replica 0's plan; replicas share its layout
     same_ranks = saved_plan.ranks == e.plan.ranks or getattr(e, "dp", 1) > 1
     if not same_ranks or saved_plan.ranges != e.plan.ranges:
