@@ -59,8 +59,11 @@ def build(arch: str = "gfx950", jobs: int = 8, debug: bool = False, verbose: boo
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         kobjs.append(obj)
         if _newer(src, obj, headers):
+            # MFMA accumulators in ArchVGPRs: the default AGPR form shuttles every softmax / epilogue
+            # read through v_accvgpr_read/write and pushed the attention forward past 256 registers
+            # (one wave per SIMD); the VGPR form holds it at 140 (three waves per SIMD)
             jobs_list.append([cc, f"--offload-arch={arch}", "-std=c++17", "-fPIC", *opt, "-munsafe-fp-atomics",
-                              "-I", CSRC, "-c", src, "-o", obj])
+                              "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-I", CSRC, "-c", src, "-o", obj])
     for src in rt_srcs:
         obj = os.path.join(BUILD_DIR, "rt_" + os.path.basename(src) + ".o")
         robjs.append(obj)

@@ -115,23 +115,21 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     // staging: 2 x 16 B of K and of V per thread per 64-key tile; the NEXT tile is loaded into
     // registers while the current one computes (one barrier per tile, LDS double-buffered)
-    uint4 kreg[2], vreg[2];
+    // staging registers as named scalars (an indexed array lands in scratch)
+    uint4 kreg0, kreg1, vreg0, vreg1;
+    const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
     auto gload = [&](int kb) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-            const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
-            kreg[i] = *(const uint4*)(kbase + goff);
-            vreg[i] = *(const uint4*)(vbase + goff);
-        }
+        const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
+        kreg0 = *(const uint4*)(kbase + g0);
+        vreg0 = *(const uint4*)(vbase + g0);
+        kreg1 = *(const uint4*)(kbase + g1);
+        vreg1 = *(const uint4*)(vbase + g1);
     };
     auto sstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-            *(uint4*)(Ks[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = kreg[i];
-            *(uint4*)(Vs[buf] + row * HD + ch * 8) = vreg[i];
-        }
+        *(uint4*)(Ks[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
+        *(uint4*)(Vs[buf] + srow0 * HD + sch * 8) = vreg0;
+        *(uint4*)(Ks[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+        *(uint4*)(Vs[buf] + srow1 * HD + sch * 8) = vreg1;
     };
     gload(0);
     sstore(0);
@@ -269,9 +267,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                                             bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
     constexpr int BK = 128, BQ = 32;
+    // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
+    // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
     __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
-    __shared__ float lse_s[2][BQ], delta_s[2][BQ];
+    __shared__ __attribute__((aligned(16))) bf16_t Qw[2][BQ * HD];
+    __shared__ __attribute__((aligned(16))) bf16_t dOw[2][BQ * HD];
+    __shared__ float lse_s[2][BQ], delta_s[2][BQ];  // lse pre-scaled by log2(e)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
     int bh, kbi;
@@ -301,11 +303,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     const int q_start = CAUSAL ? kblk : 0;
     const int srow = tid >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 tile per operand
 
+    const int swz = ((sch ^ (srow & 7)) * 8);
+    constexpr float LOG2E = 1.4426950408889634f;
+    const float sl2 = scale * LOG2E;
     // prologue: tile q_start -> buffer 0
-    *(uint4*)(Qs[0] + srow * HD + sch * 8) = *(const uint4*)(qbase + (size_t)(q_start + srow) * ldq + sch * 8);
-    *(uint4*)(dOs[0] + srow * HD + sch * 8) = *(const uint4*)(dobase + (size_t)(q_start + srow) * ldo + sch * 8);
+    {
+        const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + srow) * ldq + sch * 8);
+        const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + srow) * ldo + sch * 8);
+        *(uint4*)(Qs[0] + srow * HD + sch * 8) = q;
+        *(uint4*)(Qw[0] + srow * HD + swz) = q;
+        *(uint4*)(dOs[0] + srow * HD + sch * 8) = d;
+        *(uint4*)(dOw[0] + srow * HD + swz) = d;
+    }
     if (tid < BQ) {
-        lse_s[0][tid] = lse_row[q_start + tid];
+        lse_s[0][tid] = lse_row[q_start + tid] * LOG2E;
         delta_s[0][tid] = delta_row[q_start + tid];
     }
     __syncthreads();
@@ -319,25 +330,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
             qn = *(const uint4*)(qbase + (size_t)(qt + BQ + srow) * ldq + sch * 8);
             dn = *(const uint4*)(dobase + (size_t)(qt + BQ + srow) * ldo + sch * 8);
             if (tid < BQ) {
-                ln = lse_row[qt + BQ + tid];
+                ln = lse_row[qt + BQ + tid] * LOG2E;
                 dln = delta_row[qt + BQ + tid];
             }
         }
         const bf16_t* Qb = Qs[buf];
         const bf16_t* dOb = dOs[buf];
+        const bf16_t* Qr = Qw[buf];
+        const bf16_t* dOr = dOw[buf];
         if (!CAUSAL || qt + BQ - 1 >= k0) {
             f32x16 sacc = {}, dpacc = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qb + r * HD + 16 * s + 8 * h));
-                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOb + r * HD + 16 * s + 8 * h));
+                const int c = ((2 * s + h) ^ (r & 7)) * 8;
+                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qr + r * HD + c));
+                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOr + r * HD + c));
                 sacc = MFMA32(aq, kf[s], sacc);
                 dpacc = MFMA32(ad, vf[s], dpacc);
             }
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                float p = __expf(sacc[i] * scale - lse_s[buf][ql]);
+                float p = fast_exp2(fmaf(sacc[i], sl2, -lse_s[buf][ql]));
                 if (CAUSAL && kj > qt + ql) p = 0.f;
                 sacc[i] = p;
                 dpacc[i] = p * (dpacc[i] - delta_s[buf][ql]);
@@ -361,7 +375,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         }
         if (has_next) {
             *(uint4*)(Qs[buf ^ 1] + srow * HD + sch * 8) = qn;
+            *(uint4*)(Qw[buf ^ 1] + srow * HD + swz) = qn;
             *(uint4*)(dOs[buf ^ 1] + srow * HD + sch * 8) = dn;
+            *(uint4*)(dOw[buf ^ 1] + srow * HD + swz) = dn;
             if (tid < BQ) {
                 lse_s[buf ^ 1][tid] = ln;
                 delta_s[buf ^ 1][tid] = dln;
@@ -428,24 +444,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         const int lim = (qblk + BM + BN - 1) / BN;
         nkb = lim < nkb ? lim : nkb;
     }
-    uint4 kreg[2], vreg[2];
+    // staging registers as named scalars (an indexed array lands in scratch)
+    uint4 kreg0, kreg1, vreg0, vreg1;
+    const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
     auto gload = [&](int kb) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-            const size_t goff = (size_t)(kb * BN + row) * ldq + ch * 8;
-            kreg[i] = *(const uint4*)(kbase + goff);
-            vreg[i] = *(const uint4*)(vbase + goff);
-        }
+        const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
+        kreg0 = *(const uint4*)(kbase + g0);
+        vreg0 = *(const uint4*)(vbase + g0);
+        kreg1 = *(const uint4*)(kbase + g1);
+        vreg1 = *(const uint4*)(vbase + g1);
     };
     auto sstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-            *(uint4*)(Kr[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = kreg[i];
-            *(uint4*)(Kp[buf] + row * HD + ch * 8) = kreg[i];
-            *(uint4*)(Vr[buf] + row * HD + ((ch ^ (row & 7)) * 8)) = vreg[i];
-        }
+        *(uint4*)(Kr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
+        *(uint4*)(Kp[buf] + srow0 * HD + sch * 8) = kreg0;
+        *(uint4*)(Vr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = vreg0;
+        *(uint4*)(Kr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+        *(uint4*)(Kp[buf] + srow1 * HD + sch * 8) = kreg1;
+        *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
     };
     gload(0);
     sstore(0);
