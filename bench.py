@@ -31,10 +31,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# Measured single-GPU throughput of GPT-2-medium (k tokens/s, MI355X, scripts/gpu_sweep_mbs.sh after
-# the split-K weight gradients and attention changes) per micro-batch size: larger micro-batches feed
-# the GEMMs and the attention kernels larger tiles.  Used only to choose the micro-batch size.
-_MBS_EFF = {4: 224.9, 8: 276.8, 16: 325.7, 32: 335.1}
+# Single-GPU GPT-2-medium throughput (k tokens/s) per micro-batch size, from per-unit fwd+bwd
+# timings on MI355X (scripts/time_units.py at micro-batch 4/8/16/32: 24 blocks + LM head +
+# embedding per sequence; profiles/r1_gpt2m_unit_times.jsonl): larger micro-batches feed the GEMMs
+# and the attention kernels larger tiles.  Used only to choose the micro-batch size.
+_MBS_EFF = {4: 220.9, 8: 269.8, 16: 329.3, 32: 354.8}
 # fill/drain slot cost relative to a steady-state slot: with the B/W split the drain advances one
 # stage per (F + B_input) ~ 2/3 of a full (F + B_input + W) slot
 _BUBBLE_WEIGHT = 2.0 / 3.0

@@ -260,12 +260,12 @@ class GPT2LMHeadModel(nn.Module):
 
     # time per token of each unit relative to 24 n^2 dense-GEMM FLOPs: the attention core and the
     # pointwise kernels run far from the GEMM rate, the LM head GEMMs close to it.  Calibrated on
-    # MI355X from per-unit fwd+bwd timings of GPT-2-medium at T=1024 (scripts/time_units.py,
-    # profiles/r1_gpt2m_unit_times.jsonl): attn half 0.527, MLP half 0.532, LM head 2.71-2.86 and
-    # embedding 0.13 block-times.
-    _ATTN_CORE_WEIGHT = 2.25     # causal attention FLOPs (4 T n) run at < half the GEMM rate
+    # MI355X from per-unit fwd+bwd timings of GPT-2-medium at T=1024, micro-batch 16
+    # (scripts/time_units.py, profiles/r1_gpt2m_unit_times.jsonl): attention half 0.50, MLP half
+    # 0.57, LM head 2.9 and embedding 0.14 block-times.
+    _ATTN_CORE_WEIGHT = 1.64     # causal attention FLOPs (4 T n) relative to GEMM FLOPs
     _POINTWISE_PER_BLOCK = 0.12  # LayerNorms, bias-GELU, residual adds: fraction of the block GEMMs
-    _EMBED_PER_BLOCK = 0.13      # gather fwd + wte/wpe scatter-add bwd
+    _EMBED_PER_BLOCK = 0.14      # gather fwd + wte/wpe scatter-add bwd
 
     def layer_costs(self, seq_len: int) -> List[float]:
         """Relative fwd+bwd time per pipeline unit (per token)."""
