@@ -99,3 +99,81 @@ TDL_API int tdl_xent_bwd(const void* logits, const int64_t* labels, const float*
     xent_bwd_kernel<<<M, 256, 0, s>>>((const bf16_t*)logits, labels, lse, scale_ptr, (bf16_t*)dlogits, V, ld, -100);
     TDL_LAUNCH_CHECK();
 }
+
+// Fused forward + backward over one logits row: pass 1 = online (max, sum-exp)
+// and the label logit -> loss row, lse; pass 2 re-reads the row (just streamed, so mostly an L2 /
+// MALL hit: a GPT-2 row is 100 KB) and overwrites it IN PLACE with
+//   dlogits = (softmax - onehot) * scale     (scale = DEVICE scalar, e.g. 1 / n_valid),
+// so the LM head's loss stage reads + writes the logits once instead of read / read / write with
+// separate forward and backward kernels.
+__global__ __launch_bounds__(256) void xent_fused_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                         float* __restrict__ loss, float* __restrict__ lse_out,
+                                                         const float* __restrict__ scale_ptr, int V, int ld,
+                                                         int ignore_index) {
+    __shared__ float red_m[4], red_s[4], bcast[1];
+    const int row = blockIdx.x;
+    bf16_t* lr = logits + (size_t)row * ld;
+    float m = -INFINITY, s = 0.f;
+    const int nvec = V / 8;
+    for (int i = threadIdx.x; i < nvec; i += 256) {
+        float v[8];
+        unpack8(((const uint4*)lr)[i], v);
+        float vm = v[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) vm = fmaxf(vm, v[k]);
+        float vs = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vs += __expf(v[k] - vm);
+        online_merge(m, s, vm, vs);
+    }
+    for (int j = nvec * 8 + threadIdx.x; j < V; j += 256) online_merge(m, s, bf2f(lr[j]), 1.f);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+        online_merge(m, s, m2, s2);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        red_m[wid] = m;
+        red_s[wid] = s;
+    }
+    __syncthreads();
+    const int64_t lab = labels[row];
+    const bool ign = (lab == ignore_index || lab < 0 || lab >= V);
+    if (threadIdx.x == 0) {
+        float M0 = red_m[0], S0 = red_s[0];
+        for (int w = 1; w < 4; ++w) online_merge(M0, S0, red_m[w], red_s[w]);
+        const float lse = M0 + __logf(S0);
+        lse_out[row] = lse;
+        loss[row] = ign ? 0.f : lse - bf2f(lr[lab]);  // label logit read before any overwrite
+        bcast[0] = lse;
+    }
+    __syncthreads();
+    const float lse = bcast[0];
+    const float sc = ign ? 0.f : scale_ptr[0];
+    const int nv = ld / 8;
+    for (int i = threadIdx.x; i < nv; i += 256) {
+        float v[8];
+        unpack8(((const uint4*)lr)[i], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = i * 8 + k;
+            float p = j < V ? __expf(v[k] - lse) : 0.f;
+            if (j == lab) p -= 1.f;
+            v[k] = p * sc;
+        }
+        ((uint4*)lr)[i] = pack8(v);
+    }
+    for (int j = nv * 8 + threadIdx.x; j < ld; j += 256) {
+        float p = j < V ? __expf(bf2f(lr[j]) - lse) : 0.f;
+        if (j == lab) p -= 1.f;
+        lr[j] = f2bf(p * sc);
+    }
+}
+
+TDL_API int tdl_xent_fused(void* logits, const int64_t* labels, float* loss, float* lse, const float* scale_ptr, int M,
+                           int V, int ld, hipStream_t s) {
+    if (M <= 0) return 0;
+    xent_fused_kernel<<<M, 256, 0, s>>>((bf16_t*)logits, labels, loss, lse, scale_ptr, V, ld, -100);
+    TDL_LAUNCH_CHECK();
+}

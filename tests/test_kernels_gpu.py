@@ -409,3 +409,38 @@ def test_weight_checksum_deterministic_and_sensitive():
     y = x.clone()
     y[1_234_567] = (y[1_234_567].float() * 1.01).to(torch.bfloat16)  # one weight nudged
     assert not torch.equal(checksum(y), a)
+
+
+@pytest.mark.parametrize("chunk", [None, 96])
+def test_fused_lm_head_cross_entropy_matches_fp32(chunk):
+    """Tied LM head + CE as one node (tdl_xent_fused, optional logits chunking) vs fp32 torch:
+    loss, dX, dW (plain grad and main_grad accumulation), ignored labels, padded vocab."""
+    from trustworthy_dl.ops.layers import lm_head_cross_entropy
+    torch.manual_seed(0)
+    N, n, V, Vp = 300, 128, 1000, 1024
+    x = (torch.randn(N, n, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(Vp, n, device=DEV) * 0.05).bfloat16()
+    w[V:] = 0
+    w.requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::7] = -100
+    seen = []
+    loss = lm_head_cross_entropy(x, w, labels, V, observe=lambda t: seen.append(t.float().clone()),
+                                 chunk_rows=chunk)
+    (loss * 0.5).backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    logits = xr @ wr.t()
+    ref = torch.nn.functional.cross_entropy(logits[:, :V], labels, ignore_index=-100)
+    (ref * 0.5).backward()
+    assert abs(float(loss) - float(ref)) < 2e-3 * float(ref)
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert seen and _rel(seen[0], logits[: seen[0].shape[0]].detach()) < 1e-2
+    # main_grad accumulation path
+    w2 = w.detach().clone().requires_grad_(True)
+    w2.main_grad = torch.zeros(Vp, n, device=DEV)
+    x2 = x.detach().clone().requires_grad_(True)
+    (lm_head_cross_entropy(x2, w2, labels, V, chunk_rows=chunk) * 0.5).backward()
+    assert w2.grad is None
+    assert _rel(w2.main_grad, wr.grad) < 2e-2

@@ -186,7 +186,11 @@ class DistributedTrainer:
             if st is None:
                 continue
             x = e._stage_input(x, st) if k == 0 else x.to(st.device)
-            y, mon = st.forward(x, labels.to(st.device) if (st.computes_loss and labels is not None) else None)
+            seen = []
+            y, mon = st.forward(x, labels.to(st.device) if (st.computes_loss and labels is not None) else None,
+                                observe=lambda t: seen.append(t.detach().clone()))
+            if mon is None and seen:
+                mon = seen[0]  # the fused LM head reuses its logits buffer: keep a copy
             outs[node] = mon if mon is not None else y
             if self.config.attack_detection_enabled and outs[node] is not None:
                 if self.attack_detector.detect_output_anomaly(outs[node], node, e.global_step):

@@ -192,12 +192,18 @@ class GPT2Head(nn.Module):
     def logits(self, h):
         return ops.layers.linear_t(self.ln_f(h), self.wte)
 
+    accepts_observer = True  # Stage passes its output monitor in (the logits buffer is reused)
+
     def forward(self, h, labels=None):
-        logits = self.logits(h)
-        self._last_logits = logits  # monitored output when the head is a stage on its own
+        observe = getattr(self, "_observe", None)
         if labels is None:
+            logits = self.logits(h)
+            self._last_logits = logits  # monitored output when the head is a stage on its own
             return logits
-        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), self.vocab_size)
+        # fused head: the logits buffer becomes dlogits inside the forward, so the monitor (if
+        # any) is handed the logits before that and there is no _last_logits afterwards
+        self._last_logits = None
+        return ops.layers.lm_head_cross_entropy(self.ln_f(h), self.wte, labels, self.vocab_size, observe=observe)
 
 
 class _Transformer(nn.Module):

@@ -86,6 +86,7 @@ _SIGNATURES = {
     # xent.hip
     "tdl_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "tdl_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _F, _P],
+    "tdl_xent_fused": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     # optim.hip
     "tdl_adamw_flat": [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _F, _P, _I, _P],
     "tdl_fill_f32": [_P, _L, _F, _P],

@@ -504,3 +504,104 @@ class _LinearT(torch.autograd.Function):
 
 def linear_t(x, weight):
     return _LinearT.apply(x, weight)
+
+
+# ============================================================== tied LM head + cross-entropy, one node
+def lmhead_chunk_rows(vocab_padded: int) -> int:
+    """Rows per logits chunk: the whole micro-batch unless its bf16 logits exceed
+    TDL_LMHEAD_CHUNK_MB (default 4096 MB) — then the [rows, vocab] logits are never materialised
+    at once."""
+    budget = int(os.environ.get("TDL_LMHEAD_CHUNK_MB", "4096")) << 20
+    return max(256, budget // (2 * vocab_padded) // 256 * 256)
+
+
+class _LMHeadXent(torch.autograd.Function):
+    """loss = mean CE(x @ W^T, labels) with W = wte [Vp, n] tied; padded vocab columns masked.
+
+    The CE forward and backward run as ONE native pass per logits row (tdl_xent_fused: loss,
+    log-sum-exp, then dlogits = (softmax - onehot) / n_valid written over the logits in place),
+    during the forward: the logits are read + written once.  ``observe(logits)`` (the stage's
+    output monitor) runs before the overwrite.  One chunk (the usual case): the dlogits buffer is
+    kept and the backward runs dX = g dL.W and dW += dL^T.(g X) (deferrable with the B/W split).
+    Several chunks (logits above the budget): each chunk's dX / dW are formed right away into
+    fp32 buffers that the backward scales by the upstream gradient g."""
+
+    @staticmethod
+    def forward(ctx, x, weight, labels, V, observe, chunk_rows):
+        shape = x.shape
+        n = shape[-1]
+        x2 = x.reshape(-1, n).contiguous()
+        N, Vp = x2.shape[0], weight.shape[0]
+        labels = labels.reshape(-1).contiguous()
+        dev = x2.device
+        n_valid = ((labels >= 0) & (labels < V)).sum().clamp(min=1).float()
+        scale = (1.0 / n_valid).reshape(1).contiguous()
+        loss_rows = torch.empty(N, dtype=torch.float32, device=dev)
+        lse = torch.empty(N, dtype=torch.float32, device=dev)
+        s = stream_ptr(dev)
+        C = N if chunk_rows is None or chunk_rows >= N else int(chunk_rows)
+        ctx.shape = shape
+        if C == N:
+            logits = torch.mm(x2, weight.t())
+            if observe is not None:
+                observe(logits)
+            _lib.call("tdl_xent_fused", ptr(logits), ptr(labels), ptr(loss_rows), ptr(lse), ptr(scale), N, V, Vp, s)
+            ctx.save_for_backward(x2, weight, logits)  # logits buffer now holds dL (unscaled by g)
+            ctx.chunked = False
+        else:
+            dx = torch.empty(N, n, dtype=torch.float32, device=dev)
+            dw = torch.zeros(Vp, n, dtype=torch.float32, device=dev)
+            buf = torch.empty(C, Vp, dtype=x2.dtype, device=dev)
+            for r0 in range(0, N, C):
+                r1 = min(N, r0 + C)
+                lc = buf[: r1 - r0]
+                torch.mm(x2[r0:r1], weight.t(), out=lc)
+                if observe is not None and r0 == 0:
+                    observe(lc)
+                _lib.call("tdl_xent_fused", ptr(lc), ptr(labels[r0:r1]), ptr(loss_rows[r0:r1]), ptr(lse[r0:r1]),
+                          ptr(scale), r1 - r0, V, Vp, s)
+                torch.mm(lc, weight, out_dtype=torch.float32, out=dx[r0:r1])
+                wgrad_acc(dw, lc.t(), x2[r0:r1])
+            ctx.save_for_backward(dx, dw, weight)
+            ctx.chunked = True
+        return loss_rows.sum() / n_valid
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.reshape(())
+        if ctx.chunked:
+            dx32, dw, weight = ctx.saved_tensors
+            dx = (dx32 * g).to(weight.dtype) if ctx.needs_input_grad[0] else None
+            mg = getattr(weight, "main_grad", None)
+            if mg is not None:
+                mg.add_(dw * g)
+                gw = None
+            else:
+                gw = (dw * g).to(weight.dtype)
+        else:
+            x2, weight, dl = ctx.saved_tensors
+            dx = None
+            if ctx.needs_input_grad[0]:
+                dx = torch.mm(dl, weight)
+                dx.mul_(g)
+            xg = x2 * g
+            if _wants_main_grad(weight):
+                run_or_defer(lambda: _wgrad_into(weight, dl.t(), xg))
+                gw = None
+            else:
+                gw = _wgrad_into(weight, dl.t(), xg)
+        return (dx.reshape(ctx.shape) if dx is not None else None), gw, None, None, None, None
+
+
+def lm_head_cross_entropy(x, weight, labels, num_classes: int, observe=None, chunk_rows: Optional[int] = None):
+    """Mean CE of the tied LM head ``x @ weight^T`` (GPU: fused single-pass CE, chunked logits;
+    CPU / no-grad: plain logits + cross_entropy).  ``observe`` sees the logits before reuse."""
+    fused = os.environ.get("TDL_FUSED_LMHEAD", "1") != "0"
+    if not (fused and x.is_cuda and torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad)):
+        logits = linear_t(x, weight)
+        if observe is not None:
+            observe(logits)
+        return cross_entropy(logits.reshape(-1, logits.shape[-1]), labels.reshape(-1), num_classes)
+    if chunk_rows is None:
+        chunk_rows = lmhead_chunk_rows(weight.shape[0])
+    return _LMHeadXent.apply(x, weight, labels, num_classes, observe, chunk_rows)

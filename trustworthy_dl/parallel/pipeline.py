@@ -343,7 +343,8 @@ class PipelineEngine:
                 st = self.stages[node]
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
-                y, mon = st.forward(x, labels)
+                obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
+                y, mon = st.forward(x, labels, observe=obs)
                 if not st.computes_loss:
                     y = self._attack_output(node, y, truth)
                     if i == 0:
@@ -391,7 +392,8 @@ class PipelineEngine:
             if not first:
                 x.requires_grad_(True)
             labels = targets[i].to(st.device, non_blocking=True) if last else None
-            y, mon = st.forward(x, labels)
+            obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
+            y, mon = st.forward(x, labels, observe=obs)
             if last:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()
@@ -523,7 +525,8 @@ class PipelineEngine:
             if not first:
                 x.requires_grad_(True)
             labels = targets[i].to(st.device, non_blocking=True) if last else None
-            y, mon = st.forward(x, labels)
+            obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
+            y, mon = st.forward(x, labels, observe=obs)
             if last:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()

@@ -89,20 +89,40 @@ class Stage:
         self._runner_cache = out
         return out
 
-    def forward(self, x, labels=None):
-        """Returns (output, monitored_activation).  Loss stages return the (scalar) loss."""
+    def forward(self, x, labels=None, observe=None):
+        """Returns (output, monitored_activation).  Loss stages return the (scalar) loss.
+
+        ``observe``: optional output monitor.  A loss layer that owns its monitored tensor (the
+        fused LM head: logits are rewritten into dlogits in place) is handed it and calls it at the
+        right moment; the returned monitored activation is then None (already observed)."""
         layers = self._runners()
         for layer in layers[:-1]:
             x = layer(x)
         last = layers[-1]
         if self.computes_loss:
             mon = x if len(layers) > 1 else None
+            if mon is None and observe is not None and getattr(last, "accepts_observer", False):
+                last._observe = observe
+                try:
+                    out = last(x, labels)
+                finally:
+                    last._observe = None
+                return out, None
             out = last(x, labels)
             if mon is None:
                 mon = getattr(last, "_last_logits", None)
             return out, mon
         y = last(x)
         return y, y
+
+    def output_observer(self):
+        """Monitor callable for this stage's output: queue its statistics on the verifier's side
+        stream, then make the compute stream wait for them (the tensor may be overwritten next)."""
+        def observe(t: torch.Tensor):
+            self.verifier.observe_output(t)
+            if self.verifier.side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.verifier.side)
+        return observe
 
     def local_param(self, layer_idx: int, attr: str) -> Optional[nn.Parameter]:
         a, b = self.layer_range
