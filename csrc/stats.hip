@@ -268,19 +268,38 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
     acc.init();
     float sq = 0.f, dot = 0.f, rsq = 0.f;
     int bad = 0;
-    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-        const float v = g[i];
+    // per element: moments of the finite gradient values, the EMA reference update and the
+    // gradient . reference dot product (returns the new reference value)
+    auto proc = [&](float v, float r) -> float {
         if (isfinite(v)) { acc.add(v); sq += v * v; } else ++bad;
-        if (ref) {
-            const float r = ref[i];
-            if (ref_valid) {
-                dot += v * r;
-                rsq += r * r;
-                ref[i] = beta * r + (1.f - beta) * (isfinite(v) ? v : 0.f);
-            } else {
-                ref[i] = isfinite(v) ? v : 0.f;
-            }
+        if (ref_valid) {
+            dot += v * r;
+            rsq += r * r;
+            return beta * r + (1.f - beta) * (isfinite(v) ? v : 0.f);
         }
+        return isfinite(v) ? v : 0.f;
+    };
+    // 16-byte vector body over the 4-aligned part of the chunk, scalar head / tail
+    int64_t vbeg = (start + 3) & ~(int64_t)3;
+    if (vbeg > end) vbeg = end;
+    const int64_t vend = vbeg + ((end - vbeg) & ~(int64_t)3);
+    for (int64_t i = start + threadIdx.x; i < vbeg; i += blockDim.x) {
+        const float nr = proc(g[i], ref ? ref[i] : 0.f);
+        if (ref) ref[i] = nr;
+    }
+    for (int64_t i = vbeg + 4 * (int64_t)threadIdx.x; i < vend; i += 4 * (int64_t)blockDim.x) {
+        const float4 v = *(const float4*)(g + i);
+        const float4 r = ref ? *(const float4*)(ref + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 nr;
+        nr.x = proc(v.x, r.x);
+        nr.y = proc(v.y, r.y);
+        nr.z = proc(v.z, r.z);
+        nr.w = proc(v.w, r.w);
+        if (ref) *(float4*)(ref + i) = nr;
+    }
+    for (int64_t i = vend + threadIdx.x; i < end; i += blockDim.x) {
+        const float nr = proc(g[i], ref ? ref[i] : 0.f);
+        if (ref) ref[i] = nr;
     }
     Moments r = block_merge(acc.to_moments(), sh);
     sq = block_sum(sq, red);
@@ -574,7 +593,7 @@ TDL_API int tdl_kl_div_softmax(const float* a, const float* b, int R, int C, flo
 // compute weights taken right after its optimizer step with the one taken before the next update —
 // any write outside the optimizer (parameter perturbation, memory corruption) shows up.
 namespace {
-constexpr int CK_BLOCKS = 512;
+constexpr int CK_BLOCKS = 2048;  // 8 blocks per CU
 
 __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __restrict__ x, int64_t n,
                                                                int64_t per_block, double* __restrict__ part) {
@@ -582,6 +601,9 @@ __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __r
     const int64_t beg = (int64_t)blockIdx.x * per_block;
     const int64_t end = beg + per_block < n ? beg + per_block : n;
     double s = 0.0, q = 0.0, w = 0.0;
+    // position weight (i % 1021) + 1, carried incrementally: one 64-bit modulo per thread, then
+    // +2048 elements per iteration = +6 (mod 1021) — a per-element int64 modulo was the cost
+    int r = (int)((beg + threadIdx.x * 8) % 1021);
     for (int64_t i = beg + threadIdx.x * 8; i < end; i += 256 * 8) {
         float f[8];
         if (i + 8 <= end) {
@@ -593,10 +615,13 @@ __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __r
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const double v = (double)f[e];
+            const int re = r + e;
             s += v;
             q += v * v;
-            w += v * (double)((i + e) % 1021 + 1);
+            w += v * (double)(re < 1021 ? re + 1 : re - 1020);
         }
+        r += 2048 - 2 * 1021;
+        if (r >= 1021) r -= 1021;
     }
     s = wave_sum_d(s);
     q = wave_sum_d(q);
@@ -614,22 +639,38 @@ __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __r
     }
 }
 
-__global__ void checksum_final_kernel(const double* __restrict__ part, int nb, double* __restrict__ out) {
+// Fixed-shape reduction of the per-block partials (256 threads, contiguous runs per thread, then
+// wave / cross-wave sums in a fixed order): deterministic for a given nb.
+__global__ __launch_bounds__(256) void checksum_final_kernel(const double* __restrict__ part, int nb,
+                                                             double* __restrict__ out) {
+    __shared__ double red[3][4];
+    const int per = (nb + 255) / 256;
+    double a[3] = {0.0, 0.0, 0.0};
+    for (int b = threadIdx.x * per; b < (threadIdx.x + 1) * per && b < nb; ++b) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a[k] += part[b * 3 + k];
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        a[k] = wave_sum_d(a[k]);
+        if (lane == 0) red[k][wid] = a[k];
+    }
+    __syncthreads();
     if (threadIdx.x < 3) {
-        double a = 0.0;
-        for (int b = 0; b < nb; ++b) a += part[b * 3 + threadIdx.x];
-        out[threadIdx.x] = a;
+        const double* r = red[threadIdx.x];
+        out[threadIdx.x] = ((r[0] + r[1]) + r[2]) + r[3];
     }
 }
 }  // namespace
 
-// out: 3 doubles; ws: 3 * 512 doubles.  n bf16 elements, 16-byte aligned base.
+// out: 3 doubles; ws: 3 * 2048 doubles.  n bf16 elements, 16-byte aligned base.
 TDL_API int tdl_checksum_bf16(const void* x, int64_t n, double* ws, double* out, hipStream_t s) {
     if (((uintptr_t)x & 15) != 0) return (int)hipErrorInvalidValue;
     int64_t per_block = (n + CK_BLOCKS - 1) / CK_BLOCKS;
     per_block = (per_block + 7) / 8 * 8;
     const int nb = (int)((n + per_block - 1) / per_block);
     checksum_partial_kernel<<<nb > 0 ? nb : 1, 256, 0, s>>>((const bf16_t*)x, n, per_block, ws);
-    checksum_final_kernel<<<1, 64, 0, s>>>(ws, nb > 0 ? nb : 1, out);
+    checksum_final_kernel<<<1, 256, 0, s>>>(ws, nb > 0 ? nb : 1, out);
     TDL_LAUNCH_CHECK();
 }

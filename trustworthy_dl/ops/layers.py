@@ -580,11 +580,12 @@ class _LMHeadXent(torch.autograd.Function):
                 gw = (dw * g).to(weight.dtype)
         else:
             x2, weight, dl = ctx.saved_tensors
+            gb = g.to(x2.dtype)  # same-dtype scalar: the vectorised elementwise path
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.mm(dl, weight)
-                dx.mul_(g)
-            xg = x2 * g
+                dx.mul_(gb)
+            xg = x2 * gb
             if _wants_main_grad(weight):
                 run_or_defer(lambda: _wgrad_into(weight, dl.t(), xg))
                 gw = None

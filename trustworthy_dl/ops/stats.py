@@ -290,7 +290,7 @@ def checksum(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tenso
     if out is None:
         out = torch.empty(3, dtype=torch.float64, device=x.device)
     if x.is_cuda and x.dtype == torch.bfloat16 and x.data_ptr() % 16 == 0:
-        ws = torch.empty(3 * 512, dtype=torch.float64, device=x.device)
+        ws = torch.empty(3 * 2048, dtype=torch.float64, device=x.device)
         _lib.call("tdl_checksum_bf16", ptr(x), x.numel(), ptr(ws), ptr(out), stream_ptr(x.device))
         return out
     v = x.double()
