@@ -670,3 +670,25 @@ TDL_API int tdl_add_into_f32(float* dst, const void* src, int64_t n, int src_bf1
     add_into_f32_kernel<<<(int)(blocks < 8192 ? blocks : 8192), 256, 0, s>>>(dst, src, n, src_bf16);
     TDL_LAUNCH_CHECK();
 }
+
+// ============================================================== y = x * (*scale), bf16, device scalar
+// Scales by an fp32 DEVICE scalar (e.g. an autograd grad_output) without a host sync and without
+// rounding the scalar to bf16 first: fp32 product, one rounding.  x, y 16-byte aligned, n % 8 == 0.
+__global__ __launch_bounds__(256) void scale_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                         const float* __restrict__ scale, int64_t n8) {
+    const float sc = scale[0];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        float v[8];
+        unpack8(((const uint4*)x)[i], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= sc;
+        ((uint4*)y)[i] = pack8(v);
+    }
+}
+
+TDL_API int tdl_scale_bf16(const void* x, void* y, const float* scale, int64_t n, hipStream_t s) {
+    if (n % 8 != 0 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15)) return (int)hipErrorInvalidValue;
+    const int64_t n8 = n / 8, blocks = (n8 + 255) / 256;
+    scale_bf16_kernel<<<(int)(blocks < 4096 ? blocks : 4096), 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, scale, n8);
+    TDL_LAUNCH_CHECK();
+}

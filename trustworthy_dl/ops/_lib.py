@@ -87,6 +87,7 @@ _SIGNATURES = {
     "tdl_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "tdl_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _F, _P],
     "tdl_xent_fused": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "tdl_scale_bf16": [_P, _P, _P, _L, _P],
     # optim.hip
     "tdl_adamw_flat": [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _F, _P, _I, _P],
     "tdl_fill_f32": [_P, _L, _F, _P],

@@ -515,6 +515,14 @@ def lmhead_chunk_rows(vocab_padded: int) -> int:
     return max(256, budget // (2 * vocab_padded) // 256 * 256)
 
 
+def _scale_bf16(x: torch.Tensor, y: torch.Tensor, g: torch.Tensor):
+    """y = x * g[0] (g: fp32 device scalar; one rounding, no host sync)."""
+    if x.dtype == torch.bfloat16 and x.numel() % 8 == 0 and x.is_contiguous() and y.is_contiguous():
+        _lib.call("tdl_scale_bf16", ptr(x), ptr(y), ptr(g), x.numel(), stream_ptr(x.device))
+    else:
+        torch.mul(x, g.reshape(()), out=y)
+
+
 class _LMHeadXent(torch.autograd.Function):
     """loss = mean CE(x @ W^T, labels) with W = wte [Vp, n] tied; padded vocab columns masked.
 
@@ -580,12 +588,13 @@ class _LMHeadXent(torch.autograd.Function):
                 gw = (dw * g).to(weight.dtype)
         else:
             x2, weight, dl = ctx.saved_tensors
-            gb = g.to(x2.dtype)  # same-dtype scalar: the vectorised elementwise path
+            gf = g.float().reshape(1).contiguous()
             dx = None
             if ctx.needs_input_grad[0]:
                 dx = torch.mm(dl, weight)
-                dx.mul_(gb)
-            xg = x2 * gb
+                _scale_bf16(dx, dx, gf)
+            xg = torch.empty_like(x2)
+            _scale_bf16(x2, xg, gf)
             if _wants_main_grad(weight):
                 run_or_defer(lambda: _wgrad_into(weight, dl.t(), xg))
                 gw = None
