@@ -33,7 +33,7 @@ def _make_batches(model_name, n, bs):
     return out
 
 
-def _build(model_name, nodes, micro, p2p_mode="async"):
+def _build(model_name, nodes, micro, p2p_mode="async", granularity="auto"):
     from trustworthy_dl.models import get_model
     from trustworthy_dl.parallel.flat import AdamWConfig
     from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
@@ -42,17 +42,17 @@ def _build(model_name, nodes, micro, p2p_mode="async"):
         kw["vocab_size"] = 1024
     m = get_model(model_name, seed=7, **kw)
     cfg = EngineConfig(num_nodes=nodes, micro_batches=micro, device="cpu", seq_len=32, p2p_mode=p2p_mode,
-                       adamw=AdamWConfig(lr=1e-2, eps=1.0, max_grad_norm=1.0), reassign=False)
+                       layer_granularity=granularity, adamw=AdamWConfig(lr=1e-2, eps=1.0, max_grad_norm=1.0), reassign=False)
     from trustworthy_dl.utils.metrics import MetricsCollector
     return PipelineEngine(m, cfg, metrics=MetricsCollector())
 
 
-def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="async"):
+def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="async", granularity="auto"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    eng = _build(model_name, world, micro, p2p_mode)
+    eng = _build(model_name, world, micro, p2p_mode, granularity)
     losses = []
     for b in _make_batches(model_name, steps, 8):
         eng.train_step(b)
@@ -67,17 +67,18 @@ def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="asy
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model_name,micro,world,p2p", [("resnet32", 2, 2, "async"), ("gpt2-tiny", 4, 2, "async"),
-                                                         ("gpt2-tiny", 4, 2, "grouped"), ("gpt2-tiny", 2, 4, "async"),
-                                                         ("gpt2-tiny", 8, 4, "async")])
-def test_pipeline_matches_single_process(model_name, micro, world, p2p):
+@pytest.mark.parametrize("model_name,micro,world,p2p,gran", [
+    ("resnet32", 2, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "grouped", "auto"),
+    ("gpt2-tiny", 2, 4, "async", "auto"), ("gpt2-tiny", 8, 4, "async", "auto"),
+    ("gpt2-tiny", 4, 4, "async", "half")])  # stage boundaries inside blocks, one process per stage
+def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran):
     steps = 4
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "res")
-        mp.spawn(_worker, args=(world, _free_port(), model_name, steps, micro, out, p2p), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), model_name, steps, micro, out, p2p, gran), nprocs=world, join=True)
         res = [json.load(open(f"{out}.{r}")) for r in range(world)]
     torch.set_num_threads(4)
-    local = _build(model_name, world, micro)
+    local = _build(model_name, world, micro, granularity=gran)
     for b in _make_batches(model_name, steps, 8):
         local.train_step(b)
     local.flush()
