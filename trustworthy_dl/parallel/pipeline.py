@@ -241,6 +241,8 @@ class PipelineEngine:
             # (s+1 -> s): each carries one-way, in-order traffic per neighbour pair
             everyone = list(range(self.world))
             self._dir_groups = (dist.new_group(ranks=everyone), dist.new_group(ranks=everyone))
+            for g in self._dir_groups:
+                self._warm_group(g, everyone)
         # tied parameters living on different ranks need a gradient all-reduce group (one per
         # replica; new_group is collective over the whole world, so every rank creates them all)
         base = self.replica * self.pp
@@ -249,13 +251,26 @@ class PipelineEngine:
         if len(local) > 1:
             for d in range(self.dp):
                 g = dist.new_group(ranks=[d * self.pp + r for r in local])
+                self._warm_group(g, [d * self.pp + r for r in local])
                 if d == self.replica:
                     self.tie_group = g
         if self.dp > 1 and self.dp_group is None:
             for pos in range(self.pp):
                 g = dist.new_group(ranks=[d * self.pp + pos for d in range(self.dp)])
+                self._warm_group(g, [d * self.pp + pos for d in range(self.dp)])
                 if pos == self.rank % self.pp:
                     self.dp_group = g
+
+    def _warm_group(self, group, members: List[int]):
+        """One 1-element all-reduce by every member, right after the group is created (groups are
+        created in the same order on every rank, so members meet in that order).  Under RCCL this
+        brings the communicator up collectively before the first pipeline P2P on it, which is posted
+        by only a subset of the ranks (torch's batch_isend_irecv requirement for the first call on a
+        group); under gloo it is a cheap rendezvous check."""
+        if self.rank not in members or len(members) < 2:
+            return
+        t = torch.zeros(1, device=self.device)
+        dist.all_reduce(t, group=group)
 
     def _init_trust_state(self):
         N = self.num_nodes
