@@ -228,3 +228,25 @@ def test_checkpoint_restores_half_block_layout(tmp_path):
     tr2.load_checkpoint(path)
     assert tr2.engine.granularity == "half" and tr2.engine.plan.ranges == tr.engine.plan.ranges
     assert tr2.engine.eval_step(batch) == pytest.approx(ref, rel=1e-6)
+
+
+def test_phase_tracer_breakdown(tmp_path):
+    eng = _engine(nodes=2, trace_phases=True)
+    for b in _batches(3):
+        eng.train_step(b)
+    eng.flush()
+    eng.tracer.resolve(block=True)
+    summ = eng.tracer.summary()
+    for k in ("fwd", "bwd_input", "verify", "optimizer", "step"):
+        assert summ.get(k, 0.0) > 0.0, (k, summ)
+    assert summ["step"] >= summ["fwd"]
+    path = tmp_path / "t.json"
+    eng.tracer.export_chrome_trace(str(path))
+    import json
+    ev = json.loads(path.read_text())["traceEvents"]
+    assert {e["name"] for e in ev} >= {"fwd", "bwd_input", "verify", "optimizer"}
+    assert all(e["dur"] >= 0 for e in ev)
+    # tracing off: no events, no overhead objects
+    eng2 = _engine(nodes=2)
+    eng2.train_step(next(_batches(1)))
+    assert eng2.tracer.summary() == {}

@@ -393,6 +393,7 @@ class DistributedTrainer:
             "metrics": self.metrics_collector.get_summary(),
             "plan": self.engine.plan.describe() if self.engine else None,
             "detection": self.attack_detector.get_detection_statistics(),
+            "phase_ms": self.engine.tracer.summary() if self.engine and self.engine.tracer.enabled else {},
         }
 
     def cleanup(self):

@@ -124,9 +124,25 @@ def _declare(l: ctypes.CDLL):
         fn.restype = ctypes.c_int64 if name.endswith(("_bytes", "_floats")) else ctypes.c_int
 
 
+# Debug mode (race detection): ``TDL_SYNC_LAUNCH=1`` synchronises the device after every
+# native launch and checks the sticky HIP error, so an asynchronous fault is reported at the kernel
+# that caused it (the HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL=3 idea, for our own entry points).
+SYNC_LAUNCH = os.environ.get("TDL_SYNC_LAUNCH", "0") not in ("", "0")
+
+
+def set_sync_launch(on: bool) -> None:
+    global SYNC_LAUNCH
+    SYNC_LAUNCH = bool(on)
+
+
 def call(name: str, *args):
     fn = getattr(lib(), name)
     check(fn(*args), name)
+    if SYNC_LAUNCH:
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # pragma: no cover - device fault path
+            raise RuntimeError(f"native kernel {name} faulted: {e}") from e
 
 
 DTYPE_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}

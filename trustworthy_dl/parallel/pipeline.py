@@ -36,6 +36,7 @@ from ..core.trust_manager import (METRIC_NAMES, NodeStatus, STATUS_CODES, STATUS
 from ..security import stage_verifier as SV
 from ..ops import stats as dstats
 from ..ops.layers import defer_weight_grads
+from ..runtime.tracing import PhaseTracer
 from .comm import P2PComm, all_gather_rows, batched_transfer
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
@@ -80,6 +81,9 @@ class EngineConfig:
     heartbeat_timeout: float = 30.0      # silence after which a peer is OFFLINE
     abort_on_offline: bool = False       # fail fast so an elastic launcher restarts from a checkpoint
     seed: int = 0
+    trace_phases: bool = False           # HIP-event per-phase step breakdown (runtime/tracing.py)
+    serialize_streams: bool = field(default_factory=lambda: os.environ.get("TDL_SERIALIZE_STREAMS", "0") == "1")
+                                         # debug: verification on the compute stream (no side-stream overlap)
 
 
 def _resolve_dtype(name: str, device: torch.device) -> torch.dtype:
@@ -145,6 +149,7 @@ class PipelineEngine:
             torch.cuda.set_device(self.device)
         # conv nets run bf16 on the native NHWC implicit-GEMM kernels (ops/conv.py), like GPT-2
         self.dtype = _resolve_dtype(cfg.compute_dtype, self.device)
+        self.tracer = PhaseTracer(self.device, enabled=cfg.trace_phases)
 
         self.costs = self._model_costs(model, cfg)
         n_stages = min(self.pp, self.num_layers)
@@ -213,6 +218,7 @@ class PipelineEngine:
         vk.setdefault("quarantine", self.cfg.quarantine)
         vk.setdefault("output_detection", self.cfg.attack_detection)
         vk.setdefault("gradient_verification", self.cfg.gradient_verification)
+        vk.setdefault("serialize_streams", self.cfg.serialize_streams)
         return vk
 
     def _build(self, layer_modules: Optional[Dict[int, List[nn.Module]]] = None):
@@ -323,6 +329,8 @@ class PipelineEngine:
         else:
             loss = self._run_local(inputs, targets, truth)
         self._finish_step(loss, truth)
+        self.tracer.end_step(self.global_step)
+        self.tracer.resolve()
         self._step_time = time.perf_counter() - t0
         return self.last_loss
 
@@ -359,7 +367,8 @@ class PipelineEngine:
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
                 obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
-                y, mon = st.forward(x, labels, observe=obs)
+                with self.tracer.phase("fwd"):
+                    y, mon = st.forward(x, labels, observe=obs)
                 if not st.computes_loss:
                     y = self._attack_output(node, y, truth)
                     if i == 0:
@@ -370,7 +379,8 @@ class PipelineEngine:
                         torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
                 x = y
             loss = x / M
-            loss.backward()
+            with self.tracer.phase("bwd_input"):
+                loss.backward()
             total = loss.detach() if total is None else total + loss.detach()
         return total
 
@@ -566,6 +576,10 @@ class PipelineEngine:
         def input_of(i, h):
             return self._stage_input(inputs[i], st) if first else take(h)
 
+        tr = self.tracer
+        if tr.enabled:
+            fwd, bwd, take = tr.wrap("fwd", fwd), tr.wrap("bwd_input", bwd), tr.wrap("p2p_wait", take)
+
         x_h = post_x(0)
         for i in range(warm):                      # warm > 0 implies not last
             x = input_of(i, x_h)
@@ -589,7 +603,8 @@ class PipelineEngine:
             dx, dw = bwd(x0, y0, dy)
             if not first:
                 send(dx, prev, grad_pg)
-            dw.run()
+            with tr.phase("bwd_weight"):
+                dw.run()
         dy_h = post_dy(rem) if warm > 0 else None
         for c in range(warm):
             b = rem + c
@@ -599,7 +614,8 @@ class PipelineEngine:
             if not first:
                 send(dx, prev, grad_pg)
             dy_h = post_dy(b + 1)                  # after the send: no send queues behind it
-            dw.run()
+            with tr.phase("bwd_weight"):
+                dw.run()
         t0 = time.perf_counter()
         for w in sends:
             w.wait()
@@ -668,6 +684,7 @@ class PipelineEngine:
                     break
 
     def _finish_step(self, loss, truth: Dict[int, bool]):
+        tv = self.tracer.begin("verify")
         self._allreduce_tied()
         N = self.num_nodes
         rows = []
@@ -721,11 +738,14 @@ class PipelineEngine:
             self.t_values[idx] = v
             self.t_counts[idx] = c
             self.t_status[idx] = s_
+        self.tracer.end(tv)
+        to = self.tracer.begin("optimizer")
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
             st.flat.adamw_step(self.cfg.adamw, ctrl=st.verifier.ctrl)
             if self.cfg.param_integrity:
                 st.param_checksum = dstats.checksum(st.flat.data, getattr(st, "param_checksum", None))
+        self.tracer.end(to)
         if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
             self._audit_params()
         # queue the host report (pinned, non-blocking)

@@ -39,7 +39,7 @@ class StageVerifier:
                  ema_beta: float = 0.8, symmetric_consistency: bool = True, quarantine: bool = True,
                  output_detection: bool = True, gradient_verification: bool = True,
                  consistency_tolerance: float = 2.0, deviation_deadzone: float = 0.25,
-                 robust_baseline: bool = True, baseline_window: int = 100):
+                 robust_baseline: bool = True, baseline_window: int = 100, serialize_streams: bool = False):
         """``consistency_tolerance`` / ``deviation_deadzone`` make the trust metrics tolerate the
         legitimate drift of training (gradient norms routinely move 2x within a few steps early in
         training): a norm ratio r scores min(1, tol * min(r, 1/r)), an output deviation d scores
@@ -68,7 +68,11 @@ class StageVerifier:
         self.ctrl[0] = 1.0
         self.digest = z(DIGEST)
         self._have_out = False
-        self.side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        # ``serialize_streams`` (debug): run the statistics on the compute stream instead of the side
+        # stream; with identical inputs the digests must match the overlapped run bit for bit (an
+        # ordering bug between the two streams shows up as a difference; tests/test_kernels_gpu.py)
+        self.side = (torch.cuda.Stream(self.device)
+                     if self.device.type == "cuda" and not serialize_streams else None)
 
     # ---------------------------------------------------------------- output path
     def observe_output(self, y: torch.Tensor):
