@@ -98,3 +98,64 @@ def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran):
     # every rank holds the same trust vector (identical all-gathered digests)
     for r in range(1, world):
         assert res[0]["trust"] == pytest.approx(res[r]["trust"])
+
+
+def _layer_sums(eng):
+    return {li: float(eng._pack_layer(st, li).double().sum())
+            for st in eng.stages.values() for li in range(*st.layer_range)}
+
+
+def _reshard_run(eng, batches, rank_is_tampered):
+    for b in batches[:4]:
+        eng.train_step(b)
+    eng.flush()
+    if rank_is_tampered:
+        with torch.no_grad():
+            eng.stages[1].flat.master.add_(1000.0)      # node 1 scribbles over its own weights
+    eng.reassign([1], step=eng.global_step)
+    rec = eng.reassignment_history[-1]
+    for b in batches[4:]:
+        eng.train_step(b)
+    eng.flush()
+    return rec
+
+
+def _reshard_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _build("gpt2-tiny", world, 2)
+    eng.cfg.shadow_interval = 2
+    rec = _reshard_run(eng, _make_batches("gpt2-tiny", 6, 8), rank == 1)
+    res = {"rank": rank, "sums": _layer_sums(eng), "restored": {str(k): v for k, v in rec["restored_from_shadow"].items()},
+           "plan": eng.plan.ranks, "last_loss": eng.last_loss}
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_reshard_restores_from_shadow_and_matches_local():
+    """Re-shard mid-training over gloo (3 stages -> 2): node 1 is excluded, its layers are rebuilt
+    from the snapshot node 2 holds (its own memory was tampered with), training continues, and the
+    final per-layer state equals the single-process run of the same sequence."""
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.spawn(_reshard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    eng = _build("gpt2-tiny", world, 2)
+    eng.cfg.shadow_interval = 2
+    rec = _reshard_run(eng, _make_batches("gpt2-tiny", 6, 8), True)
+    ref = _layer_sums(eng)
+    got = {}
+    for r in res:
+        assert r["restored"] == {"1": 4} and r["plan"] == [0, 2]
+        got.update({int(k): v for k, v in r["sums"].items()})
+    assert rec["restored_from_shadow"] == {1: 4}
+    assert sorted(got) == sorted(ref)
+    for li in ref:
+        assert abs(got[li] - ref[li]) <= 1e-4 * max(1.0, abs(ref[li])), (li, got[li], ref[li])
+    assert max(abs(v) for v in ref.values()) < 1e6
+    assert res[0]["last_loss"] is not None and abs(res[0]["last_loss"] - eng.last_loss) < 1e-3

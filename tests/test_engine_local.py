@@ -250,3 +250,49 @@ def test_phase_tracer_breakdown(tmp_path):
     eng2 = _engine(nodes=2)
     eng2.train_step(next(_batches(1)))
     assert eng2.tracer.summary() == {}
+
+
+def test_shadow_snapshot_restores_compromised_stage():
+    """A compromised stage's layers are rebuilt from the trusted copy its ring neighbour holds,
+    not from its own (tampered) memory."""
+    eng = _engine(nodes=3, shadow_interval=2)
+    for b in _batches(4):
+        eng.train_step(b)
+    eng.flush()
+    assert 1 in eng._shadow_meta and eng._shadow_meta[1][2] == 2   # node 1's copy lives on node 2
+    snap_step, (a, b), _ = eng._shadow_meta[1]
+    st1 = eng.stages[1]
+    assert st1.layer_range == (a, b)
+    snap = torch.cat([eng._pack_layer(st1, li) for li in range(a, b)]).clone()
+    assert torch.equal(snap, eng._shadow_data[1])      # no step since the last snapshot
+    with torch.no_grad():
+        st1.flat.master.add_(1000.0)                    # tampering with the stage's own memory
+    eng.reassign([1], step=eng.global_step)
+    rec = eng.reassignment_history[-1]
+    assert rec["restored_from_shadow"] == {1: snap_step}
+    assert 1 not in eng.plan.ranks
+    got = []
+    for li in range(a, b):
+        owner = eng.plan.owner_of_layer(li)
+        got.append(eng._pack_layer(eng.stages[owner], li))
+    assert torch.equal(torch.cat(got), snap)
+    # training continues on the new plan and re-snapshots on the new ring
+    for bb in _batches(2, seed=1):
+        eng.train_step(bb)
+    eng.flush()
+    assert eng.last_loss is not None and eng.last_loss < 100
+
+
+def test_shadow_not_committed_for_flagged_step():
+    eng = _engine(nodes=3, shadow_interval=1)
+    eng.train_step(next(_batches(1)))
+    eng.flush()
+    assert set(eng._shadow_meta) == {0, 1, 2}
+    old = eng._shadow_meta[1][0]
+    eng.train_step(next(_batches(1, seed=3)))
+    # pretend node 1 was blamed at this step: its pending copy must be dropped
+    step = eng.global_step
+    eng._consume_reports(upto=step - 1)
+    N = eng.num_nodes
+    eng._commit_shadows(step, [n == 1 for n in range(N)], [0] * N)
+    assert eng._shadow_meta[1][0] == old and eng._shadow_meta[0][0] == step

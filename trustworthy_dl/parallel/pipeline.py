@@ -71,6 +71,8 @@ class EngineConfig:
     outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
+    shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
+                                         # (0 = off); a compromised stage is restored from it, not from itself
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
     layer_granularity: str = "auto"      # "block" | "half" (GPT-2 attention / MLP halves as pipeline
@@ -133,6 +135,7 @@ class PipelineEngine:
         self.ties = tied_groups(model)
         self.last_loss: Optional[float] = None
         self._pending: deque = deque()
+        self._reset_shadows()
         self._host_metrics: Dict[int, List[float]] = {}
         self._comm_wait = 0.0
         self._step_time = 0.0
@@ -746,6 +749,8 @@ class PipelineEngine:
             if self.cfg.param_integrity:
                 st.param_checksum = dstats.checksum(st.flat.data, getattr(st, "param_checksum", None))
         self.tracer.end(to)
+        if self._shadow_enabled() and self.global_step % self.cfg.shadow_interval == 0:
+            self._take_shadow()
         if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
             self._audit_params()
         # queue the host report (pinned, non-blocking)
@@ -995,6 +1000,7 @@ class PipelineEngine:
             if (statuses[n] == OFF) != (prev_status.get(n) == NodeStatus.OFFLINE):
                 self.node_events.append({"node_id": n, "step": step, "timestamp": time.time(),
                                          "event": "offline" if statuses[n] == OFF else "online"})
+        self._commit_shadows(step, blamed, statuses)
         newly = [n for n in range(N) if n in present and statuses[n] == STATUS_CODES[NodeStatus.COMPROMISED]
                  and prev_status.get(n) != NodeStatus.COMPROMISED]
         newly += [n for n in range(N) if n in present and statuses[n] == STATUS_CODES[NodeStatus.COMPROMISED]
@@ -1033,7 +1039,8 @@ class PipelineEngine:
         keep = keep[: self.num_layers]
         new_plan = make_plan(self.costs, keep, self.plan.version + 1, self.cfg.balanced_partition)
         t0 = time.perf_counter()
-        moved = self._migrate(new_plan)
+        restored = {c: self._shadow_meta[c][0] for c in compromised if self._shadow_usable(c)}
+        moved = self._migrate(new_plan, restore=list(restored))
         dt = time.perf_counter() - t0
         self.excluded = sorted(set(self.excluded) | set(compromised))
         to_nodes = sorted({new_plan.owner_of_layer(li) for li in range(self.num_layers)
@@ -1042,6 +1049,7 @@ class PipelineEngine:
                "to_nodes": to_nodes, "timestamp": time.time(), "migration_time": dt,
                "estimated_migration_time": self.estimate_migration_time(moved),
                "moved_params": moved, "step": step if step is not None else self.global_step,
+               "restored_from_shadow": restored,
                "plan": new_plan.describe()}
         self.reassignment_history.append(rec)
         logger.warning("Reassigned tasks from %s -> %s in %.3fs; new plan %s", compromised, to_nodes, dt,
@@ -1086,9 +1094,16 @@ class PipelineEngine:
             b.copy_(vec[off:off + n].view(b.shape).to(b.dtype))
             off += n
 
-    def _migrate(self, new_plan: PlacementPlan) -> int:
+    def _migrate(self, new_plan: PlacementPlan, restore: Sequence[int] = ()) -> int:
+        """Move every layer to its new owner.  Layers of the nodes in ``restore`` come from their
+        last committed shadow snapshot (held by a trusted neighbour), not from the node itself."""
         old_plan = self.plan
         self._old_owner = {li: old_plan.owner_of_layer(li) for li in range(self.num_layers)}
+        from_shadow: Dict[int, int] = {}     # layer -> holder rank serving it from a shadow
+        for c in restore:
+            a, b = self._shadow_meta[c][1]
+            for li in range(a, b):
+                from_shadow[li] = self._shadow_meta[c][2]
         step_count = next(iter(self.stages.values())).flat.step_count if self.stages else 0
         packed: Dict[int, torch.Tensor] = {}
         moved = 0
@@ -1096,8 +1111,11 @@ class PipelineEngine:
             sends, recvs = [], []
             for li in range(self.num_layers):
                 src, dst = old_plan.owner_of_layer(li), new_plan.owner_of_layer(li)
+                if li in from_shadow:
+                    src = from_shadow[li]
                 if src == self.rank:
-                    vec = self._pack_layer(self.stages[self.rank], li)
+                    vec = (self._shadow_slice(li) if li in from_shadow
+                           else self._pack_layer(self.stages[self.rank], li))
                     if dst == self.rank:
                         packed[li] = vec
                     else:
@@ -1115,7 +1133,8 @@ class PipelineEngine:
         else:
             for li in range(self.num_layers):
                 src, dst = old_plan.owner_of_layer(li), new_plan.owner_of_layer(li)
-                packed[li] = self._pack_layer(self.stages[src], li).cpu()
+                packed[li] = (self._shadow_slice(li).cpu() if li in from_shadow
+                              else self._pack_layer(self.stages[src], li).cpu())
                 if src != dst:
                     moved += self._layer_numel(li)
         old_verifiers = {n: st.verifier for n, st in self.stages.items()}
@@ -1134,7 +1153,82 @@ class PipelineEngine:
             if ov is not None and ov.S == st.verifier.S:
                 st.verifier.load_state_dict(ov.state_dict())
         self._shape_cache = {}
+        self._reset_shadows()                # the snapshot ring follows the plan: re-taken next interval
         return moved
+
+    # ================================================================== trusted shadow snapshots
+    # SURVEY 5 ("shadow copies of each stage's weights on a neighbour GPU"): every
+    # ``shadow_interval`` steps each stage packs its layers (fp32 master + AdamW moments + buffers,
+    # the migration format) and sends them over xGMI to the next stage of the ring, which keeps the
+    # copy in HBM (~0.5 GB for a GPT-2-medium stage).  The copy is committed only when that step's
+    # report shows the stage unflagged; a stage later marked compromised is rebuilt from its last
+    # committed copy instead of from its own (possibly tampered) memory.  Metadata (step, layer
+    # range, holder) is tracked identically on every rank; only the holder keeps the data.
+    def _reset_shadows(self):
+        self._shadow_meta: Dict[int, Tuple[int, Tuple[int, int], int]] = {}   # owner -> committed (step, range, holder)
+        self._shadow_pend_meta: Dict[int, Tuple[int, Tuple[int, int], int]] = {}
+        self._shadow_data: Dict[int, torch.Tensor] = {}      # owner -> committed vector (holder only)
+        self._shadow_pend: Dict[int, Tuple[int, torch.Tensor]] = {}
+
+    def _shadow_enabled(self) -> bool:
+        return self.cfg.shadow_interval > 0 and self.dp == 1 and self.plan.num_stages > 1
+
+    def _shadow_holder(self, node: int) -> int:
+        ranks = self.plan.ranks
+        return ranks[(ranks.index(node) + 1) % len(ranks)]
+
+    def _shadow_usable(self, c: int) -> bool:
+        if c not in self._shadow_meta:
+            return False
+        holder = self._shadow_meta[c][2]
+        return holder not in self.excluded and self.trust.can_assign_task(holder)
+
+    def _shadow_slice(self, li: int) -> torch.Tensor:
+        for c, (_, (a, b), holder) in self._shadow_meta.items():
+            if a <= li < b:
+                off = sum(self._packed_numel(k) for k in range(a, li))
+                return self._shadow_data[c][off:off + self._packed_numel(li)]
+        raise KeyError(li)
+
+    @torch.no_grad()
+    def _take_shadow(self):
+        step = self.global_step
+        owners = list(self.plan.ranks)
+        for node, rng in zip(self.plan.ranks, self.plan.ranges):
+            self._shadow_pend_meta[node] = (step, tuple(rng), self._shadow_holder(node))
+        if self.distributed:
+            st = self.my_stage()
+            if st is None:
+                return
+            i = owners.index(self.rank)
+            pred = owners[(i - 1) % len(owners)]
+            a, b = self.plan.ranges[(i - 1) % len(owners)]
+            vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
+            buf = torch.empty(sum(self._packed_numel(li) for li in range(a, b)), dtype=torch.float32,
+                              device=self.device)
+            batched_transfer([(vec, self._shadow_holder(self.rank))], [(buf, pred)])
+            self._shadow_pend[pred] = (step, buf)
+        else:
+            for node, st in self.stages.items():
+                dev = self.stages[self._shadow_holder(node)].device
+                vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
+                self._shadow_pend[node] = (step, vec.to(dev, copy=True))
+
+    def _commit_shadows(self, step: int, blamed: Sequence[bool], statuses: Sequence[int]):
+        bad = (STATUS_CODES[NodeStatus.COMPROMISED], STATUS_CODES[NodeStatus.SUSPICIOUS])
+        for owner, meta in list(self._shadow_pend_meta.items()):
+            if meta[0] != step:
+                continue
+            del self._shadow_pend_meta[owner]
+            data = self._shadow_pend.pop(owner, None)
+            if data is not None and data[0] != step:   # a newer snapshot replaced it: keep that one
+                self._shadow_pend[owner] = data
+                data = None
+            if blamed[owner] or statuses[owner] in bad:
+                continue
+            self._shadow_meta[owner] = meta
+            if data is not None:
+                self._shadow_data[owner] = data[1]
 
     # ================================================================== evaluation
     @torch.no_grad()
