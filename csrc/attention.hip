@@ -24,6 +24,17 @@
 
 // Block-order mode: default = every head's block y dispatched together across heads (LPT over the
 // whole grid); TDL_ATTN_MAP=xcd -> one head's blocks back to back on one XCD (head_xcd_map).
+// dK/dV query-tile depth (32-row sub-tiles per barrier): TDL_ATTN_DKDV_NS=1|2 (default 1).  NS=2
+// measured slower on MI355X (B=32 H=16 T=1024 causal bwd: 306.6 vs 327.6 TFLOP/s; the second
+// staging register set and sub-tile loop cost more than the halved barrier count saves).
+static int dkdv_ns() {
+    static int ns = [] {
+        const char* e = std::getenv("TDL_ATTN_DKDV_NS");
+        return (e && e[0] == '2') ? 2 : 1;
+    }();
+    return ns;
+}
+
 static int attn_nbh_arg(int nbh) {
     const char* e = std::getenv("TDL_ATTN_MAP");
     return (e && std::strcmp(e, "xcd") == 0) ? -nbh : nbh;
@@ -257,16 +268,18 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------- dK, dV (key-owned)
-// Workgroup = 128 keys (4 waves x 32, key on the MFMA lane); walks query tiles of 32 with a
-// double-buffered LDS pipeline: the next tile's Q / dO / lse / delta are loaded into registers
-// while the current tile computes, then written to the other buffer -> ONE barrier per tile.
-// Products per tile and wave: S = Q.K^T, dP = dO.V^T (row-read A, K/V fragments resident in
-// registers), dV^T += dO^T.P and dK^T += Q^T.dS (tr-read A, S/dP accumulators as B operands).
-template <bool CAUSAL>
+// Workgroup = 128 keys (4 waves x 32, key on the MFMA lane); walks query tiles of BQ = 32 NS rows
+// with a double-buffered LDS pipeline: the next tile's Q / dO / lse / delta are loaded into
+// registers while the current tile computes, then written to the other buffer -> ONE barrier per
+// tile.  NS = 2 halves the barriers per MFMA (16 -> 32 MFMAs per wave between barriers) at twice
+// the LDS (64 KB, still 2 workgroups per CU) but measures slower (see dkdv_ns).
+// Products per 32-row sub-tile and wave: S = Q.K^T, dP = dO.V^T (row-read A, K/V fragments
+// resident in registers), dV^T += dO^T.P and dK^T += Q^T.dS (tr-read A, S/dP accumulators as B).
+template <bool CAUSAL, int NS>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                                             bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
-    constexpr int BK = 128, BQ = 32;
+    constexpr int BK = 128, BQ = 32 * NS;
     // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
     // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
     __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
@@ -300,20 +313,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     }
     f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
-    const int q_start = CAUSAL ? kblk : 0;
-    const int srow = tid >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 tile per operand
-
-    const int swz = ((sch ^ (srow & 7)) * 8);
+    const int q_start = CAUSAL ? kblk : 0;   // multiple of 128, so BQ (32 or 64) tiles end at T
+    const int srow = tid >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 slab per operand
+    const int swz = ((sch ^ (srow & 7)) * 8);  // (srow + 32 j) & 7 == srow & 7
     constexpr float LOG2E = 1.4426950408889634f;
     const float sl2 = scale * LOG2E;
     // prologue: tile q_start -> buffer 0
-    {
-        const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + srow) * ldq + sch * 8);
-        const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + srow) * ldo + sch * 8);
-        *(uint4*)(Qs[0] + srow * HD + sch * 8) = q;
-        *(uint4*)(Qw[0] + srow * HD + swz) = q;
-        *(uint4*)(dOs[0] + srow * HD + sch * 8) = d;
-        *(uint4*)(dOw[0] + srow * HD + swz) = d;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const int row = srow + 32 * j;
+        const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + row) * ldq + sch * 8);
+        const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + row) * ldo + sch * 8);
+        *(uint4*)(Qs[0] + row * HD + sch * 8) = q;
+        *(uint4*)(Qw[0] + row * HD + swz) = q;
+        *(uint4*)(dOs[0] + row * HD + sch * 8) = d;
+        *(uint4*)(dOw[0] + row * HD + swz) = d;
     }
     if (tid < BQ) {
         lse_s[0][tid] = lse_row[q_start + tid] * LOG2E;
@@ -324,21 +338,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     int buf = 0;
     for (int qt = q_start; qt < T; qt += BQ) {
         const bool has_next = qt + BQ < T;
-        uint4 qn = make_uint4(0, 0, 0, 0), dn = make_uint4(0, 0, 0, 0);
+        uint4 qn[NS], dn[NS];
         float ln = 0.f, dln = 0.f;
         if (has_next) {
-            qn = *(const uint4*)(qbase + (size_t)(qt + BQ + srow) * ldq + sch * 8);
-            dn = *(const uint4*)(dobase + (size_t)(qt + BQ + srow) * ldo + sch * 8);
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                qn[j] = *(const uint4*)(qbase + (size_t)(qt + BQ + srow + 32 * j) * ldq + sch * 8);
+                dn[j] = *(const uint4*)(dobase + (size_t)(qt + BQ + srow + 32 * j) * ldo + sch * 8);
+            }
             if (tid < BQ) {
                 ln = lse_row[qt + BQ + tid] * LOG2E;
                 dln = delta_row[qt + BQ + tid];
             }
         }
-        const bf16_t* Qb = Qs[buf];
-        const bf16_t* dOb = dOs[buf];
-        const bf16_t* Qr = Qw[buf];
-        const bf16_t* dOr = dOw[buf];
-        if (!CAUSAL || qt + BQ - 1 >= k0) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const int qs = qt + 32 * j;   // this sub-tile's first query
+            if (CAUSAL && qs + 31 < k0) continue;
+            const bf16_t* Qb = Qs[buf] + 32 * j * HD;
+            const bf16_t* dOb = dOs[buf] + 32 * j * HD;
+            const bf16_t* Qr = Qw[buf] + 32 * j * HD;
+            const bf16_t* dOr = dOw[buf] + 32 * j * HD;
+            const float* lsb = lse_s[buf] + 32 * j;
+            const float* dlb = delta_s[buf] + 32 * j;
             f32x16 sacc = {}, dpacc = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
@@ -351,10 +373,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                float p = fast_exp2(fmaf(sacc[i], sl2, -lse_s[buf][ql]));
-                if (CAUSAL && kj > qt + ql) p = 0.f;
+                float p = fast_exp2(fmaf(sacc[i], sl2, -lsb[ql]));
+                if (CAUSAL && kj > qs + ql) p = 0.f;
                 sacc[i] = p;
-                dpacc[i] = p * (dpacc[i] - delta_s[buf][ql]);
+                dpacc[i] = p * (dpacc[i] - dlb[ql]);
             }
             const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
             const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
@@ -374,10 +396,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
             }
         }
         if (has_next) {
-            *(uint4*)(Qs[buf ^ 1] + srow * HD + sch * 8) = qn;
-            *(uint4*)(Qw[buf ^ 1] + srow * HD + swz) = qn;
-            *(uint4*)(dOs[buf ^ 1] + srow * HD + sch * 8) = dn;
-            *(uint4*)(dOw[buf ^ 1] + srow * HD + swz) = dn;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                const int row = srow + 32 * j;
+                *(uint4*)(Qs[buf ^ 1] + row * HD + sch * 8) = qn[j];
+                *(uint4*)(Qw[buf ^ 1] + row * HD + swz) = qn[j];
+                *(uint4*)(dOs[buf ^ 1] + row * HD + sch * 8) = dn[j];
+                *(uint4*)(dOw[buf ^ 1] + row * HD + swz) = dn[j];
+            }
             if (tid < BQ) {
                 lse_s[buf ^ 1][tid] = ln;
                 delta_s[buf ^ 1][tid] = dln;
@@ -539,12 +565,15 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;
     auto dQKV = (bf16_t*)dqkv;
+    const int nb = attn_nbh_arg(B * H);
     if (causal) {
-        attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
-        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else attn_bwd_dkdv_kernel<true, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
     } else {
-        attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
-        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, attn_nbh_arg(B * H), scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else attn_bwd_dkdv_kernel<false, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
     }
     TDL_LAUNCH_CHECK();
 }
