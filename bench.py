@@ -34,6 +34,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# before the first GPU call (torch.cuda.is_available() below starts the HIP runtime): RCCL streams
+# on hardware queues of their own, so pre-posted receives never block compute (runtime/hwqueues.py)
+from trustworthy_dl.runtime.hwqueues import ensure_hw_queues, effective_hw_queues  # noqa: E402
+ensure_hw_queues()
+
 
 # Single-GPU GPT-2-medium throughput (k tokens/s) per micro-batch size, from per-unit fwd+bwd
 # timings on MI355X (scripts/time_units.py at micro-batch 4/8/16/32: 24 blocks + LM head +
@@ -156,7 +161,8 @@ def main():
                        "micro_batch": mbs, "micro_batches": M,
                        "parallelism": f"pp{stages}" + (f"xdp{dp}" if dp > 1 else ""),
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
-                       "plan": engine.plan.describe(), "last_loss": engine.last_loss},
+                       "plan": engine.plan.describe(), "last_loss": engine.last_loss,
+                       "p2p_mode": engine.p2p_mode, "hw_queues": effective_hw_queues()},
         }
         print(json.dumps(line), flush=True)
     if args.trace_phases:

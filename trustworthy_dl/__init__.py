@@ -5,6 +5,11 @@ GradientVerifier, AdversarialAttacker, get_model.
 """
 __version__ = "0.1.0"
 
+# before anything touches the GPU: enough HIP hardware queues that the pipeline's pre-posted RCCL
+# receives never share a queue with the compute stream (runtime/hwqueues.py)
+from .runtime.hwqueues import ensure_hw_queues as _ensure_hw_queues
+_ensure_hw_queues()
+
 from .core.trust_manager import TrustManager, NodeStatus  # noqa: F401
 from .security.attack_detection import AttackDetector, AttackType  # noqa: F401
 from .security.gradient_verification import GradientVerifier  # noqa: F401

@@ -129,6 +129,7 @@ class PipelineEngine:
         self.reassignment_history: List[Dict] = []
         self.excluded: List[int] = []
         self.state_flags = {"under_attack": False}
+        self.p2p_mode = self._choose_p2p_mode(cfg)
         self.granularity = self._choose_granularity(model, cfg)
         self.layers = model.pipeline_layers()
         self.num_layers = len(self.layers)
@@ -245,7 +246,7 @@ class PipelineEngine:
         prev = self.plan.ranks[s - 1] if s is not None and s > 0 else None
         nxt = self.plan.ranks[s + 1] if s is not None and s + 1 < self.plan.num_stages else None
         self.comm = P2PComm(prev, nxt, self.device)
-        if self.cfg.p2p_mode == "async" and getattr(self, "_dir_groups", None) is None:
+        if self.p2p_mode == "async" and getattr(self, "_dir_groups", None) is None:
             # one communicator for activations (stage s -> s+1), one for activation gradients
             # (s+1 -> s): each carries one-way, in-order traffic per neighbour pair
             everyone = list(range(self.world))
@@ -269,6 +270,23 @@ class PipelineEngine:
                 self._warm_group(g, [d * self.pp + pos for d in range(self.dp)])
                 if pos == self.rank % self.pp:
                     self.dp_group = g
+
+    def _choose_p2p_mode(self, cfg: EngineConfig) -> str:
+        """Pre-posted receives ("async") need the RCCL streams on hardware queues of their own:
+        an RCCL receive spins until its data lands, and a compute kernel queued behind it on a shared
+        queue cannot run (runtime/hwqueues.py, profiles/r1_hwqueue_probe.json).  When the HIP runtime
+        started with too few queues (GPU touched before ``trustworthy_dl`` was imported, or
+        TDL_KEEP_HW_QUEUES=1), fall back to grouped exchanges, which post a receive only where the
+        compute needs its data anyway."""
+        mode = cfg.p2p_mode
+        if mode == "async" and self.distributed and dist.get_backend() == "nccl":
+            from ..runtime.hwqueues import ENGINE_QUEUES, effective_hw_queues
+            q = effective_hw_queues()
+            if q < ENGINE_QUEUES:
+                logger.warning("GPU_MAX_HW_QUEUES=%d < %d: pipeline P2P falls back to grouped exchanges",
+                               q, ENGINE_QUEUES)
+                mode = "grouped"
+        return mode
 
     def _warm_group(self, group, members: List[int]):
         """One 1-element all-reduce by every member, right after the group is created (groups are
@@ -389,7 +407,7 @@ class PipelineEngine:
 
     # ------------------------------------------------------------------ distributed 1F1B schedule
     def _run_1f1b(self, inputs, targets, truth) -> Optional[torch.Tensor]:
-        if self.cfg.p2p_mode == "async":
+        if self.p2p_mode == "async":
             return self._run_1f1b_async(inputs, targets, truth)
         st = self.my_stage()
         if st is None:
