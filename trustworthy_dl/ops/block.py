@@ -31,7 +31,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import ptr, stream_ptr
-from .layers import _f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, run_or_defer, wgrad_acc
+from .layers import (_f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, bump_weight_generation,  # noqa: F401
+                     fwd_weight, run_or_defer, wgrad_acc)
 
 _FUSED_WIDTHS = (256, 512, 768, 1024, 1280, 1536, 2048)
 
@@ -151,15 +152,15 @@ class _GPT2BlockFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         h1, mean1, rstd1 = _ln_fwd(x2, ln1_w, ln1_b, eps)
-        qkv = torch.addmm(b_qkv, h1, w_qkv)
+        qkv = torch.addmm(b_qkv, h1, fwd_weight(w_qkv))
         o, lse, scale = attn_fwd(qkv.view(B, T, 3 * C), n_head, True)
         o2 = o.view(B * T, C)
-        z = torch.mm(o2, w_o)
+        z = torch.mm(o2, fwd_weight(w_o))
         y1, y, h2, mean2, rstd2 = _add_bias_ln_fwd(x2, z, b_o, b_p, ln2_w, ln2_b, eps, (B, T, C))
         del z
-        pre = torch.mm(h2, w_fc)
+        pre = torch.mm(h2, fwd_weight(w_fc))
         f = _bias_gelu_fwd(pre, b_fc)
-        _addmm_inplace(y.view(B * T, C), f, w_p)  # y = y1 + bp + f @ Wp
+        _addmm_inplace(y.view(B * T, C), f, fwd_weight(w_p))  # y = y1 + bp + f @ Wp
         ctx.save_for_backward(x2, h1, mean1, rstd1, qkv, o2, lse, y1, h2, mean2, rstd2, pre, f,
                               ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, w_fc, b_fc, w_p, b_p)
         ctx.dims = (B, T, C, n_head, scale)

@@ -141,6 +141,44 @@ def layer_norm(x, weight, bias, eps: float = 1e-5):
 
 
 # ============================================================== Linear (HF Conv1D layout: weight [in, out])
+# ---------------------------------------------------------------- forward-layout weight copies
+# hipBLASLt on gfx950 runs Y = X @ W fastest with W stored [out, in] (the "NT" form) and the input
+# gradient dX = dY @ W^T fastest with W stored [in, out] (scripts/gemm_layout_probe.py,
+# profiles/r1_gemm_layout_probe.jsonl: GPT-2-medium block shapes, 16k-32k tokens, forward
+# +11-26 %, dgrad -12-16 % when the layout is swapped).  The parameters keep the HF [in, out]
+# layout (checkpoints, dgrad); each forward GEMM reads a transposed bf16 copy that is rebuilt
+# once per weight generation.  Generations advance on every optimizer update and at the start of
+# every engine step (which covers re-shards, restores, checkpoint loads and injected parameter
+# attacks); torch in-place writes are caught by the tensor version counter.
+_WEIGHT_GEN = [0]
+
+
+def bump_weight_generation() -> None:
+    _WEIGHT_GEN[0] += 1
+
+
+def _fwd_layout_enabled() -> bool:
+    return os.environ.get("TDL_FWD_WEIGHT_T", "1") != "0"
+
+
+def fwd_weight(w: torch.Tensor) -> torch.Tensor:
+    """Operand for ``x @ W`` with W = ``w`` [in, out]: a view of a cached [out, in] copy on the
+    GPU (same values, faster GEMM form), ``w`` itself elsewhere."""
+    if not (w.is_cuda and w.dim() == 2 and _fwd_layout_enabled()):
+        return w
+    key = (_WEIGHT_GEN[0], w._version, w.data_ptr())
+    cached = getattr(w, "_tdl_fwd_t", None)
+    if cached is not None and cached[0] == key:
+        return cached[1].t()
+    if cached is not None and cached[1].shape == (w.shape[1], w.shape[0]) and cached[1].dtype == w.dtype:
+        wt = cached[1]
+    else:
+        wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+    wt.copy_(w.t())
+    w._tdl_fwd_t = (key, wt)
+    return wt.t()
+
+
 def _gemm_backend(t: torch.Tensor) -> str:
     """GEMM route for GPU tensors: ``torch`` (default: torch.mm on the hipBLASLt build torch ships
     with) or ``blaslt`` (direct binding, csrc/blaslt.hip; opt-in via TDL_GEMM=blaslt — it links the
@@ -255,12 +293,13 @@ class _Linear(torch.autograd.Function):
                 y = F.gelu(y, approximate="tanh")
         else:  # torch GEMM + native bias-GELU kernel
             if act == "gelu":
-                pre = torch.mm(x2, weight)
+                pre = torch.mm(x2, fwd_weight(weight))
                 y = torch.empty_like(pre)
                 _lib.call("tdl_bias_gelu_fwd", ptr(pre), ptr(bias), ptr(y), pre.shape[0], pre.shape[1],
                           stream_ptr(x.device))
             else:
-                y = torch.addmm(bias, x2, weight) if bias is not None else torch.mm(x2, weight)
+                wf = fwd_weight(weight)
+                y = torch.addmm(bias, x2, wf) if bias is not None else torch.mm(x2, wf)
         ctx.save_for_backward(x2, weight, bias, pre)
         ctx.act = act
         ctx.backend = backend

@@ -25,6 +25,7 @@ import torch.nn as nn
 
 from ..ops import _lib
 from ..ops._lib import ptr, stream_ptr
+from ..ops.layers import bump_weight_generation
 
 
 def _no_decay(name: str, p: torch.Tensor) -> bool:
@@ -108,6 +109,7 @@ class FlatParams:
                           ptr(self.grad[lo:]), ptr(None if self.data is self.master else self.data[lo:]),
                           n, cfg.lr, b1, b2, cfg.eps, wd, bc1, bc2,
                           ptr(ctrl), int(zero_grad), stream_ptr(self.device))
+            bump_weight_generation()   # compute weights rewritten in place: forward-layout copies are stale
             return
         scale = 1.0 if ctrl is None else float(ctrl[0])
         skip = False if ctrl is None else bool(float(ctrl[1]) != 0.0)

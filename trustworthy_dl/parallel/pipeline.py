@@ -35,6 +35,7 @@ import torch.nn as nn
 from ..core.trust_manager import (METRIC_NAMES, NodeStatus, STATUS_CODES, STATUS_FROM_CODE, TrustManager)
 from ..security import stage_verifier as SV
 from ..ops import stats as dstats
+from ..ops.layers import bump_weight_generation
 from ..ops.layers import defer_weight_grads
 from ..runtime.tracing import PhaseTracer
 from .comm import P2PComm, all_gather_rows, batched_transfer
@@ -332,6 +333,7 @@ class PipelineEngine:
         host never stalls the device queue, and collective decisions such as a re-shard happen
         at the same step everywhere); ``flush()`` drains the rest."""
         self._consume_reports(upto=self.global_step + 1 - self.REPORT_LAG)
+        bump_weight_generation()   # weights may have changed since the last step (update, re-shard, restore, load)
         self.global_step += 1
         self.trust.advance_step(self.global_step)
         t0 = time.perf_counter()
@@ -1252,6 +1254,7 @@ class PipelineEngine:
     @torch.no_grad()
     def eval_step(self, batch: Dict[str, torch.Tensor]) -> float:
         """Forward-only loss over the global batch (no detector side effects: reference A21 fixed)."""
+        bump_weight_generation()
         M = self.cfg.micro_batches
         inp, tgt = batch["input"], batch["target"]
         if self.dp > 1:
