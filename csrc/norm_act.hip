@@ -707,3 +707,44 @@ TDL_API int tdl_scale_bf16(const void* x, void* y, const float* scale, int64_t n
     scale_bf16_kernel<<<(int)(blocks < 4096 ? blocks : 4096), 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, scale, n8);
     TDL_LAUNCH_CHECK();
 }
+
+// ============================================================== bf16 transpose: out[C,R] = in[R,C]^T
+// Builds the [out, in] forward-GEMM copy of a block weight once per weight generation
+// (ops/layers.py fwd_weight).  64x64 tile per 256-thread block: every lane moves 16 B per access
+// on both sides (8 lanes cover one 128-B row segment), the turn happens in LDS.  A row of the LDS
+// tile is 64 + 2 bf16 wide so the column reads of one wave spread over the banks.  R % 64 == 0 and
+// C % 64 == 0 (checked by the entry point).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                             int R, int C) {
+    constexpr int LDW = 66;
+    __shared__ unsigned short tile[64 * LDW];
+    const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+    const unsigned short* src = reinterpret_cast<const unsigned short*>(in);
+    unsigned short* dst = reinterpret_cast<unsigned short*>(out);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int v = threadIdx.x + h * 256;          // 512 vectors of 8 bf16
+        const int r = v >> 3, cg = (v & 7) * 8;
+        const uint4 q = *reinterpret_cast<const uint4*>(src + (size_t)(r0 + r) * C + c0 + cg);
+        const unsigned short* e = reinterpret_cast<const unsigned short*>(&q);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) tile[r * LDW + cg + k] = e[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int v = threadIdx.x + h * 256;
+        const int c = v >> 3, rg = (v & 7) * 8;
+        uint4 q;
+        unsigned short* e = reinterpret_cast<unsigned short*>(&q);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e[k] = tile[(rg + k) * LDW + c];
+        *reinterpret_cast<uint4*>(dst + (size_t)(c0 + c) * R + r0 + rg) = q;
+    }
+}
+
+TDL_API int tdl_transpose_bf16(const void* in, void* out, int R, int C, hipStream_t s) {
+    if (R % 64 || C % 64 || R <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+    transpose_bf16_kernel<<<dim3(C / 64, R / 64), 256, 0, s>>>((const bf16_t*)in, (bf16_t*)out, R, C);
+    TDL_LAUNCH_CHECK();
+}

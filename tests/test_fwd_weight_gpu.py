@@ -29,6 +29,17 @@ def test_fwd_weight_exact_cached_and_refreshed():
     assert torch.equal(B.fwd_weight(w), w)
 
 
+@pytest.mark.parametrize("R,C", [(1024, 3072), (4096, 1024), (64, 128), (192, 64)])
+def test_native_transpose_matches_torch(R, C):
+    from trustworthy_dl.ops import _lib
+    from trustworthy_dl.ops._lib import ptr, stream_ptr
+    w = torch.randn(R, C, device="cuda").to(torch.bfloat16)
+    out = torch.empty(C, R, dtype=torch.bfloat16, device="cuda")
+    _lib.call("tdl_transpose_bf16", ptr(w), ptr(out), R, C, stream_ptr(w.device))
+    torch.cuda.synchronize()
+    assert torch.equal(out, w.t())
+
+
 def _batches(n, bs=8, T=128, seed=0):
     g = torch.Generator().manual_seed(seed)
     out = []

@@ -174,7 +174,11 @@ def fwd_weight(w: torch.Tensor) -> torch.Tensor:
         wt = cached[1]
     else:
         wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
-    wt.copy_(w.t())
+    R, C = w.shape
+    if w.dtype == torch.bfloat16 and w.is_contiguous() and R % 64 == 0 and C % 64 == 0:
+        _lib.call("tdl_transpose_bf16", ptr(w), ptr(wt), R, C, stream_ptr(w.device))
+    else:
+        wt.copy_(w.t())
     w._tdl_fwd_t = (key, wt)
     return wt.t()
 
