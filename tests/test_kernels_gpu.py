@@ -444,3 +444,38 @@ def test_fused_lm_head_cross_entropy_matches_fp32(chunk):
     (lm_head_cross_entropy(x2, w2, labels, V, chunk_rows=chunk) * 0.5).backward()
     assert w2.grad is None
     assert _rel(w2.main_grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("V,ld", [(50257, 50304), (32000, 32000), (1000, 1024)])
+def test_xent_fused_rows_vs_fp32(V, ld):
+    """tdl_xent_fused on full GPT-2-vocab rows (register-resident kernel, 25 vectors per lane), a
+    32k vocab (16-vector bucket) and a small padded row: loss, lse and in-place dlogits vs fp32."""
+    from trustworthy_dl.ops import _lib
+    from trustworthy_dl.ops._lib import ptr, stream_ptr
+    torch.manual_seed(1)
+    M = 64
+    logits = (torch.randn(M, ld, device=DEV) * 3.0).bfloat16()
+    labels = torch.randint(0, V, (M,), device=DEV)
+    labels[::5] = -100
+    ref_in = logits.float()[:, :V]
+    loss = torch.empty(M, device=DEV)
+    lse = torch.empty(M, device=DEV)
+    n_valid = int((labels != -100).sum())
+    scale = torch.tensor([1.0 / n_valid], device=DEV)
+    buf = logits.clone()
+    _lib.call("tdl_xent_fused", ptr(buf), ptr(labels), ptr(loss), ptr(lse), ptr(scale), M, V, ld,
+              stream_ptr(buf.device))
+    torch.cuda.synchronize()
+    ref_lse = torch.logsumexp(ref_in, dim=1)
+    assert torch.allclose(lse, ref_lse, rtol=1e-5, atol=1e-4)
+    valid = labels != -100
+    ref_loss = ref_lse - ref_in.gather(1, labels.clamp(min=0)[:, None])[:, 0]
+    assert torch.allclose(loss[valid], ref_loss[valid], rtol=1e-4, atol=1e-3)
+    assert torch.all(loss[~valid] == 0)
+    p = torch.softmax(ref_in, dim=1)
+    p[valid, labels[valid]] -= 1.0
+    p[~valid] = 0
+    ref_d = p / n_valid
+    d = buf.float()
+    assert _rel(d[:, :V], ref_d) < 1e-2
+    assert torch.all(d[:, V:] == 0)
