@@ -448,8 +448,8 @@ def test_fused_lm_head_cross_entropy_matches_fp32(chunk):
 
 @pytest.mark.parametrize("V,ld", [(50257, 50304), (32000, 32000), (1000, 1024)])
 def test_xent_fused_rows_vs_fp32(V, ld):
-    """tdl_xent_fused on full GPT-2-vocab rows (register-resident kernel, 25 vectors per lane), a
-    32k vocab (16-vector bucket) and a small padded row: loss, lse and in-place dlogits vs fp32."""
+    """tdl_xent_fused on full GPT-2-vocab rows, a 32k vocab and a small padded row: loss, lse and
+    in-place dlogits vs fp32 (the default two-pass kernel; TDL_XENT_REG=1 runs the register one)."""
     from trustworthy_dl.ops import _lib
     from trustworthy_dl.ops._lib import ptr, stream_ptr
     torch.manual_seed(1)
