@@ -248,23 +248,31 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
 
 // ============================================================================ backward
 // delta[bh, t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
+// Lane = 8 consecutive elements, so a wave instruction reads 1 KB contiguous of O and of dO (8 heads
+// of one token); the 8 lanes of a head reduce by xor-shuffles and one of them stores the head's delta.
+static_assert(HD / 8 == 8, "delta kernel: 8 lanes per head row");
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
                                                          float* __restrict__ delta, int B, int T, int H) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over B*T*H
-    if (idx >= B * T * H) return;
-    const int hd = idx % H, bt = idx / H, b = bt / T, t = bt - b * T;
-    const bf16_t* op = o + (size_t)bt * H * HD + hd * HD;
-    const bf16_t* dp = dout + (size_t)bt * H * HD + hd * HD;
+    const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;   // 16-byte vector index over B*T*H*HD/8
+    const size_t nvec = (size_t)B * T * H * (HD / 8);
     float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < HD / 8; ++c) {
+    if (v < nvec) {
         float a[8], g[8];
-        unpack8(((const uint4*)op)[c], a);
-        unpack8(((const uint4*)dp)[c], g);
+        unpack8(((const uint4*)o)[v], a);
+        unpack8(((const uint4*)dout)[v], g);
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
     }
-    delta[((size_t)b * H + hd) * T + t] = acc;
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
+    if (v < nvec && (threadIdx.x & 7) == 0) {
+        const size_t row = v >> 3;                               // (b * T + t) * H + h
+        const int hd = (int)(row % H);
+        const size_t bt = row / H;
+        const int b = (int)(bt / T), t = (int)(bt - (size_t)b * T);
+        delta[((size_t)b * H + hd) * T + t] = acc;
+    }
 }
 
 // ---------------------------------------------------------------------------- dK, dV (key-owned)
@@ -560,7 +568,7 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                          float* delta, int B, int T, int H, int D, float scale, int causal, hipStream_t s) {
     (void)unused;
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
-    attn_delta_kernel<<<(B * T * H + 255) / 256, 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
+    attn_delta_kernel<<<(unsigned)(((size_t)B * T * H * (HD / 8) + 255) / 256), 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
     const int grid = B * H * (T / 128);
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;

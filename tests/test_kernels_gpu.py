@@ -83,7 +83,7 @@ def test_linear_t():
     assert _rel(W.grad, Wr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("T,H", [(128, 2), (256, 4)])
+@pytest.mark.parametrize("T,H", [(128, 2), (256, 4), (384, 3)])
 def test_flash_attention(T, H):
     from trustworthy_dl.ops import causal_attention
     B, D = 2, 64
