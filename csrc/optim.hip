@@ -21,26 +21,45 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
     const float inv_sqrt_bc2 = rsqrtf(bc2);
     const int64_t n4 = n / 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-        float4 g = ((float4*)grad)[i];
-        if (!skip) {
-            float4 p = ((float4*)master)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
-            float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w};
-            float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
+    // two float4 groups per lane per trip, all eight 16-B loads issued before any math (the single-
+    // group loop kept one load set in flight per lane: ~4.6 TB/s over the 34 B / parameter stream)
+    auto update = [&](float4 g, float4 p, float4 mm, float4 vv, int64_t i) {
+        float pa[4] = {p.x, p.y, p.z, p.w}, ga[4] = {g.x, g.y, g.z, g.w};
+        float ma[4] = {mm.x, mm.y, mm.z, mm.w}, va[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float gg = ga[k] * gscale;
-                ma[k] = b1 * ma[k] + (1.f - b1) * gg;
-                va[k] = b2 * va[k] + (1.f - b2) * gg * gg;
-                pa[k] = pa[k] * (1.f - lr * wd);
-                pa[k] -= step_size * ma[k] / (sqrtf(va[k]) * inv_sqrt_bc2 + eps);
-            }
-            ((float4*)master)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
-            ((float4*)m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
-            ((float4*)v)[i] = make_float4(va[0], va[1], va[2], va[3]);
-            if (out) ((uint2*)out)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+        for (int k = 0; k < 4; ++k) {
+            const float gg = ga[k] * gscale;
+            ma[k] = b1 * ma[k] + (1.f - b1) * gg;
+            va[k] = b2 * va[k] + (1.f - b2) * gg * gg;
+            pa[k] = pa[k] * (1.f - lr * wd);
+            pa[k] -= step_size * ma[k] / (sqrtf(va[k]) * inv_sqrt_bc2 + eps);
         }
-        if (zero_grad) ((float4*)grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        ((float4*)master)[i] = make_float4(pa[0], pa[1], pa[2], pa[3]);
+        ((float4*)m)[i] = make_float4(ma[0], ma[1], ma[2], ma[3]);
+        ((float4*)v)[i] = make_float4(va[0], va[1], va[2], va[3]);
+        if (out) ((uint2*)out)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));
+    };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+        const int64_t j = i + stride;
+        const float4 g0 = ((const float4*)grad)[i], g1 = ((const float4*)grad)[j];
+        if (!skip) {
+            const float4 p0 = ((const float4*)master)[i], p1 = ((const float4*)master)[j];
+            const float4 m0 = ((const float4*)m)[i], m1 = ((const float4*)m)[j];
+            const float4 v0 = ((const float4*)v)[i], v1 = ((const float4*)v)[j];
+            update(g0, p0, m0, v0, i);
+            update(g1, p1, m1, v1, j);
+        }
+        if (zero_grad) {
+            ((float4*)grad)[i] = z4;
+            ((float4*)grad)[j] = z4;
+        }
+    }
+    for (; i < n4; i += stride) {
+        const float4 g = ((const float4*)grad)[i];
+        if (!skip) update(g, ((const float4*)master)[i], ((const float4*)m)[i], ((const float4*)v)[i], i);
+        if (zero_grad) ((float4*)grad)[i] = z4;
     }
     // tail (n % 4)
     for (int64_t i = n4 * 4 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
