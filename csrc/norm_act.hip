@@ -354,7 +354,67 @@ __global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict
     else atomicAdd(acc + col, v[0]);
 }
 
+// Vectorised column sum of G partial rows: lane = 4 columns (16-B loads), a wave = 256 columns, the
+// four waves of a block take consecutive row strips of `rw` rows each and merge through LDS, so each
+// column gets ONE atomic per 4*rw rows.  The scalar kernels above load 4 B per lane and issue one
+// atomic per 16 rows (rocprof: 17 us for the 16.7 MB of a 32k-row LayerNorm backward, ~1 TB/s).
+struct AccPtrs4 { float* p[4]; };
+__global__ __launch_bounds__(256) void colsum_f32_vec_kernel(const float* __restrict__ part, int G, int N, int ld,
+                                                             int rw, AccPtrs4 accs) {
+    __shared__ float4 red[3][64];
+    float* acc = accs.p[blockIdx.z];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int col = (blockIdx.x * 64 + lane) * 4;
+    const bool live = acc != nullptr && col < N;
+    const float* src = part + (size_t)blockIdx.z * N;
+    const int r0 = (blockIdx.y * 4 + wid) * rw;
+    const int r1 = min(r0 + rw, G);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (live) {
+        int r = r0;
+        for (; r + 8 <= r1; r += 8) {
+            float4 q[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) q[i] = *(const float4*)(src + (size_t)(r + i) * ld + col);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { a.x += q[i].x; a.y += q[i].y; a.z += q[i].z; a.w += q[i].w; }
+        }
+        for (; r < r1; ++r) {
+            const float4 q = *(const float4*)(src + (size_t)r * ld + col);
+            a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+        }
+    }
+    if (wid) red[wid - 1][lane] = a;
+    __syncthreads();
+    if (wid == 0 && live) {
+#pragma unroll
+        for (int w = 0; w < 3; ++w) {
+            const float4 q = red[w][lane];
+            a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+        }
+        if (gridDim.y == 1) {
+            acc[col] += a.x; acc[col + 1] += a.y; acc[col + 2] += a.z; acc[col + 3] += a.w;
+        } else {
+            atomicAdd(acc + col, a.x); atomicAdd(acc + col + 1, a.y);
+            atomicAdd(acc + col + 2, a.z); atomicAdd(acc + col + 3, a.w);
+        }
+    }
+}
+
+// rows per wave: the largest of 64/32/16/8 that still gives >= 512 blocks (a few per CU)
+static inline void launch_colsum_vec(const float* part, int G, int N, int ld, AccPtrs4 a, int sets, hipStream_t s) {
+    const int gx = (N / 4 + 63) / 64;
+    int rw = 64;
+    while (rw > 8 && (long)gx * ((G + 4 * rw - 1) / (4 * rw)) * sets < 512) rw >>= 1;
+    const dim3 grd(gx, (G + 4 * rw - 1) / (4 * rw), sets);
+    colsum_f32_vec_kernel<<<grd, 256, 0, s>>>(part, G, N, ld, rw, a);
+}
+
 static inline void launch_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s) {
+    if (N % 4 == 0 && ld % 4 == 0) {
+        launch_colsum_vec(part, G, N, ld, AccPtrs4{{acc, nullptr, nullptr, nullptr}}, 1, s);
+        return;
+    }
     const dim3 grd((N + 255) / 256, (G + CS_ROWS - 1) / CS_ROWS);
     colsum_f32_kernel<<<grd, 256, 0, s>>>(part, G, N, ld, acc);
 }
@@ -445,9 +505,14 @@ TDL_API int tdl_layernorm_bwd_res(const void* dy, const void* x, const void* w, 
     else launch_ln_bwd<true, true>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
     if (tiled) {
         const int ns = sums ? 4 : 2;
-        AccPtrs a{{dw_acc, db_acc, sums ? sres_acc : nullptr, sums ? sdx_acc : nullptr}};
-        const dim3 grd((N + 255) / 256, (G + CS_ROWS - 1) / CS_ROWS, ns);
-        colsum_f32_multi_kernel<<<grd, 256, 0, s>>>(part, G, N, ns * N, a);
+        if (N % 4 == 0) {
+            launch_colsum_vec(part, G, N, ns * N,
+                              AccPtrs4{{dw_acc, db_acc, sums ? sres_acc : nullptr, sums ? sdx_acc : nullptr}}, ns, s);
+        } else {
+            AccPtrs a{{dw_acc, db_acc, sums ? sres_acc : nullptr, sums ? sdx_acc : nullptr}};
+            const dim3 grd((N + 255) / 256, (G + CS_ROWS - 1) / CS_ROWS, ns);
+            colsum_f32_multi_kernel<<<grd, 256, 0, s>>>(part, G, N, ns * N, a);
+        }
     } else {
         ln_bwd_generic<<<M, 256, 0, s>>>(DY, X, W, mean, rstd, DR, DX, dw_acc, db_acc, sres_acc, sdx_acc, M, N);
     }
