@@ -6,6 +6,7 @@
 // float atomic per column per workgroup (row-summed on chip first), so the per-micro-batch
 // bf16 weight-grad tensor and its separate accumulate kernel never exist.
 #include "common.h"
+#include <cstdlib>
 
 template <int VEC, int CH>
 __device__ __forceinline__ void ln_vload(const bf16_t* p, float* v) {
@@ -471,10 +472,9 @@ __global__ __launch_bounds__(256) void ln_bwd_generic(const bf16_t* __restrict__
     }
 }
 
-template <bool RES, bool SUMS>
+template <int RPW, bool RES, bool SUMS>
 static void launch_ln_bwd(const bf16_t* DY, const bf16_t* X, const bf16_t* W, const float* mean, const float* rstd,
                           const bf16_t* DR, bf16_t* DX, float* part, int M, int G, int N, bool& tiled, hipStream_t s) {
-    constexpr int RPW = 2;
     const dim3 blk(256), grd(G);
     tiled = true;
     switch (N) {
@@ -498,11 +498,24 @@ TDL_API int tdl_layernorm_bwd_res(const void* dy, const void* x, const void* w, 
     auto DR = (const bf16_t*)dres;
     const bool sums = sres_acc != nullptr || sdx_acc != nullptr;
     if (sums && !dres) return (int)hipErrorInvalidValue;
-    const int G = (M + 7) / 8;
+    // Rows per wave.  With the four partial sets (SUMS) the column partials at 8 rows / block are as large
+    // as dx; 32 rows / block (rpw 8) writes a quarter of them and the column-sum pass shrinks to match,
+    // at an unchanged kernel time.  With two sets the longer row loop costs more than it saves
+    // (rocprof A/B, profiles/r1_ln_bwd_rpw_ab.json), so those keep 8 rows / block.  TDL_LN_RPW=2|8
+    // forces one choice.
+    static const int forced = [] { const char* e = getenv("TDL_LN_RPW"); return e ? atoi(e) : 0; }();
+    const int rpw = forced == 2 || forced == 8 ? forced : (sums ? 8 : 2);
+    const int G = (M + 4 * rpw - 1) / (4 * rpw);
     bool tiled;
-    if (!dres) launch_ln_bwd<false, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
-    else if (!sums) launch_ln_bwd<true, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
-    else launch_ln_bwd<true, true>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+    if (rpw == 8) {
+        if (!dres) launch_ln_bwd<8, false, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+        else if (!sums) launch_ln_bwd<8, true, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+        else launch_ln_bwd<8, true, true>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+    } else {
+        if (!dres) launch_ln_bwd<2, false, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+        else if (!sums) launch_ln_bwd<2, true, false>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+        else launch_ln_bwd<2, true, true>(DY, X, W, mean, rstd, DR, DX, part, M, G, N, tiled, s);
+    }
     if (tiled) {
         const int ns = sums ? 4 : 2;
         if (N % 4 == 0) {
