@@ -43,3 +43,19 @@ def test_too_late_reports_what_hip_started_with(clean):
     assert hq.ensure_hw_queues() == 4
     assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
     assert hq.effective_hw_queues() < hq.ENGINE_QUEUES
+
+
+def test_engine_p2p_mode_follows_queue_budget(clean):
+    """Pre-posted receives only when RCCL streams got queues of their own (parallel/pipeline.py)."""
+    import types
+    from trustworthy_dl.parallel import pipeline as P
+    clean.setattr(P.dist, "get_backend", lambda *a, **k: "nccl")
+    fake = types.SimpleNamespace(distributed=True)
+    cfg = P.EngineConfig(num_nodes=2)
+    clean.setattr(hq, "_effective", 4)
+    assert P.PipelineEngine._choose_p2p_mode(fake, cfg) == "grouped"
+    clean.setattr(hq, "_effective", 32)
+    assert P.PipelineEngine._choose_p2p_mode(fake, cfg) == "async"
+    fake.distributed = False                      # local mode: no RCCL, nothing to decide
+    clean.setattr(hq, "_effective", 4)
+    assert P.PipelineEngine._choose_p2p_mode(fake, cfg) == "async"
