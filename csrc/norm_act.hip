@@ -736,6 +736,30 @@ __global__ __launch_bounds__(256) void embed_bwd_wte_kernel(const int64_t* __res
         for (int k = 0; k < 4; ++k) atomicAdd(wte_grad + id * H + col + k, g[k]);
     }
 }
+// Same scatter with coalesced atomics (H % 256 == 0): the lane that loaded 4 columns is not the lane
+// that adds them; after four shuffles, atomic instruction k of a wave covers the 64 consecutive fp32
+// columns c0 + 64k .. +63 (256 B, two cache lines) instead of one column in every 16 B of a 1 KB span
+// (eight lines), so L2 sees a quarter of the atomic transactions.
+__global__ __launch_bounds__(256) void embed_bwd_wte_coalesced_kernel(const int64_t* __restrict__ ids,
+                                                                      const bf16_t* __restrict__ dout,
+                                                                      float* __restrict__ wte_grad, int BT, int H) {
+    const int tok = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tok >= BT) return;  // uniform per wave: the shuffles below see all 64 lanes
+    const int lane = threadIdx.x & 63;
+    float* dst = wte_grad + ids[tok] * (int64_t)H;
+    const int e = lane & 3;
+    for (int c0 = 0; c0 < H; c0 += 256) {
+        float g[4];
+        unpack4(*(const uint2*)(dout + (size_t)tok * H + c0 + lane * 4), g);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int src = k * 16 + (lane >> 2);  // holder of column c0 + 64k + lane
+            const float v0 = __shfl(g[0], src, 64), v1 = __shfl(g[1], src, 64);
+            const float v2 = __shfl(g[2], src, 64), v3 = __shfl(g[3], src, 64);
+            atomicAdd(dst + c0 + k * 64 + lane, e == 0 ? v0 : e == 1 ? v1 : e == 2 ? v2 : v3);
+        }
+    }
+}
 // wpe_grad[t,:] += sum_b dout[b,t,:]  (single writer per element, no atomics)
 __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const bf16_t* __restrict__ dout, float* __restrict__ wpe_grad,
                                                             int B, int T, int H) {
@@ -749,7 +773,9 @@ __global__ __launch_bounds__(256) void embed_bwd_wpe_kernel(const bf16_t* __rest
 TDL_API int tdl_embedding_bwd(const int64_t* ids, const void* dout, float* wte_grad, float* wpe_grad, int B, int T, int H,
                               int unused, hipStream_t s) {
     (void)unused;
-    if (wte_grad)
+    if (wte_grad && H % 256 == 0)
+        embed_bwd_wte_coalesced_kernel<<<(B * T + 3) / 4, 256, 0, s>>>(ids, (const bf16_t*)dout, wte_grad, B * T, H);
+    else if (wte_grad)
         embed_bwd_wte_kernel<<<(B * T + 3) / 4, 256, 0, s>>>(ids, (const bf16_t*)dout, wte_grad, B * T, H);
     if (wpe_grad)
         embed_bwd_wpe_kernel<<<(int)(((size_t)T * H + 255) / 256), 256, 0, s>>>((const bf16_t*)dout, wpe_grad, B, T, H);
