@@ -387,17 +387,26 @@ __global__ __launch_bounds__(256) void colsum_f32_vec_kernel(const float* __rest
     }
     if (wid) red[wid - 1][lane] = a;
     __syncthreads();
-    if (wid == 0 && live) {
+    if (wid == 0 && acc != nullptr) {  // whole wave (uniform): the shuffles below need every lane
 #pragma unroll
         for (int w = 0; w < 3; ++w) {
             const float4 q = red[w][lane];
             a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
         }
         if (gridDim.y == 1) {
-            acc[col] += a.x; acc[col + 1] += a.y; acc[col + 2] += a.z; acc[col + 3] += a.w;
+            if (live) { acc[col] += a.x; acc[col + 1] += a.y; acc[col + 2] += a.z; acc[col + 3] += a.w; }
         } else {
-            atomicAdd(acc + col, a.x); atomicAdd(acc + col + 1, a.y);
-            atomicAdd(acc + col + 2, a.z); atomicAdd(acc + col + 3, a.w);
+            // coalesced atomics: instruction k covers the 64 consecutive columns base + 64k + lane
+            // (held by lane 16k + lane/4, component lane%4), as in embed_bwd_wte_coalesced_kernel
+            const int base = blockIdx.x * 256, e = lane & 3;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int src = k * 16 + (lane >> 2);
+                const float v0 = __shfl(a.x, src, 64), v1 = __shfl(a.y, src, 64);
+                const float v2 = __shfl(a.z, src, 64), v3 = __shfl(a.w, src, 64);
+                const int c = base + k * 64 + lane;
+                if (c < N) atomicAdd(acc + c, e == 0 ? v0 : e == 1 ? v1 : e == 2 ? v2 : v3);
+            }
         }
     }
 }
