@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "trustworthy_dl", "_native")
 BUILD_DIR = os.path.join(ROOT, "build", "native")
+AGPR_FORM = {"gemm.hip"}
 
 
 def hipcc() -> str:
@@ -62,8 +63,11 @@ def build(arch: str = "gfx950", jobs: int = 8, debug: bool = False, verbose: boo
             # MFMA accumulators in ArchVGPRs: the default AGPR form shuttles every softmax / epilogue
             # read through v_accvgpr_read/write and pushed the attention forward past 256 registers
             # (one wave per SIMD); the VGPR form holds it at 140 (three waves per SIMD)
+            # the persistent GEMM keeps its 256 accumulators per lane in AGPRs (one wave per SIMD,
+            # 512 registers): it is built in the default AGPR form
+            form = [] if os.path.basename(src) in AGPR_FORM else ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
             jobs_list.append([cc, f"--offload-arch={arch}", "-std=c++17", "-fPIC", *opt, "-munsafe-fp-atomics",
-                              "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-I", CSRC, "-c", src, "-o", obj])
+                              *form, "-I", CSRC, "-c", src, "-o", obj])
     for src in rt_srcs:
         obj = os.path.join(BUILD_DIR, "rt_" + os.path.basename(src) + ".o")
         robjs.append(obj)

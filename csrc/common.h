@@ -112,4 +112,23 @@ __device__ __forceinline__ float u32_to_unit(uint32_t x) {  // (0, 1]
     return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
 }
 
+// ---------------------------------------------------------------- GELU (tanh approximation)
+// gelu(u) = 0.5 u (1 + tanh(a)) = u * sigmoid(2a),  a = k0 (u + k1 u^3).
+// Written as u / (1 + 2^(u (c0 + c1 u^2))) with the log2(e) factor folded into c0/c1: one v_exp, one
+// v_rcp (1 ulp, far below bf16 resolution) and a few FMAs per element.  The IEEE division of the
+// tanh form cost ~10 VALU per element and left both kernels ALU-bound (fwd 24, bwd 31 VALU / element).
+#define TDL_GELU_C0 (-2.0f * 0.7978845608028654f * 1.4426950408889634f)
+#define TDL_GELU_C1 (-2.0f * 0.7978845608028654f * 0.044715f * 1.4426950408889634f)
+__device__ __forceinline__ float gelu_sigmoid2a(float u) {  // sigmoid(2a)
+    const float e = __builtin_amdgcn_exp2f(u * fmaf(TDL_GELU_C1, u * u, TDL_GELU_C0));
+    return __builtin_amdgcn_rcpf(1.0f + e);
+}
+__device__ __forceinline__ float gelu_tanh(float u) { return u * gelu_sigmoid2a(u); }
+__device__ __forceinline__ float gelu_tanh_grad(float u) {
+    // d/du [u s(u)] = s + u s (1 - s) 2 k0 (1 + 3 k1 u^2)
+    const float s = gelu_sigmoid2a(u);
+    const float da = 2.0f * 0.7978845608028654f * fmaf(3.0f * 0.044715f, u * u, 1.0f);
+    return fmaf(u * s * (1.0f - s), da, s);
+}
+
 #define TDL_LAUNCH_CHECK() return (int)hipGetLastError()

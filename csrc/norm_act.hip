@@ -550,24 +550,6 @@ TDL_API int tdl_layernorm_bwd(const void* dy, const void* x, const void* w, cons
 TDL_API int64_t tdl_layernorm_bwd_ws_floats(int M, int N) { return (int64_t)4 * N * ((M + 7) / 8); }
 
 // ============================================================== bias + GELU(tanh)
-// gelu(u) = 0.5 u (1 + tanh(a)) = u * sigmoid(2a),  a = k0 (u + k1 u^3).
-// Written as u / (1 + 2^(u (c0 + c1 u^2))) with the log2(e) factor folded into c0/c1: one v_exp, one
-// v_rcp (1 ulp, far below bf16 resolution) and a few FMAs per element.  The IEEE division of the
-// tanh form cost ~10 VALU per element and left both kernels ALU-bound (fwd 24, bwd 31 VALU / element).
-#define TDL_GELU_C0 (-2.0f * 0.7978845608028654f * 1.4426950408889634f)
-#define TDL_GELU_C1 (-2.0f * 0.7978845608028654f * 0.044715f * 1.4426950408889634f)
-__device__ __forceinline__ float gelu_sigmoid2a(float u) {  // sigmoid(2a)
-    const float e = __builtin_amdgcn_exp2f(u * fmaf(TDL_GELU_C1, u * u, TDL_GELU_C0));
-    return __builtin_amdgcn_rcpf(1.0f + e);
-}
-__device__ __forceinline__ float gelu_tanh(float u) { return u * gelu_sigmoid2a(u); }
-__device__ __forceinline__ float gelu_tanh_grad(float u) {
-    // d/du [u s(u)] = s + u s (1 - s) 2 k0 (1 + 3 k1 u^2)
-    const float s = gelu_sigmoid2a(u);
-    const float da = 2.0f * 0.7978845608028654f * fmaf(3.0f * 0.044715f, u * u, 1.0f);
-    return fmaf(u * s * (1.0f - s), da, s);
-}
-
 // y = gelu(x + b); x,y [M,N] bf16 (may alias), N % 8 == 0.  Block tile: R rows x 2048 columns
 // (256 threads x 8); every row's 16-B load is issued before any math, so each lane keeps R loads
 // in flight (a grid-stride loop with one load per iteration left this kernel latency-bound at

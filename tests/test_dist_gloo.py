@@ -42,7 +42,8 @@ def _build(model_name, nodes, micro, p2p_mode="async", granularity="auto"):
         kw["vocab_size"] = 1024
     m = get_model(model_name, seed=7, **kw)
     cfg = EngineConfig(num_nodes=nodes, micro_batches=micro, device="cpu", seq_len=32, p2p_mode=p2p_mode,
-                       layer_granularity=granularity, adamw=AdamWConfig(lr=1e-2, eps=1.0, max_grad_norm=1.0), reassign=False)
+                       layer_granularity=granularity, adamw=AdamWConfig(lr=1e-2, eps=1.0, max_grad_norm=float(os.environ.get("TDL_TEST_CLIP", "1.0"))),
+                       reassign=False)
     from trustworthy_dl.utils.metrics import MetricsCollector
     return PipelineEngine(m, cfg, metrics=MetricsCollector())
 
@@ -53,14 +54,15 @@ def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="asy
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = _build(model_name, world, micro, p2p_mode, granularity)
-    losses = []
+    clip = []
     for b in _make_batches(model_name, steps, 8):
         eng.train_step(b)
+        clip.append(float(eng.my_stage().verifier.ctrl[0]))
     eng.flush()
     st = eng.stage_state_dicts()
     res = {"rank": rank, "last_loss": eng.last_loss, "losses": [m["loss"] for m in eng.metrics.batch_metrics],
            "weights": {n: float(t.double().sum()) for sd in st.values() for n, t in sd.items()},
-           "trust": [eng.trust.get_trust_score(i) for i in range(world)]}
+           "trust": [eng.trust.get_trust_score(i) for i in range(world)], "clip": clip}
     with open(f"{out_path}.{rank}", "w") as f:
         json.dump(res, f)
     dist.barrier()
@@ -71,8 +73,10 @@ def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="asy
     ("resnet32", 2, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "grouped", "auto"),
     ("gpt2-tiny", 2, 4, "async", "auto"), ("gpt2-tiny", 8, 4, "async", "auto"),
     ("gpt2-tiny", 4, 4, "async", "half")])  # stage boundaries inside blocks, one process per stage
-def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran):
+def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran, monkeypatch):
     steps = 4
+    if model_name.startswith("gpt2"):
+        monkeypatch.setenv("TDL_TEST_CLIP", "0.05")  # clipping binds on every step
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "res")
         mp.spawn(_worker, args=(world, _free_port(), model_name, steps, micro, out, p2p, gran), nprocs=world, join=True)
@@ -98,6 +102,21 @@ def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran):
     # every rank holds the same trust vector (identical all-gathered digests)
     for r in range(1, world):
         assert res[0]["trust"] == pytest.approx(res[r]["trust"])
+    if model_name.startswith("gpt2"):
+        # ... and the pipeline depth does not change the training trajectory: the same model on ONE
+        # stage (global-norm clipping on, the tied wte counted once) gives the same losses
+        single = _build(model_name, 1, micro, granularity="block")
+        clip1 = []
+        for b in _make_batches(model_name, steps, 8):
+            single.train_step(b)
+            clip1.append(float(single.stages[0].verifier.ctrl[0]))
+        single.flush()
+        one = [m["loss"] for m in single.metrics.batch_metrics]
+        assert res[0]["losses"] == pytest.approx(one, rel=1e-4), (res[0]["losses"], one)
+        # the global clip scale (from the all-gathered per-stage sums of squares) is the one-stage scale
+        assert max(clip1) < 0.99, "clipping must bind for this check"
+        for r in range(world):
+            assert res[r]["clip"] == pytest.approx(clip1, rel=1e-4), (r, res[r]["clip"], clip1)
 
 
 def _layer_sums(eng):

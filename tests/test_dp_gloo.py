@@ -117,13 +117,24 @@ class _ScaleAttacker:
         return False
 
 
-def _attack_worker(rank, world, port, out_path):
+class _NaNAttacker:
+    """Writes NaN / Inf into node 1's gradient every step (a replica producing non-finite values)."""
+
+    def on_gradients(self, node, grad, step):
+        if node == 1:
+            grad[:64] = float("nan")
+            grad[64:128] = float("inf")
+            return True
+        return False
+
+
+def _attack_worker(rank, world, port, out_path, kind="scale"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = _engine(1, 2, dp=3)
-    eng.attacker = _ScaleAttacker()
+    eng.attacker = _ScaleAttacker() if kind == "scale" else _NaNAttacker()
     excluded = []
     for b in _batches(3, 12):
         eng.train_step(b)
@@ -137,13 +148,18 @@ def _attack_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_dp3_robust_aggregation_excludes_poisoned_replica():
+@pytest.mark.parametrize("kind", ["scale", "nan"])
+def test_dp3_robust_aggregation_excludes_poisoned_replica(kind):
+    """x50 gradients or NaN/Inf gradients on one replica: it is left out of the mean and every
+    replica (the poisoned one included) ends with the same finite weights."""
+    import math
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "res")
-        mp.spawn(_attack_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+        mp.spawn(_attack_worker, args=(3, _free_port(), out, kind), nprocs=3, join=True)
         res = [json.load(open(f"{out}.{r}")) for r in range(3)]
     for r in range(3):
         assert res[r]["excluded"] == [[0, 1, 0]] * 3
+        assert all(math.isfinite(v) for v in res[r]["weights"].values())
     for r in (1, 2):
         for n, v in res[r]["weights"].items():
             assert v == pytest.approx(res[0]["weights"][n], rel=1e-6, abs=1e-7)

@@ -296,3 +296,50 @@ def test_shadow_not_committed_for_flagged_step():
     N = eng.num_nodes
     eng._commit_shadows(step, [n == 1 for n in range(N)], [0] * N)
     assert eng._shadow_meta[1][0] == old and eng._shadow_meta[0][0] == step
+
+
+@pytest.mark.parametrize("clip", [1.0, 0.0])
+def test_pipeline_depth_invariance_with_clipping(clip):
+    """pp1 == pp2 == pp4 loss trajectories with global-norm clipping on: the tied wte / LM-head
+    gradient is counted once in the clipping norm (reference: one optimizer over the whole model,
+    distributed_trainer.py:441-446), whatever the number of stages holding a copy."""
+    losses = {}
+    for nodes in (1, 2, 4):
+        m = get_model("gpt2-tiny", seq_len=32, seed=0, vocab_size=1024)
+        cfg = EngineConfig(num_nodes=nodes, micro_batches=2, seq_len=32, device="cpu", layer_granularity="block",
+                           adamw=AdamWConfig(lr=1e-3, max_grad_norm=clip), reassign=False)
+        eng = PipelineEngine(m, cfg, metrics=MetricsCollector())
+        for b in _batches(8):
+            eng.train_step(b)
+        eng.flush()
+        losses[nodes] = [r["loss"] for r in eng.metrics.batch_metrics]
+        assert len(losses[nodes]) == 8
+    for n in (2, 4):
+        for a, b in zip(losses[n], losses[1]):
+            assert abs(a - b) <= 2e-5 * abs(b), (n, losses[n], losses[1])
+
+
+def test_quarantined_stage_does_not_shrink_clip_scale():
+    """A x10 gradient attack on one stage is quarantined; the honest stages' clip scale must be the
+    one computed from their own gradients only."""
+    atk = AdversarialAttacker(AttackConfig(["gradient_poisoning"], target_nodes=[1], intensity=1.0, start_step=15))
+    atk.activate_attacks()
+    m = get_model("gpt2-tiny", seq_len=32, seed=0, vocab_size=1024)
+    cfg = EngineConfig(num_nodes=3, micro_batches=2, seq_len=32, device="cpu", layer_granularity="block",
+                       adamw=AdamWConfig(lr=1e-3, max_grad_norm=1.0), reassign=False)
+    eng = PipelineEngine(m, cfg, TrustManager(3), attacker=atk, metrics=MetricsCollector(), detector=AttackDetector())
+    from trustworthy_dl.security import stage_verifier as SV
+    scales = []
+    for i, b in enumerate(_batches(20)):
+        eng.train_step(b)
+        st0, st1 = eng.stages[0], eng.stages[1]
+        if eng.global_step >= 15 and float(st1.verifier.ctrl[1]) > 0:
+            # honest stages: clip scale from (stage 0 + stage 2) sumsq only
+            d0 = float(st0.verifier.digest[SV.D_GRAD_SUMSQ])
+            d2 = float(eng.stages[2].verifier.digest[SV.D_GRAD_SUMSQ])
+            want = min(1.0, 1.0 / ((d0 + d2) ** 0.5 + 1e-6))
+            scales.append((float(st0.verifier.ctrl[0]), want))
+    eng.flush()
+    assert scales, "the attacked stage was never quarantined"
+    for got, want in scales:
+        assert abs(got - want) <= 1e-4 * max(1.0, want)

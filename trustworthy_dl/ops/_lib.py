@@ -106,6 +106,8 @@ _SIGNATURES = {
     # attention.hip
     "tdl_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
     "tdl_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
+    # gemm.hip
+    "tdl_gemm": [_P] * 6 + [_I] * 10 + [_L, _P],
     # conv.hip / bn.hip
     "tdl_conv_nt": [_P] * 5 + [_I] * 12 + [_P],
     "tdl_conv_stats_ws_floats": [_I, _I],

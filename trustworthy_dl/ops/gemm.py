@@ -1,0 +1,140 @@
+"""Native bf16 MFMA GEMM (csrc/gemm.hip) with fused epilogues.
+
+``matmul(a, b)`` computes ``a @ b`` for a logical ``a [M, K]`` and ``b [K, N]`` whose storage may be
+either row-major or a transposed view of a row-major tensor (the kernel reads both forms: k-contiguous
+operands with ``ds_read_b128``, row-contiguous ones with the gfx950 transposing LDS read).  So every
+product of a linear layer runs on the parameters as they are stored, with no transposed copies:
+
+    forward   y  = x @ W             a = x,     b = W            (W [in, out], HF Conv1D)
+    dgrad     dx = dy @ W.t()        a = dy,    b = W.t()
+    wgrad     dW += x.t() @ dy       a = x.t(), b = dy           (fp32, into main_grad)
+
+Epilogues (fused into the GEMM's store): ``bias``; ``gelu`` (stores the pre-activation too);
+``resadd`` (out += a @ b, the residual stream); ``dgelu`` (out = (a @ b) * gelu'(pre), bias
+gradient accumulated as fp32 column sums); fp32 ``acc`` / ``store`` / split-K ``atomic``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import ptr, stream_ptr
+
+EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f32atomic": 6}
+BK = 64
+# A/B switch for benchmarks: 0 = shipped schedule, 1 = plain (unpipelined) schedule, >= 2 = the
+# pipeline variants of tdl_gemm (NT, bf16 out only; some are timing-only ablations)
+VARIANT = 0
+
+
+def _operand_a(a: torch.Tensor):
+    """(transposed_storage, ld) for a logical [M, K] operand."""
+    if a.stride(1) == 1 and a.stride(0) >= a.shape[1]:
+        return 0, a.stride(0)
+    if a.stride(0) == 1 and a.stride(1) >= a.shape[0]:
+        return 1, a.stride(1)
+    raise ValueError(f"operand A needs a row-major or transposed-row-major layout (strides {a.stride()})")
+
+
+def _operand_b(b: torch.Tensor):
+    """(transposed_storage, ld) for a logical [K, N] operand: tb = 1 when stored [K][N]."""
+    if b.stride(1) == 1 and b.stride(0) >= b.shape[1]:
+        return 1, b.stride(0)
+    if b.stride(0) == 1 and b.stride(1) >= b.shape[0]:
+        return 0, b.stride(1)
+    raise ValueError(f"operand B needs a row-major or transposed-row-major layout (strides {b.stride()})")
+
+
+def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Shapes/layouts the native kernel takes (everything else stays on the caller's path)."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2 and b.dim() == 2):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    if K % BK or N % 8 or M % 8 or b.shape[0] != K:
+        return False
+    try:
+        ta, lda = _operand_a(a)
+        tb, ldb = _operand_b(b)
+    except ValueError:
+        return False
+    return lda % 8 == 0 and ldb % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+
+
+def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_stride=0):
+    M, K = a.shape
+    N = b.shape[1]
+    ta, lda = _operand_a(a)
+    tb, ldb = _operand_b(b)
+    _lib.call("tdl_gemm", ptr(a), ptr(b), ptr(c), ptr(bias), ptr(aux), ptr(colsum), M, N, K, lda, ldb, ldc,
+              ta, tb, EPI[epi] | (VARIANT << 8), int(split), int(split_stride), stream_ptr(a.device))
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           epi: str = "none", aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 ``epi(a @ b)``.  ``epi='gelu'`` needs ``aux`` (receives the pre-activation, shape of the
+    output); ``'resadd'`` adds into ``out``; ``'dgelu'`` reads the pre-activation from ``aux`` and
+    accumulates the column sums of the result into ``colsum`` (fp32) when given."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        if epi == "resadd":
+            raise ValueError("resadd needs out")
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    if out.stride(1) != 1:
+        raise ValueError("out must be row-major")
+    if epi in ("gelu", "dgelu") and (aux is None or aux.stride() != out.stride()):
+        raise ValueError(f"{epi} needs aux with the output's layout")
+    _launch(a, b, out, out.stride(0), epi, bias=bias, aux=aux, colsum=colsum)
+    return out
+
+
+def wgrad_split(M: int, K: int, N: int, num_cu: int = 256) -> int:
+    """Split of the token reduction for an fp32 weight-gradient product [K, M] @ [M, N]: enough
+    256x256 tiles x splits to fill the CUs once, each split at least 16 K steps deep."""
+    if os.environ.get("TDL_WGRAD_SPLITK", "1") == "0":
+        return 1
+    tiles = ((K + 255) // 256) * ((N + 255) // 256)
+    s = max(1, num_cu // tiles)
+    s = min(s, max(1, M // (16 * BK)))
+    return s
+
+
+def matmul_f32_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, split: Optional[int] = None,
+                   mode: Optional[str] = None) -> torch.Tensor:
+    """``acc (fp32) += a @ b``.  With a split reduction the partial products go to fp32 slabs
+    reduced by one native pass (``mode='slab'``) or straight into ``acc`` with fp32 atomics
+    (``mode='atomic'``)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if acc.dtype != torch.float32 or tuple(acc.shape) != (M, N) or not acc.is_contiguous():
+        raise ValueError("acc must be a contiguous fp32 [M, N] buffer")
+    S = wgrad_split(K, M, N) if split is None else max(1, int(split))
+    if S <= 1:
+        _launch(a, b, acc, N, "f32acc")
+        return acc
+    mode = mode or os.environ.get("TDL_WGRAD_REDUCE", "slab")
+    S = effective_split(K, S)
+    if S <= 1:
+        _launch(a, b, acc, N, "f32acc")
+        return acc
+    if mode == "atomic":
+        _launch(a, b, acc, N, "f32atomic", split=S)
+        return acc
+    slabs = torch.empty(S, M, N, dtype=torch.float32, device=acc.device)
+    _launch(a, b, slabs, N, "f32", split=S, split_stride=M * N)
+    _lib.call("tdl_splitk_reduce_add", ptr(acc), ptr(slabs), S, acc.numel(), stream_ptr(acc.device))
+    return acc
+
+
+def effective_split(K: int, split: int) -> int:
+    """The split the kernel runs: the largest value <= ``split`` dividing the K / 64 steps (every
+    slice the same depth; mirrors tdl_gemm)."""
+    steps = K // BK
+    s = max(1, min(int(split), steps))
+    while s > 1 and steps % s:
+        s -= 1
+    return s

@@ -10,7 +10,8 @@ Every stage re-homes its parameters into contiguous buffers:
 so that (a) the fused AdamW is one bandwidth-bound launch per weight-decay group
 (csrc/optim.hip), (b) gradient verification is one segmented reduction over ``grad``
 (csrc/stats.hip K3), and (c) re-sharding a stage to another GPU is a handful of large
-contiguous P2P transfers over xGMI (parallel/reshard.py) instead of hundreds of small ones.
+contiguous P2P transfers over xGMI (``PipelineEngine._migrate`` in parallel/pipeline.py) instead
+of hundreds of small ones.
 Parameters are ordered [weight-decay group | no-decay group] (biases, LayerNorm, embeddings
 of positions are not decayed).
 """

@@ -235,7 +235,22 @@ class PipelineEngine:
             st = Stage(self.model, rng, sid, self.plan.num_stages, self._stage_device(node), self.dtype,
                        self._verifier_kwargs(), layers=layers)
             self.stages[node] = st
+        self._set_clip_exclusions()
         self._build_comm()
+
+    def _set_clip_exclusions(self):
+        """Count every tied weight once in the global clipping norm: the stage owning the first
+        member of a tie group (the embedding) counts it, other stages' copies are excluded."""
+        for node, st in self.stages.items():
+            ex = set()
+            for grp in self.ties:
+                if self.plan.owner_of_layer(grp[0][0]) == node:
+                    continue
+                for li, attr in grp:
+                    prm = st.local_param(li, attr)
+                    if prm is not None:
+                        ex.add(id(prm))
+            st.set_clip_exclusions(ex)
 
     def _build_comm(self):
         self.comm = None
@@ -740,8 +755,13 @@ class PipelineEngine:
         if self.dp > 1:
             total_sumsq = self._dp_aggregate(D, evidence)
         else:
-            # global gradient norm for clipping (sum of per-stage sumsq), trust update on identical data
-            total_sumsq = D[:, SV.D_GRAD_SUMSQ].sum()
+            # global gradient norm for clipping: sum of the per-stage sumsq of the updates that will
+            # be applied (each tied weight counted once, quarantined stages left out); every rank
+            # computes it from the same all-gathered digest
+            sq = D[:, SV.D_GRAD_SUMSQ]
+            if self.quarantine_on_evidence:
+                sq = sq * (1.0 - evidence)
+            total_sumsq = sq.sum()
         present_nodes = self.all_ranks()
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
         raw = blame.to(torch.int32)
@@ -896,9 +916,11 @@ class PipelineEngine:
         w = ok[me] / torch.clamp(n_ok, min=1.0)
         if st is not None:
             st.flat.grad.mul_(w)
+            # an excluded replica contributes exactly zero: NaN/Inf * 0 is NaN, so clear it outright
+            st.flat.grad.masked_fill_(w <= 0, 0.0)
             dist.all_reduce(st.flat.grad, group=self.dp_group)
             st.verifier.ctrl[1:2].copy_((n_ok < 0.5).float().reshape(1))
-            sq = (st.flat.grad * st.flat.grad).sum().reshape(1)
+            sq = st.clip_sumsq(st.flat.grad).reshape(1)
         else:
             sq = torch.zeros(1, device=self.device)
         self._dp_excluded = bad

@@ -56,6 +56,25 @@ class Stage:
         vk = dict(verifier_kwargs or {})
         self.verifier = StageVerifier(self.flat.sizes, self.device, **vk)
 
+    def set_clip_exclusions(self, excluded_ids) -> None:
+        """Parameters whose gradient another stage already counts in the global clipping norm (the
+        non-owner copies of a tied weight, e.g. the LM head's ``wte`` on the last stage: after the
+        tied all-reduce both copies hold the same summed gradient).  A single optimizer over the
+        whole model (reference distributed_trainer.py:441-446) sees that gradient once."""
+        ex = set(excluded_ids)
+        self.clip_excluded = [(o, n) for q, o, n in zip(self.flat.params, self.flat.offsets, self.flat.sizes)
+                              if id(q) in ex]
+        self.verifier.set_clip_weights([0.0 if id(q) in ex else 1.0 for q in self.flat.params])
+
+    def clip_sumsq(self, grad: torch.Tensor) -> torch.Tensor:
+        """Sum of squares of ``grad`` (this stage's flat gradient) over the parameters this stage
+        counts for clipping (device scalar)."""
+        sq = (grad * grad).sum()
+        for o, n in getattr(self, "clip_excluded", []):
+            g = grad[o:o + n]
+            sq = sq - (g * g).sum()
+        return sq
+
     @staticmethod
     def _fold_grad(p: torch.Tensor):
         """Modules not routed through the fused ops (convs, BN, nn.Linear) produce ``.grad``;

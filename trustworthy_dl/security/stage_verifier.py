@@ -63,6 +63,7 @@ class StageVerifier:
         self.out_stats = z(13)
         self.out_mu, self.out_sd, self.out_n = z(1), z(1), z(1)
         self.norm_ema = z(max(self.S, 1))
+        self.clip_w = torch.ones(max(self.S, 1), dtype=torch.float32, device=self.device)
         self.norm_n = z(1)
         self.ctrl = z(2)
         self.ctrl[0] = 1.0
@@ -129,7 +130,7 @@ class StageVerifier:
             g = self.grad_stats.compute(flat_grad)
             Sn = self.S
             norms = g[18:18 + Sn]
-            d[D_GRAD_SUMSQ] = (norms * norms).sum()
+            sumsq = (norms * norms * self.clip_w[:Sn]).sum()
             d[D_GRAD_L2] = g[10]
             d[D_GRAD_COS] = g[16]
             d[D_NONFINITE] += g[17]
@@ -168,8 +169,18 @@ class StageVerifier:
             self.ctrl[1:2].copy_(torch.maximum(gflag, (d[D_NONFINITE:D_NONFINITE + 1] > 0).float()))
         else:
             self.ctrl[1] = 0.0
+        # clipping norm contribution: the gradient this stage will actually apply (a quarantined
+        # update is skipped, so it must not shrink the honest stages' updates through the clip scale)
+        if self.grad_stats is not None and flat_grad is not None:
+            d[D_GRAD_SUMSQ] = sumsq * (1.0 - self.ctrl[1])
         self._have_out = False
         return d
+
+    def set_clip_weights(self, weights: Sequence[float]):
+        """Per-parameter weights (1 = counted, 0 = counted on another stage) for the digest's
+        clipping sum of squares."""
+        if len(weights):
+            self.clip_w[:len(weights)].copy_(torch.tensor(list(weights), dtype=torch.float32))
 
     def set_clip_scale(self, total_sumsq: torch.Tensor, max_norm: float):
         """ctrl[0] = min(1, max_norm / ||g||_global) from the all-gathered per-stage sumsq (device)."""
