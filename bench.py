@@ -18,14 +18,22 @@ verification passes are spread over twice the tokens of the README's 32 (measure
 337k tok/s at 32 sequences, 349k at 64; ``--batch-per-gpu 32`` reproduces the former).  Timing: W untimed steps,
 then barrier + device sync, K timed optimizer steps, barrier + device sync; the MAX elapsed over
 ranks is reported.  ``value`` = whole-job tokens/s.
+
+Failure reporting (multi-rank): every rank publishes where it is (runtime/progress.py) to the
+c10d store; when a rank raises, or any rank stops advancing for ``--watchdog`` seconds, rank 0
+prints ONE failure JSON line (``value`` null, ``error``, ``failed_phase`` per rank) and the job
+exits non-zero.  ``--debug-fault hang|raise --debug-fault-rank R --debug-fault-step S`` injects
+such a failure (tests/test_bench_gloo.py).
 """
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
 import time
+import traceback
 
 import torch
 import torch.distributed as dist
@@ -83,7 +91,73 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--trace-phases", default="",
                     help="write a per-phase HIP-event breakdown (JSON, + Chrome trace next to it) to this path")
+    ap.add_argument("--p2p-mode", default="auto", choices=["auto", "async", "grouped"],
+                    help="pipeline P2P: pre-posted receives on per-direction communicators (async) or one "
+                         "batched exchange per transfer (grouped); auto = async when the HIP runtime has "
+                         "enough hardware queues")
+    ap.add_argument("--timeout", type=float, default=600.0,
+                    help="process-group timeout (s) for init and collectives")
+    ap.add_argument("--watchdog", type=float, default=300.0,
+                    help="seconds without progress on any rank before the run is reported failed (0 = off)")
+    ap.add_argument("--reassign-at", type=int, default=-1,
+                    help="after this many steps (warmup included), exclude the last pipeline rank and "
+                         "re-shard its layers over the others (exercises migration mid-run)")
+    ap.add_argument("--debug-fault", default="", choices=["", "hang", "raise"])
+    ap.add_argument("--debug-fault-rank", type=int, default=-1)
+    ap.add_argument("--debug-fault-step", type=int, default=1)
     args = ap.parse_args()
+    try:
+        run(args)
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: BLE001 - every failure becomes a legible line + non-zero exit
+        _fail(args, "error", f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
+
+
+_WATCHDOG = None
+METRIC = "tokens/sec GPT-2-medium MP=N with grad-verify on"
+
+
+def _failure_line(args, kind: str, marks, errors) -> str:
+    from trustworthy_dl.runtime import progress
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if errors:
+        msg = "; ".join(f"rank {e['rank']} raised in '{e['phase']}': {e['error'].splitlines()[0]}" for e in errors)
+    elif kind == "stall":
+        stale = sorted(marks.items(), key=lambda kv: -(kv[1].get("stalled_s") or 0))
+        r, st = stale[0]
+        msg = f"no progress for {st.get('stalled_s')}s on rank {r} in '{st.get('phase')}'"
+    else:
+        msg = kind
+    return json.dumps({
+        "metric": METRIC, "value": None, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens, random-init weights",
+        "error": msg, "failure_kind": kind,
+        "failed_phase": {str(r): m.get("phase") for r, m in marks.items()},
+        "stalled_s": {str(r): m.get("stalled_s") for r, m in marks.items()},
+        "errors": errors, "config": {"model": args.model, "p2p_mode": args.p2p_mode},
+        "phase_now": progress.current()["phase"]})
+
+
+def _fail(args, kind: str, message: str):
+    """This rank's main loop raised: rank 0 prints the failure line, other ranks hand the error
+    to rank 0 through the store (and print it to stderr); exit non-zero either way."""
+    from trustworthy_dl.runtime import progress
+    rank = int(os.environ.get("RANK", "0"))
+    print(f"[bench] rank {rank} failed in '{progress.current()['phase']}': {message}", file=sys.stderr, flush=True)
+    if _WATCHDOG is not None:
+        _WATCHDOG.report_error(message)          # rank 0: prints the line and exits here
+    elif rank == 0:
+        rec = [{"rank": 0, "phase": progress.current()["phase"], "error": message[-2000:]}]
+        print(_failure_line(args, kind, {0: progress.current()}, rec), flush=True)
+    sys.stdout.flush()
+    os._exit(1)
+
+
+def run(args):
+    global _WATCHDOG
+    from trustworthy_dl.runtime import progress
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -95,10 +169,19 @@ def main():
     use_cuda = torch.cuda.is_available()
     if use_cuda:
         torch.cuda.set_device(local_rank)
+    progress.mark("init_process_group")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend="nccl" if use_cuda else "gloo",
+                                timeout=datetime.timedelta(seconds=args.timeout),
                                 device_id=torch.device("cuda", local_rank) if use_cuda else None)
+        _WATCHDOG = progress.StallWatchdog(
+            rank, world, args.watchdog, store=dist.distributed_c10d._get_default_store(),
+            on_failure=lambda kind, marks, errs: print(_failure_line(args, kind, marks, errs), flush=True)
+            if rank == 0 else None).start()
+    hwq = effective_hw_queues()
+    print(f"[bench] rank {rank} local_rank {local_rank} GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} "
+          f"effective_hw_queues={hwq}", file=sys.stderr, flush=True)
 
     from trustworthy_dl.models import get_model
     from trustworthy_dl.parallel.flat import AdamWConfig
@@ -113,7 +196,9 @@ def main():
     M = per_replica // mbs
     model = get_model(args.model, seq_len=args.seq_len, seed=1234)
     verify = not args.no_verify
-    cfg = EngineConfig(num_nodes=N, micro_batches=M, seq_len=args.seq_len, data_parallel=dp,
+    progress.mark("build engine")
+    p2p = {"auto": "async"}.get(args.p2p_mode, args.p2p_mode)
+    cfg = EngineConfig(p2p_mode=p2p, num_nodes=N, micro_batches=M, seq_len=args.seq_len, data_parallel=dp,
                        adamw=AdamWConfig(lr=args.lr, weight_decay=0.01, max_grad_norm=1.0),
                        attack_detection=verify, gradient_verification=verify, quarantine=verify,
                        reassign=False, trace_phases=bool(args.trace_phases))
@@ -134,25 +219,47 @@ def main():
         if use_cuda:
             torch.cuda.synchronize()
 
-    for i in range(args.warmup):
+    done = [0]
+
+    def step(i):
+        if args.debug_fault and rank == args.debug_fault_rank and done[0] == args.debug_fault_step:
+            progress.mark(f"step {done[0] + 1}: injected {args.debug_fault} (--debug-fault)")
+            if args.debug_fault == "raise":
+                raise RuntimeError("injected fault (--debug-fault raise)")
+            while True:                      # a rank that stops answering (its peers block in P2P)
+                time.sleep(3600)
         engine.train_step(batches[i % 2])
+        done[0] += 1
+        if done[0] == args.reassign_at:
+            progress.mark(f"step {done[0]}: re-shard away from rank {engine.plan.ranks[-1]}")
+            engine.flush()
+            engine.reassign([engine.plan.ranks[-1]], done[0])
+
+    for i in range(args.warmup):
+        step(i)
     engine.flush()
+    progress.mark("timing barrier (start)")
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        engine.train_step(batches[i % 2])
+        step(i)
+    progress.mark("timing barrier (end)")
     sync()
     elapsed = time.perf_counter() - t0
     engine.flush()
+    progress.mark("report")
     el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}" if use_cuda else "cpu")
+    hwq_all = [hwq]
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        hwq_all = [None] * world
+        dist.all_gather_object(hwq_all, hwq)
     elapsed = float(el)
     tokens = global_batch * args.seq_len * args.steps
     tps = tokens / elapsed
     if rank == 0:
         line = {
-            "metric": "tokens/sec GPT-2-medium MP=N with grad-verify on",
+            "metric": METRIC,
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -162,7 +269,11 @@ def main():
                        "parallelism": f"pp{stages}" + (f"xdp{dp}" if dp > 1 else ""),
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
                        "plan": engine.plan.describe(), "last_loss": engine.last_loss,
-                       "p2p_mode": engine.p2p_mode, "hw_queues": effective_hw_queues()},
+                       "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
+                       "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
+                       "reassignments": [{"step": r["step"], "from_nodes": r["from_nodes"],
+                                          "migration_ms": round(1000 * r["migration_time"], 2),
+                                          "plan": r["plan"]} for r in engine.reassignment_history]},
         }
         print(json.dumps(line), flush=True)
     if args.trace_phases:
@@ -173,6 +284,8 @@ def main():
             json.dump({"rank": rank, "stage_plan": engine.plan.describe(),
                        "ms_per_step": engine.tracer.summary(skip=args.warmup)}, f, indent=1)
         engine.tracer.export_chrome_trace(f"{base}_rank{rank}.trace.json", pid=rank)
+    if _WATCHDOG is not None:
+        _WATCHDOG.finish()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

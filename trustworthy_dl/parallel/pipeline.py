@@ -42,6 +42,7 @@ from .comm import P2PComm, all_gather_rows, batched_transfer
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
 from .stage import Stage, tied_groups
+from ..runtime import progress
 
 logger = logging.getLogger(__name__)
 
@@ -351,6 +352,7 @@ class PipelineEngine:
         bump_weight_generation()   # weights may have changed since the last step (update, re-shard, restore, load)
         self.global_step += 1
         self.trust.advance_step(self.global_step)
+        progress.mark(f"step {self.global_step}: pipeline schedule")
         t0 = time.perf_counter()
         truth: Dict[int, bool] = {}
         if self.attacker is not None and hasattr(self.attacker, "apply_attacks"):
@@ -448,6 +450,7 @@ class PipelineEngine:
         def get_input(i):
             if first:
                 return self._stage_input(inputs[i], st)
+            progress.mark(f"step {self.global_step}: stage {s} grouped exchange with rank {comm.prev}")
             x, _ = comm.exchange(recv_prev=(in_shape, act_dtype))
             return x
 
@@ -563,14 +566,18 @@ class PipelineEngine:
         waited = [0.0]
         defer_w = self.cfg.defer_wgrad and not first
 
+        step = self.global_step
+
         def post_recv(shape, src, group):
             buf = torch.empty(shape, dtype=dt, device=st.device)
-            return dist.irecv(buf, src, group=group), buf
+            return dist.irecv(buf, src, group=group), buf, src
 
         def take(h):
+            progress.mark(f"step {step}: stage {s} waits for a P2P receive from rank {h[2]}")
             t0 = time.perf_counter()
             h[0].wait()
             waited[0] += time.perf_counter() - t0
+            progress.mark(f"step {step}: stage {s} compute")
             return h[1]
 
         def post_x(i):
@@ -654,6 +661,7 @@ class PipelineEngine:
             dy_h = post_dy(b + 1)                  # after the send: no send queues behind it
             with tr.phase("bwd_weight"):
                 dw.run()
+        progress.mark(f"step {step}: stage {s} drains its P2P sends")
         t0 = time.perf_counter()
         for w in sends:
             w.wait()
@@ -723,6 +731,7 @@ class PipelineEngine:
 
     def _finish_step(self, loss, truth: Dict[int, bool]):
         tv = self.tracer.begin("verify")
+        progress.mark(f"step {self.global_step}: tied-weight gradient all-reduce")
         self._allreduce_tied()
         N = self.num_nodes
         rows = []
@@ -738,6 +747,7 @@ class PipelineEngine:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
             if self.heartbeat is not None:
                 mine[SV.D_OFFLINE_MASK] = float(sum(1 << n for n in self.heartbeat.offline() if n < 24))
+            progress.mark(f"step {self.global_step}: digest all-gather")
             D = all_gather_rows(mine, self.world)
             if self.heartbeat is not None:
                 self._apply_offline(D)
@@ -782,6 +792,7 @@ class PipelineEngine:
             self.t_counts[idx] = c
             self.t_status[idx] = s_
         self.tracer.end(tv)
+        progress.mark(f"step {self.global_step}: optimizer")
         to = self.tracer.begin("optimizer")
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
