@@ -926,10 +926,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
 // Requirements: K % 64 == 0, N % 4 == 0; TA needs M % 8 == 0, TB N % 8 == 0; 16-byte aligned rows
 // (lda/ldb % 8 == 0), ldc % 4 == 0.  split > 1 only with EPI 4 (slab i at C + i * split_stride) or
 // 6 (atomics); the split is reduced until it divides K / 64 (every slice the same depth).
-// epi bits 8..15 select a benchmark variant: 0 = persistent 8-wave kernel (default), 11 = the
-// persistent 4-wave (one wave per SIMD) kernel, 1 = the non-persistent 8-wave kernel with its plain
-// schedule, 10 = that kernel's pipelined schedule, 2..9 = its NT bf16 schedule variants (some
-// timing-only ablations).
+// epi bits 8..15 select a benchmark variant: 0 (and 10) = the 8-wave kernel with its pipelined
+// schedule (default: the fastest of these on MI355X, profiles/r2_gemm_variants.jsonl), 1 = its plain
+// schedule, 2..9 = its NT bf16 schedule variants, 11 = the persistent 4-wave kernel, 12 = the
+// persistent 8-wave kernel (register-staged producer), 13..18 its timing-only ablations, 19 = 12
+// without the per-XCD K rotation (11..19: NT bf16 only).
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -955,47 +956,23 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     GemmParams p{(const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (bf16_t*)aux, colsum, M, N, K,
                  lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split, 1};
     p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
-    if (variant == 12) {  // benchmark: persistent 8-wave kernel without the K-order rotation
-        variant = 0;
-        p.rotate = 0;
-    }
-    if (variant >= 13 && variant <= 19) {  // benchmark ablations of the persistent 8-wave kernel (NT bf16)
+    if (variant >= 11 && variant <= 19) {  // benchmark-only persistent kernels (NT, bf16 out)
         if (ta || tb || epi != 0) return (int)hipErrorInvalidValue;
         const int items = p.tiles * split;
         const int grid = items < num_cus() ? items : num_cus();
-        switch (variant - 12) {
-            case 1: gemm_persistent8<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;
-            case 2: gemm_persistent8<false, false, 0, 2><<<grid, NTHR, 0, s>>>(p); break;
-            case 3: gemm_persistent8<false, false, 0, 3><<<grid, NTHR, 0, s>>>(p); break;
-            case 4: gemm_persistent8<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;
-            case 5: gemm_persistent8<false, false, 0, 5><<<grid, NTHR, 0, s>>>(p); break;
-            case 6: gemm_persistent8<false, false, 0, 6><<<grid, NTHR, 0, s>>>(p); break;
-            default: gemm_persistent8<false, false, 0, 7><<<grid, NTHR, 0, s>>>(p); break;
+        if (variant == 11) {
+            gemm_persistent<false, false, 0><<<grid, PNTHR, 0, s>>>(p);
+        } else {
+            p.rotate = variant != 19;
+            switch (variant - 12) {
+                case 1: gemm_persistent8<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;  // no staging
+                case 2: gemm_persistent8<false, false, 0, 2><<<grid, NTHR, 0, s>>>(p); break;  // no LDS reads
+                case 4: gemm_persistent8<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;  // no waits
+                case 5: gemm_persistent8<false, false, 0, 5><<<grid, NTHR, 0, s>>>(p); break;
+                case 6: gemm_persistent8<false, false, 0, 7><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only
+                default: gemm_persistent8<false, false, 0, 0><<<grid, NTHR, 0, s>>>(p); break;
+            }
         }
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant == 0 || variant == 11) {
-        const int items = p.tiles * split;
-        const int grid = items < num_cus() ? items : num_cus();
-#define P_LAUNCH(TA_, TB_, E_)                                                   \
-    (variant == 0 ? gemm_persistent8<TA_, TB_, E_><<<grid, NTHR, 0, s>>>(p)      \
-                  : gemm_persistent<TA_, TB_, E_><<<grid, PNTHR, 0, s>>>(p))
-#define P_EPI(TA_, TB_)                                  \
-    switch (epi) {                                       \
-        case 0: P_LAUNCH(TA_, TB_, 0); break;            \
-        case 1: P_LAUNCH(TA_, TB_, 1); break;            \
-        case 2: P_LAUNCH(TA_, TB_, 2); break;            \
-        case 3: P_LAUNCH(TA_, TB_, 3); break;            \
-        case 4: P_LAUNCH(TA_, TB_, 4); break;            \
-        case 5: P_LAUNCH(TA_, TB_, 5); break;            \
-        default: P_LAUNCH(TA_, TB_, 6); break;           \
-    }
-        if (!ta && !tb) { P_EPI(false, false) }
-        else if (!ta && tb) { P_EPI(false, true) }
-        else if (ta && !tb) { P_EPI(true, false) }
-        else { P_EPI(true, true) }
-#undef P_EPI
-#undef P_LAUNCH
         TDL_LAUNCH_CHECK();
     }
     const dim3 grid(p.tiles, split);
@@ -1013,13 +990,24 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         }
         TDL_LAUNCH_CHECK();
     }
-    const int sched = variant == 1 ? 0 : 1;
-#define G_LAUNCH(TA_, TB_, E_) (sched ? gemm_kernel<TA_, TB_, E_, 1><<<grid, NTHR, 0, s>>>(p) : gemm_kernel<TA_, TB_, E_, 0><<<grid, NTHR, 0, s>>>(p))
+    if (variant == 1) {  // plain (unpipelined) schedule, benchmark reference
+        if (epi != 0) return (int)hipErrorInvalidValue;
+        if (!ta && !tb) gemm_kernel<false, false, 0, 0><<<grid, NTHR, 0, s>>>(p);
+        else if (!ta && tb) gemm_kernel<false, true, 0, 0><<<grid, NTHR, 0, s>>>(p);
+        else if (ta && !tb) gemm_kernel<true, false, 0, 0><<<grid, NTHR, 0, s>>>(p);
+        else gemm_kernel<true, true, 0, 0><<<grid, NTHR, 0, s>>>(p);
+        TDL_LAUNCH_CHECK();
+    }
+#define G_LAUNCH(TA_, TB_, E_) gemm_kernel<TA_, TB_, E_, 1><<<grid, NTHR, 0, s>>>(p)
 #define G_EPI(TA_, TB_)                                  \
     switch (epi) {                                       \
         case 0: G_LAUNCH(TA_, TB_, 0); break;            \
+        case 1: G_LAUNCH(TA_, TB_, 1); break;            \
+        case 2: G_LAUNCH(TA_, TB_, 2); break;            \
+        case 3: G_LAUNCH(TA_, TB_, 3); break;            \
         case 4: G_LAUNCH(TA_, TB_, 4); break;            \
-        default: return (int)hipErrorInvalidValue;      \
+        case 5: G_LAUNCH(TA_, TB_, 5); break;            \
+        default: G_LAUNCH(TA_, TB_, 6); break;           \
     }
     if (!ta && !tb) { G_EPI(false, false) }
     else if (!ta && tb) { G_EPI(false, true) }

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Fused GEMM epilogues vs library GEMM + separate elementwise pass, at the GPT-2 MLP shapes.
+
+    fc forward:   torch.mm(h2, Wfc) -> tdl_bias_gelu_fwd          vs  gemm.matmul(epi='gelu')
+    proj dgrad:   torch.mm(dy, Wp^T) -> tdl_bias_gelu_bwd (+ db)   vs  gemm.matmul(epi='dgelu', colsum)
+
+Both paths are timed in interleaved rounds in one process on uniform random data; one JSON line
+per product with the median ms of each path and the ratio (library path / fused path).
+
+    python scripts/bench_block_fusion.py [--tokens 32768] [--model medium]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from trustworthy_dl.ops import _lib, gemm  # noqa: E402
+from trustworthy_dl.ops import block  # noqa: E402
+
+
+def timer(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=32768)
+    ap.add_argument("--model", default="medium")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    _lib.lib()
+    dev = torch.device("cuda:0")
+    C = 1024 if args.model == "medium" else 768
+    M = args.tokens
+    r = lambda *s, sc=1.0: ((torch.rand(*s, device=dev) * 2 - 1) * sc).bfloat16()
+    h2, wfc, bfc = r(M, C), r(C, 4 * C, sc=0.05), r(4 * C, sc=0.1)
+    dy, wp = r(M, C), r(4 * C, C, sc=0.05)
+    pre_lib = torch.mm(h2, wfc)
+    pre_fused = torch.empty_like(pre_lib)
+    db = torch.zeros(4 * C, device=dev)
+
+    def fc_lib():
+        return block._bias_gelu_fwd(torch.mm(h2, wfc), bfc)
+
+    def fc_fused():
+        return gemm.matmul(h2, wfc, bias=bfc, epi="gelu", aux=pre_fused)
+
+    def dg_lib():
+        return block._bias_gelu_bwd(torch.mm(dy, wp.t()), pre_lib, bfc, db)
+
+    def dg_fused():
+        return gemm.matmul(dy, wp.t(), epi="dgelu", aux=pre_fused, colsum=db)
+
+    # numerics: both paths against each other (fp32 reference checks live in tests/test_gemm_gpu.py)
+    f1, f2 = fc_lib(), fc_fused()
+    err_fc = float((f1.float() - f2.float()).abs().max() / f1.float().abs().max())
+    d1, d2 = dg_lib(), dg_fused()
+    err_dg = float((d1.float() - d2.float()).abs().max() / d1.float().abs().max())
+    for name, lib_fn, fused_fn, err, fl in (("fc_fwd_gelu", fc_lib, fc_fused, err_fc, 2.0 * M * C * 4 * C),
+                                            ("proj_dgrad_dgelu", dg_lib, dg_fused, err_dg, 2.0 * M * C * 4 * C)):
+        t_l, t_f = [], []
+        lib_fn(); fused_fn()
+        for _ in range(args.rounds):
+            t_l.append(timer(lib_fn, args.iters))
+            t_f.append(timer(fused_fn, args.iters))
+        ml, mf = statistics.median(t_l), statistics.median(t_f)
+        print(json.dumps({"product": name, "M": M, "C": C, "lib_ms": round(ml, 4), "fused_ms": round(mf, 4),
+                          "lib_tf": round(fl / ml / 1e9, 1), "fused_tf": round(fl / mf / 1e9, 1),
+                          "speedup": round(ml / mf, 3), "relerr_vs_lib": round(err, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

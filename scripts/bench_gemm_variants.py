@@ -13,11 +13,11 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from trustworthy_dl.ops import gemm  # noqa: E402
 
-NAMES = {0: "persistent8", 1: "plain", 2: "pipe", 3: "pipe+interleave", 4: "pipe+b_early", 5: "pipe+b_early+interleave",
+NAMES = {0: "default", 1: "plain", 2: "pipe", 3: "pipe+interleave", 4: "pipe+b_early", 5: "pipe+b_early+interleave",
          6: "ABL_no_vmwait", 7: "ABL_no_vmwait_no_barrier", 8: "pipe+setprio", 9: "pipe+interleave+setprio",
-         10: "k8wave", 11: "persistent4", 12: "persistent8_norot",
-         13: "P8_ABL_noDMA", 14: "P8_ABL_noLDSread", 15: "P8_ABL_noDMA_noread", 16: "P8_ABL_nowait",
-         17: "P8_ABL_noDMA_nowait", 18: "P8_ABL_noread_nowait", 19: "P8_ABL_mfma_only"}
+         10: "k8wave", 11: "persistent4", 12: "persistent8",
+         13: "P8_ABL_noDMA", 14: "P8_ABL_noLDSread", 16: "P8_ABL_nowait", 17: "P8_ABL_noDMA_nowait",
+         18: "P8_ABL_mfma_only", 19: "persistent8_norot"}
 
 
 def timer(fn, iters):
@@ -32,7 +32,7 @@ def timer(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,10,13,14,15,16,17,18,19")
+    ap.add_argument("--variants", default="0,11,12")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()

@@ -343,3 +343,43 @@ def test_quarantined_stage_does_not_shrink_clip_scale():
     assert scales, "the attacked stage was never quarantined"
     for got, want in scales:
         assert abs(got - want) <= 1e-4 * max(1.0, want)
+
+
+def test_reference_per_phase_loop_matches_train_step():
+    """The reference's per-phase loop (distributed_trainer.py:382-446): forward_pass ->
+    calculate_loss -> backward_pass -> update_trust_scores -> optimizer_step changes the weights
+    exactly as ``train_step`` does on the same batch (same loss, same updated parameters)."""
+    from trustworthy_dl import DistributedTrainer
+    kw = dict(model_name="gpt2-tiny", num_nodes=2, seq_len=32, micro_batches=1, batch_size=4, device="cpu",
+              compute_dtype="fp32", checkpoint_interval=0, seed=3, layer_granularity="block")
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(0, 50257, (4, 33), generator=g)
+    batch = {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+
+    a = DistributedTrainer(**kw)
+    a.create_model_partitions()
+    a.engine.train_step(batch)
+    loss_a = a.engine.flush()
+
+    b = DistributedTrainer(**kw)
+    b.create_model_partitions()
+    before = {n: st.flat.master.clone() for n, st in b.engine.stages.items()}
+    out, node_outputs = b.forward_pass(batch["input"])
+    assert out.shape[-1] >= 50257 and set(node_outputs) == set(b.engine.plan.ranks)
+    loss = b.calculate_loss(out, batch["target"])
+    grads = b.backward_pass(loss)
+    assert set(grads) == set(b.engine.plan.ranks)
+    b.update_trust_scores(node_outputs, grads)
+    loss_b = b.optimizer_step()
+    b.engine.flush()
+    assert loss_b == pytest.approx(loss_a, rel=1e-5)
+    assert b.engine.global_step == a.engine.global_step == 1
+    for n, st in b.engine.stages.items():
+        assert not torch.equal(st.flat.master, before[n]), f"stage {n} weights did not change"
+        ref = a.engine.stages[n].flat.master
+        assert torch.allclose(st.flat.master, ref, rtol=1e-4, atol=1e-6), n
+    # a second reference-style step keeps going (step bookkeeping closes/opens correctly)
+    out, node_outputs = b.forward_pass(batch["input"])
+    loss2 = b.calculate_loss(out, batch["target"])
+    b.backward_pass(loss2)
+    assert b.optimizer_step() < loss_b

@@ -32,6 +32,10 @@ def main(argv=None):
     p.add_argument("--resume", type=str, default=None, help="checkpoint path or 'latest'")
     p.add_argument("--attack", action="store_true")
     p.add_argument("--device", type=str, default=None)
+    p.add_argument("--heartbeat", type=float, default=None, help="seconds between liveness beats (0 = off)")
+    p.add_argument("--abort-on-offline", action="store_true",
+                   help="exit non-zero when a peer goes OFFLINE; restart the job with --resume latest "
+                        "on the surviving ranks (the checkpoint is re-planned over them)")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
 
@@ -43,7 +47,8 @@ def main(argv=None):
     over = {"model_name": a.model, "model_size": a.size, "dataset_name": a.dataset, "num_nodes": a.nodes,
             "num_epochs": a.epochs, "batch_size": a.batch_size, "learning_rate": a.lr, "seq_len": a.seq_len,
             "micro_batches": a.micro_batches, "batches_per_epoch": a.batches_per_epoch,
-            "checkpoint_dir": a.checkpoint_dir, "device": a.device}
+            "checkpoint_dir": a.checkpoint_dir, "device": a.device, "heartbeat_interval": a.heartbeat,
+            "abort_on_offline": True if a.abort_on_offline else None}
     if a.config:
         cfg, atk, _ = load_config(a.config, over)
     else:

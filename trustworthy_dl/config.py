@@ -55,6 +55,10 @@ class TrainingConfig:
     device: str = "auto"
     seed: int = 0
     verifier: Dict[str, Any] = field(default_factory=dict)
+    heartbeat_interval: float = 0.0       # distributed: seconds between liveness beats (0 = off)
+    heartbeat_timeout: float = 30.0       # silence after which a peer is OFFLINE
+    abort_on_offline: bool = False        # exit non-zero on OFFLINE so an elastic restart resumes
+                                          # from the latest checkpoint on the surviving ranks
 
 
 @dataclass
@@ -104,6 +108,11 @@ def load_config(path: str, overrides: Optional[Dict[str, Any]] = None):
         tc["data_parallel"] = int(ds["data_parallel"])
     if "layer_granularity" in ds:
         tc["layer_granularity"] = str(ds["layer_granularity"])
+    for k in ("heartbeat_interval", "heartbeat_timeout"):
+        if k in ds:
+            tc[k] = float(ds[k])
+    if "abort_on_offline" in ds:
+        tc["abort_on_offline"] = bool(ds["abort_on_offline"])
     sec = raw.get("security", {}) or {}
     mapping = {"trust_threshold": "trust_threshold", "attack_detection": "attack_detection_enabled",
                "gradient_verification": "gradient_verification_enabled", "reassignment": "reassignment_enabled",

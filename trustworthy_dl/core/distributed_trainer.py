@@ -83,6 +83,8 @@ class DistributedTrainer:
         self.schedulers: Dict[int, Any] = {}
         self.engine: Optional[PipelineEngine] = None
         self._owns_pg = False
+        self._phase_open = False      # per-phase API: a step opened by forward_pass, closed by optimizer_step
+        self._phase_loss: Optional[torch.Tensor] = None
         logger.info("Initialized DistributedTrainer with %d nodes", config.num_nodes)
 
     # ------------------------------------------------------------------ properties mirroring engine state
@@ -131,7 +133,8 @@ class DistributedTrainer:
             trust_decay_per_step=c.trust_decay_per_step, reassign=c.reassignment_enabled,
             max_reassignment_attempts=c.max_reassignment_attempts, seed=c.seed,
             data_parallel=c.data_parallel, defer_wgrad=c.defer_wgrad,
-            layer_granularity=c.layer_granularity)
+            layer_granularity=c.layer_granularity, heartbeat_interval=c.heartbeat_interval,
+            heartbeat_timeout=c.heartbeat_timeout, abort_on_offline=c.abort_on_offline)
 
     def create_model_partitions(self, model_name: Optional[str] = None) -> Dict[int, torch.nn.Module]:
         """Build the model, plan a cost-balanced partition over the nodes and instantiate the stages
@@ -178,6 +181,10 @@ class DistributedTrainer:
         are re-sharded by ``reassign_node_tasks`` instead."""
         self._ensure_engine()
         e = self.engine
+        if not self._phase_open:       # first phase of a reference-style step
+            e.begin_step()
+            self._phase_open = True
+            self._phase_loss = None
         seq = list(node_sequence) if node_sequence is not None else list(e.plan.ranks)
         x = inputs
         outs = {}
@@ -202,6 +209,7 @@ class DistributedTrainer:
         """loss.backward() then per-node gradient verification (distributed_trainer.py:177-207)."""
         self._ensure_engine()
         loss.backward()
+        self._phase_loss = loss.detach() if self._phase_loss is None else self._phase_loss + loss.detach()
         grads = {}
         for node in reversed(list(node_sequence) if node_sequence is not None else list(self.engine.plan.ranks)):
             st = self.engine.stages.get(node)
@@ -224,7 +232,8 @@ class DistributedTrainer:
     def calculate_output_deviation(self, output: Optional[torch.Tensor], node_id: int) -> float:
         if output is None:
             return 1.0
-        mean, std = float(output.float().mean()), float(output.float().std())
+        o = output.detach().float()
+        mean, std = float(o.mean()), float(o.std())
         dev = output_deviation(mean, std, self.node_monitor.get_expected_mean(node_id),
                                self.node_monitor.get_expected_std(node_id))
         self.node_monitor.record_output(node_id, mean, std)
@@ -286,11 +295,26 @@ class DistributedTrainer:
         from ..ops import cross_entropy
         if outputs.dim() == 0:
             return outputs  # loss stages already return the loss
-        return cross_entropy(outputs.reshape(-1, outputs.shape[-1]), targets.reshape(-1))
+        # GPT-2 logits carry the padded vocabulary rows (50257 -> 50304): the softmax covers the
+        # real classes only, as the fused LM-head loss of train_step does
+        cfg = getattr(self.engine.model, "config", None) if self.engine is not None else None
+        ncls = getattr(cfg, "vocab_size", None) or self.config.num_classes
+        return cross_entropy(outputs.reshape(-1, outputs.shape[-1]), targets.reshape(-1), ncls)
 
-    def optimizer_step(self, gradients=None):
-        """Optimizer steps run inside the engine (fused AdamW after verification); kept for API parity."""
-        return None
+    def optimizer_step(self, gradients=None) -> Optional[float]:
+        """Apply the step whose gradients ``backward_pass`` accumulated (distributed_trainer.py:441-446):
+        tied-weight reduction, device verification digest + quarantine, global-norm clipping and
+        the fused AdamW on every local stage — the tail ``train_step`` runs, so the per-phase loop
+        and ``train_step`` update the weights identically.  ``gradients`` is accepted for API
+        parity; the engine reads the stages' flat gradient buffers directly.  Returns the loss."""
+        self._ensure_engine()
+        if not self._phase_open:
+            return None
+        loss = self._phase_loss
+        self.engine.end_step(loss)
+        self._phase_open = False
+        self._phase_loss = None
+        return None if loss is None else float(loss)
 
     def train_epoch(self, dataloader, epoch: int) -> float:
         self._ensure_engine()

@@ -145,7 +145,7 @@ class ExperimentRunner:
         for i, m in enumerate(new):
             if m.get("loss") is None:
                 continue
-            if i % max(1, self.config.save_interval) == 0 or True:
+            if i % max(1, self.config.save_interval) == 0:   # experiment_runner.py:196
                 self._collect_batch_metrics(epoch, m.get("step", i), m["loss"], m)
         losses = [m["loss"] for m in new if m.get("loss") is not None]
         return float(np.mean(losses)) if losses else float("nan")
@@ -163,7 +163,9 @@ class ExperimentRunner:
         attack = self.attacker.get_attack_statistics() if self.attacker else {}
         system = {"memory": MetricsCollector.device_memory(), "epoch_time_s": epoch_time,
                   "communication_overhead": self._estimate_communication_overhead(),
-                  "gpu_utilization": self._get_gpu_utilization()}
+                  "gpu_utilization": self._get_gpu_utilization(),
+                  "pipeline_busy_fraction": self._pipeline_busy_fraction(),
+                  "gpu": MetricsCollector.gpu_system_metrics()}
         self.results_data["attack_metrics"].append({"epoch": epoch, **{k: v for k, v in attack.items()
                                                                         if not isinstance(v, (list, dict))}})
         self.results_data["system_metrics"].append({"epoch": epoch, **system})
@@ -178,6 +180,14 @@ class ExperimentRunner:
         return float(mem.get("hbm_used_fraction", 0.0))
 
     def _get_gpu_utilization(self) -> float:
+        """Device busy fraction from the amdgpu driver (sysfs ``gpu_busy_percent``, the counter
+        rocm-smi reports); on hosts without one, the pipeline busy fraction below."""
+        m = MetricsCollector.gpu_system_metrics()
+        if "gpu_busy_percent" in m:
+            return m["gpu_busy_percent"] / 100.0
+        return self._pipeline_busy_fraction()
+
+    def _pipeline_busy_fraction(self) -> float:
         """Fraction of step time not spent blocked in pipeline communication (host-measured)."""
         e = self.trainer.engine
         return 1.0 - (e._comm_wait / e._step_time) if e._step_time > 0 else 0.0

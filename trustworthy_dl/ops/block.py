@@ -15,6 +15,13 @@ is one ``torch.autograd.Function`` whose forward/backward call the gfx950 kernel
 * the bias gradients of the two residual-stream projections (``bp`` = colsum(dy), ``bo`` =
   colsum(dy1)) are column partials of that same LayerNorm-backward pass, not separate reductions;
 * weight gradients accumulate in fp32 straight into ``param.main_grad`` (GEMM beta=1 epilogue);
+* optionally the MLP's elementwise work rides in the native MFMA GEMM's epilogue (csrc/gemm.hip):
+  forward ``f = gelu(h2 @ Wfc + bfc)`` stores the pre-activation and the activation from one
+  kernel, backward ``dpre = (dy @ Wp^T) * gelu'(pre)`` accumulates the ``bfc`` gradient as column
+  sums in the same kernel (TDL_NATIVE_GEMM=mlp; ``all`` also routes the plain projections to it).
+  The default is ``off`` (hipBLASLt + the separate bias/GELU kernels) because that measures
+  faster on MI355X today: profiles/r2_gemm_native_vs_hipblaslt.jsonl (native 0.69-0.86x of
+  hipBLASLt per product) and profiles/r2_gemm_fused_epilogue_vs_lib.jsonl (fused 0.65-0.77x);
 * autograd bookkeeping is one node per block instead of ~12 (host time matters at 8 stages x
   64 micro-batches per step).
 
@@ -136,9 +143,33 @@ def _colsum_into(acc, d):
         acc.add_(d.float().sum(0))
 
 
+def _native_gemm_mode() -> str:
+    return os.environ.get("TDL_NATIVE_GEMM", "off")
+
+
+def _native_mlp(h2, wfc, bfc) -> bool:
+    if not h2.is_cuda or _native_gemm_mode() == "off" or bfc.dtype != torch.bfloat16:
+        return False
+    from . import gemm
+    return gemm.supported(h2, wfc)
+
+
+def _mm(a, b, bias=None):
+    """a @ b (+ bias): the native kernel under TDL_NATIVE_GEMM=all, the library GEMM otherwise."""
+    if a.is_cuda and _native_gemm_mode() == "all":
+        from . import gemm
+        if gemm.supported(a, b) and (bias is None or bias.dtype == torch.bfloat16):
+            return gemm.matmul(a, b, bias=bias)
+    return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)
+
+
 def _addmm_inplace(c, a, b):
     """c += a @ b (c is a fresh, un-saved buffer)."""
     if c.is_cuda:
+        if _native_gemm_mode() == "all":
+            from . import gemm
+            if gemm.supported(a, b):
+                return gemm.matmul(a, b, out=c, epi="resadd")
         return c.addmm_(a, b)
     return c.copy_((c.float() + a.float() @ b.float()).to(c.dtype))
 
@@ -152,18 +183,26 @@ class _GPT2BlockFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         h1, mean1, rstd1 = _ln_fwd(x2, ln1_w, ln1_b, eps)
-        qkv = torch.addmm(b_qkv, h1, fwd_weight(w_qkv))
+        qkv = _mm(h1, fwd_weight(w_qkv), b_qkv)
         o, lse, scale = attn_fwd(qkv.view(B, T, 3 * C), n_head, True)
         o2 = o.view(B * T, C)
-        z = torch.mm(o2, fwd_weight(w_o))
+        z = _mm(o2, fwd_weight(w_o))
         y1, y, h2, mean2, rstd2 = _add_bias_ln_fwd(x2, z, b_o, b_p, ln2_w, ln2_b, eps, (B, T, C))
         del z
-        pre = torch.mm(h2, fwd_weight(w_fc))
-        f = _bias_gelu_fwd(pre, b_fc)
+        wfc = fwd_weight(w_fc)
+        fused_mlp = _native_mlp(h2, wfc, b_fc)
+        if fused_mlp:   # pre = h2 @ Wfc + bfc and f = gelu(pre) from one GEMM epilogue
+            pre = torch.empty(h2.shape[0], wfc.shape[1], dtype=h2.dtype, device=h2.device)
+            from . import gemm
+            f = gemm.matmul(h2, wfc, bias=b_fc, epi="gelu", aux=pre)
+        else:           # pre = h2 @ Wfc (bias added inside the GELU kernel)
+            pre = torch.mm(h2, wfc)
+            f = _bias_gelu_fwd(pre, b_fc)
         _addmm_inplace(y.view(B * T, C), f, fwd_weight(w_p))  # y = y1 + bp + f @ Wp
         ctx.save_for_backward(x2, h1, mean1, rstd1, qkv, o2, lse, y1, h2, mean2, rstd2, pre, f,
                               ln1_w, ln1_b, w_qkv, b_qkv, w_o, b_o, ln2_w, ln2_b, w_fc, b_fc, w_p, b_p)
         ctx.dims = (B, T, C, n_head, scale)
+        ctx.fused_mlp = fused_mlp
         return y
 
     @staticmethod
@@ -182,18 +221,25 @@ class _GPT2BlockFn(torch.autograd.Function):
         wdefer = run_or_defer if all(_wants_main_grad(p) for p in (w_qkv, b_qkv, w_o, w_fc, w_p)) else (lambda fn: fn())
         # MLP branch
         wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2))
-        df = torch.mm(dy2, w_p.t())
-        dpre = _bias_gelu_bwd(df, pre, b_fc, g_bfc)
-        del df
+        if ctx.fused_mlp and _native_mlp(dy2, w_p.t(), b_fc):
+            from . import gemm   # dpre = (dy @ Wp^T) * gelu'(pre), bfc grad as column sums
+            dpre = gemm.matmul(dy2, w_p.t(), epi="dgelu", aux=pre, colsum=g_bfc)
+        else:
+            df = torch.mm(dy2, w_p.t())
+            if ctx.fused_mlp:    # pre already holds the bias
+                dpre = _bias_gelu_bwd(df, pre, torch.zeros_like(b_fc), g_bfc)
+            else:
+                dpre = _bias_gelu_bwd(df, pre, b_fc, g_bfc)
+            del df
         wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre))
-        dh2 = torch.mm(dpre, w_fc.t())
+        dh2 = _mm(dpre, w_fc.t())
         del dpre
         # dy1 = dy + LN2_bwd(dh2); bp grad = colsum(dy), bo grad = colsum(dy1) from the same pass
         dy1 = _ln_bwd(dh2, y1, ln2_w, mean2, rstd2, g_ln2w, g_ln2b, dres=dy2, sres_acc=g_bp, sdx_acc=g_bo)
         del dh2
         # attention branch
         wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1))
-        do = torch.mm(dy1, w_o.t())
+        do = _mm(dy1, w_o.t())
         dqkv = attn_bwd(qkv.view(B, T, 3 * C), o2.view(B, T, C), lse, do.view(B, T, C), H, True, scale)
         del do
         dqkv2 = dqkv.view(B * T, 3 * C)
@@ -204,7 +250,7 @@ class _GPT2BlockFn(torch.autograd.Function):
         wdefer(_qkv_grads)
         dx = None
         if ctx.needs_input_grad[0]:
-            dh1 = torch.mm(dqkv2, w_qkv.t())
+            dh1 = _mm(dqkv2, w_qkv.t())
             dx = _ln_bwd(dh1, x2, ln1_w, mean1, rstd1, g_ln1w, g_ln1b, dres=dy1).view(B, T, C)
         grads = tuple(None if _wants_main_grad(p) else a.to(p.dtype) for p, a in zip(params, acc))
         return (dx, *grads, None, None)

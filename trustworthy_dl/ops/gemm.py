@@ -25,8 +25,9 @@ from ._lib import ptr, stream_ptr
 
 EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f32atomic": 6}
 BK = 64
-# A/B switch for benchmarks: 0 = shipped schedule, 1 = plain (unpipelined) schedule, >= 2 = the
-# pipeline variants of tdl_gemm (NT, bf16 out only; some are timing-only ablations)
+# A/B switch for benchmarks: 0 = shipped kernel (8-wave, pipelined), 1 = plain (unpipelined)
+# schedule, >= 2 = schedule variants / persistent kernels of tdl_gemm (NT, bf16 out only; some are
+# timing-only ablations: csrc/gemm.hip tdl_gemm)
 VARIANT = 0
 
 

@@ -38,7 +38,7 @@ from ..ops import stats as dstats
 from ..ops.layers import bump_weight_generation
 from ..ops.layers import defer_weight_grads
 from ..runtime.tracing import PhaseTracer
-from .comm import P2PComm, all_gather_rows, batched_transfer
+from .comm import P2PComm, all_gather_rows, batched_transfer, broadcast_ints
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
 from .stage import Stage, tied_groups
@@ -348,10 +348,7 @@ class PipelineEngine:
         read: step reports are consumed exactly ``REPORT_LAG`` steps later on every rank (so the
         host never stalls the device queue, and collective decisions such as a re-shard happen
         at the same step everywhere); ``flush()`` drains the rest."""
-        self._consume_reports(upto=self.global_step + 1 - self.REPORT_LAG)
-        bump_weight_generation()   # weights may have changed since the last step (update, re-shard, restore, load)
-        self.global_step += 1
-        self.trust.advance_step(self.global_step)
+        self.begin_step()
         progress.mark(f"step {self.global_step}: pipeline schedule")
         t0 = time.perf_counter()
         truth: Dict[int, bool] = {}
@@ -372,6 +369,24 @@ class PipelineEngine:
         self.tracer.end_step(self.global_step)
         self.tracer.resolve()
         self._step_time = time.perf_counter() - t0
+        return self.last_loss
+
+    def begin_step(self) -> int:
+        """Open an optimizer step (``train_step`` does this itself; the reference per-phase API —
+        DistributedTrainer.forward_pass / backward_pass / optimizer_step — calls it explicitly)."""
+        self._consume_reports(upto=self.global_step + 1 - self.REPORT_LAG)
+        bump_weight_generation()   # weights may have changed since the last step (update, re-shard, restore, load)
+        self.global_step += 1
+        self.trust.advance_step(self.global_step)
+        return self.global_step
+
+    def end_step(self, loss: Optional[torch.Tensor], truth: Optional[Dict[int, bool]] = None) -> Optional[float]:
+        """Close a step whose gradients are already accumulated in the stages' flat buffers (by an
+        external ``loss.backward()``): tied all-reduce, verification digest, attribution, trust
+        update, global-norm clipping + quarantine, fused AdamW — the same tail as ``train_step``."""
+        self._finish_step(None if loss is None else loss.detach(), dict(truth or {}))
+        self.tracer.end_step(self.global_step)
+        self.tracer.resolve()
         return self.last_loss
 
     # ------------------------------------------------------------------ attacks on a stage
@@ -1091,6 +1106,11 @@ class PipelineEngine:
             return
         keep = keep[: self.num_layers]
         new_plan = make_plan(self.costs, keep, self.plan.version + 1, self.cfg.balanced_partition)
+        if self.distributed:
+            # one decision for everyone: rank 0's plan is broadcast (every rank computed it from the
+            # same all-gathered report, but floats / trust state must not be able to split the job)
+            new_plan = PlacementPlan.from_list(broadcast_ints(new_plan.to_list() if self.rank == 0 else None, 0,
+                                                              self.device))
         t0 = time.perf_counter()
         restored = {c: self._shadow_meta[c][0] for c in compromised if self._shadow_usable(c)}
         moved = self._migrate(new_plan, restore=list(restored))
@@ -1341,13 +1361,58 @@ class PipelineEngine:
     def trust_state(self) -> Dict[str, torch.Tensor]:
         return {"values": self.t_values.cpu(), "counts": self.t_counts.cpu(), "status": self.t_status.cpu()}
 
-    def load_trust_state(self, sd):
-        self.t_values.copy_(sd["values"])
-        self.t_counts.copy_(sd["counts"])
-        self.t_status.copy_(sd["status"])
+    def load_trust_state(self, sd, partial: bool = False):
+        """``partial``: the saved job had a different node count; the first ``len`` entries are
+        restored, the rest keep their initial values."""
+        for dst, key in ((self.t_values, "values"), (self.t_counts, "counts"), (self.t_status, "status")):
+            src = sd[key]
+            if partial:
+                k = min(dst.numel(), src.numel())
+                dst[:k].copy_(src[:k])
+            else:
+                dst.copy_(src)
+
+    def load_layer_states(self, layers: Dict[int, Dict], step: int):
+        """Fill the local stages layer by layer (fp32 master + AdamW moments + buffers) from a saved
+        job whose plan differs from this one (utils/checkpoint.load_checkpoint).  Tied parameters
+        that the saved stage stored under another layer of their tie group are found there."""
+        alias: Dict[Tuple[int, str], List[Tuple[int, str]]] = {}
+        for grp in self.ties:
+            for m in grp:
+                alias[m] = [o for o in grp if o != m]
+
+        def find(kind, li, attr):
+            ent = layers.get(li, {}).get(kind, {})
+            if attr in ent:
+                return ent[attr]
+            for lj, aj in alias.get((li, attr), []):
+                ent = layers.get(lj, {}).get(kind, {})
+                if aj in ent:
+                    return ent[aj]
+            raise KeyError(f"checkpoint holds no {kind[:-1]} '{attr}' of layer {li}")
+
+        for node, st in self.stages.items():
+            a, _ = st.layer_range
+            for i, name in enumerate(st.flat.names):
+                k, attr = name.split(".", 1)
+                m, ea, eas = find("params", a + int(k), attr)
+                st.flat.view(st.flat.master, i).copy_(m)
+                st.flat.view(st.flat.exp_avg, i).copy_(ea)
+                st.flat.view(st.flat.exp_avg_sq, i).copy_(eas)
+            for name, b in st.module.named_buffers():
+                k, attr = name.split(".", 1)
+                b.copy_(find("buffers", a + int(k), attr))
+            st.flat.step_count = int(step)
+            if st.flat.data is not st.flat.master:
+                st.flat.data.copy_(st.flat.master)
+            st.param_checksum = None
+        bump_weight_generation()
 
     def load_stage_states(self, model_sd: Dict[int, Dict], optim_sd: Dict[int, Dict],
                           verifier_sd: Optional[Dict[int, Dict]] = None):
+        missing = [n for n in self.stages if n not in optim_sd and n not in model_sd]
+        if missing:
+            raise KeyError(f"checkpoint holds no state for local stage node(s) {missing}")
         for node, st in self.stages.items():
             if node in optim_sd:
                 st.flat.load_state_dict(optim_sd[node])

@@ -20,7 +20,7 @@ import json
 import logging
 import os
 from dataclasses import asdict
-from typing import Dict, Optional
+from typing import Dict, Optional, Sequence, Set, Tuple
 
 import torch
 import torch.distributed as dist
@@ -76,49 +76,145 @@ def save_checkpoint(trainer, path: Optional[str] = None) -> str:
     return path
 
 
-def consolidate(path: str) -> Dict:
-    """Merge a sharded checkpoint into the reference's single top-level dict."""
+def _shard_path(path: str, shard: str) -> str:
+    sp = os.path.join(os.path.dirname(path), shard)
+    if not os.path.exists(sp):
+        raise FileNotFoundError(f"checkpoint {path}: shard {shard} is missing (refusing to resume a stage "
+                                f"from freshly initialised weights)")
+    return sp
+
+
+def consolidate(path: str, nodes: Optional[Sequence[int]] = None) -> Dict:
+    """Merge a sharded checkpoint into the reference's single top-level dict.  ``nodes``: load only
+    these ranks' shards (a resuming rank needs its own, not every rank's).  A listed shard that is
+    missing raises: silently resuming a stage from fresh weights is worse than failing."""
     ck = torch.load(path, map_location="cpu", weights_only=True)
-    for shard in ck.pop("shards", []):
-        sp = os.path.join(os.path.dirname(path), shard)
-        if not os.path.exists(sp):
+    shards = ck.pop("shards", [])
+    for r, shard in enumerate(shards):
+        if nodes is not None and r not in nodes:
             continue
-        s = torch.load(sp, map_location="cpu", weights_only=True)
+        s = torch.load(_shard_path(path, shard), map_location="cpu", weights_only=True)
         for key in ("model_partitions", "optimizers", "verifiers"):
             ck.setdefault(key, {}).update(s.get(key, {}))
     return ck
 
 
+def _layer_states(path: str, ck: Dict, saved_plan, want: Set[int]) -> Tuple[Dict[int, Dict], int]:
+    """Per-layer optimizer state {layer: {"params": {attr: (master, exp_avg, exp_avg_sq)},
+    "buffers": {attr: tensor}}} for the layers in ``want``, read from the saved stages that held
+    them (stage-local names ``"<i>.<attr>"`` -> global layer ``a + i``); only those stages'
+    shards are loaded.  Also returns the saved optimizer step count."""
+    shards = ck.get("shards")
+    out: Dict[int, Dict] = {}
+    step = 0
+    for node, (a, b) in zip(saved_plan.ranks, saved_plan.ranges):
+        if not any(a <= li < b for li in want):
+            continue
+        if shards is not None:
+            sh = torch.load(_shard_path(path, shards[node]), map_location="cpu", weights_only=True)
+            opt, model = sh["optimizers"].get(node), sh["model_partitions"].get(node, {})
+        else:
+            opt, model = ck["optimizers"].get(node), ck["model_partitions"].get(node, {})
+        if opt is None:
+            raise KeyError(f"checkpoint {path}: no optimizer state for saved stage on node {node}")
+        step = max(step, int(opt["step"]))
+        off = 0
+        for name, shp in zip(opt["names"], opt["shapes"]):
+            n = int(torch.Size(shp).numel())
+            i, attr = name.split(".", 1)
+            li = a + int(i)
+            if li in want:
+                ent = out.setdefault(li, {"params": {}, "buffers": {}})
+                ent["params"][attr] = tuple(opt[k][off:off + n].view(shp) for k in ("master", "exp_avg", "exp_avg_sq"))
+            off += n
+        pnames = set(opt["names"])
+        for name, t in model.items():
+            if name in pnames:
+                continue
+            i, attr = name.split(".", 1)
+            li = a + int(i)
+            if li in want:
+                out.setdefault(li, {"params": {}, "buffers": {}})["buffers"][attr] = t
+    return out, step
+
+
+def _resize_trust(trainer, ck: Dict, live: int):
+    """Trust state of a job resumed on ``live`` nodes: nodes beyond it are retired (their records
+    stay in the attack / reassignment histories), missing ones start fresh."""
+    tm = trainer.trust_manager
+    if "trust_manager" in ck:
+        tm.load_state_dict(ck["trust_manager"])
+    for n in [n for n in list(tm.trust_scores) if n >= live]:
+        tm.trust_scores.pop(n, None)
+        tm.node_status.pop(n, None)
+        tm.node_metrics.pop(n, None)
+    tm.num_nodes = min(tm.num_nodes, live)
+    tm.resize(live)
+    if "device_trust" in ck:
+        sd = ck["device_trust"]
+        k = min(live, int(sd["values"].numel()))
+        trainer.engine.load_trust_state({key: v[:k] for key, v in sd.items()}, partial=True)
+
+
 def load_checkpoint(trainer, path: str):
-    """Restore weights, optimizer state, trust + detector state; re-shards if the saved plan differs
-    from the live one (layers are redistributed through the engine's migration path)."""
-    from ..parallel.partition import PlacementPlan
+    """Restore weights, optimizer state, trust + detector state.
+
+    * same plan as the live engine: each rank reads only its own shard;
+    * a different plan that this job can host (e.g. saved after a re-shard): the saved plan is
+      adopted and the stages rebuilt;
+    * a different world size (a restart with fewer / more ranks, e.g. after ``abort_on_offline``
+      took a node out): rank 0 re-plans the saved layers over the live ranks, the plan is
+      broadcast (``broadcast_ints``) so every rank builds the same one, and each rank assembles its
+      new stages layer by layer from the saved stages that held them (only those shards are read).
+    The reference has no load path at all (distributed_trainer.py:448-463 only saves)."""
+    from ..parallel.comm import broadcast_ints
+    from ..parallel.partition import PlacementPlan, make_plan
     e = trainer.engine
-    ck = consolidate(path)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
     saved_plan = PlacementPlan.from_list(ck["plan"])
     g = ck.get("granularity", "block")
     if g != getattr(e, "granularity", "block"):
         e.set_granularity(g)  # layer indices of the saved plan refer to that unit size
+        e._build()
+    dp = getattr(e, "dp", 1)
     # with data-parallel replicas the manifest holds replica 0's plan; replicas share its layout
-    same_ranks = saved_plan.ranks == e.plan.ranks or getattr(e, "dp", 1) > 1
-    if not same_ranks or saved_plan.ranges != e.plan.ranges:
-        if all(r < e.num_nodes for r in saved_plan.ranks):
-            e.plan = saved_plan
-            e._build()
+    same = (saved_plan.ranks == e.plan.ranks or dp > 1) and saved_plan.ranges == e.plan.ranges
+    hostable = all(r < e.num_nodes for r in saved_plan.ranks) and len(saved_plan.ranks) <= e.pp
+    if same:
+        # each rank reads its own shard (a DP replica's stage node is its own rank)
+        full = consolidate(path, nodes=sorted(e.stages) if e.distributed else None)
+        e.load_stage_states(full["model_partitions"], full["optimizers"], full.get("verifiers") or {})
+    elif dp > 1:
+        raise ValueError("resuming a data-parallel job under a different pipeline layout is not supported")
+    else:
+        if hostable:
+            new_plan = saved_plan
         else:
-            raise ValueError("checkpoint plan references nodes that do not exist in this job")
-    e.load_stage_states(ck["model_partitions"], ck["optimizers"], ck.get("verifiers"))
+            live = list(range(e.pp))[: e.num_layers]
+            new_plan = make_plan(e.costs, live, saved_plan.version + 1, e.cfg.balanced_partition)
+        if e.distributed:
+            new_plan = PlacementPlan.from_list(broadcast_ints(new_plan.to_list() if e.rank == 0 else None, 0,
+                                                              e.device))
+        e.plan = new_plan
+        e._build()
+        want = {li for st in e.stages.values() for li in range(*st.layer_range)}
+        layers, step = _layer_states(path, ck, saved_plan, want)
+        e.load_layer_states(layers, step)
+        if not hostable:
+            e.reassignment_history.append({
+                "event": "resume_replan", "from_plan": saved_plan.describe(), "plan": new_plan.describe(),
+                "step": int(ck["global_step"]), "from_nodes": [r for r in saved_plan.ranks if r >= e.num_nodes],
+                "to_nodes": list(new_plan.ranks)})
     e.global_step = int(ck["global_step"])
     trainer.current_epoch = int(ck["epoch"])
+    hist = list(ck.get("reassignment_history", []))
     e.attack_history[:] = list(ck.get("attack_history", []))
-    e.reassignment_history[:] = list(ck.get("reassignment_history", []))
-    if "trust_manager" in ck:
-        trainer.trust_manager.load_state_dict(ck["trust_manager"])
-    if "device_trust" in ck:
-        e.load_trust_state(ck["device_trust"])
+    e.reassignment_history[:] = hist + [r for r in e.reassignment_history if r.get("event") == "resume_replan"]
+    _resize_trust(trainer, ck, e.num_nodes)
     if "detector" in ck:
         trainer.attack_detector.load_state_dict(ck["detector"])
-    logger.info("Checkpoint loaded: %s (step %d)", path, e.global_step)
+    trainer.config.num_nodes = e.num_nodes
+    logger.info("Checkpoint loaded: %s (step %d, plan %s)", path, e.global_step, e.plan.describe())
 
 
 def latest_checkpoint(ckdir: str) -> Optional[str]:

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import csv
 import json
+import glob
+import os
 import time
 from collections import defaultdict
 from typing import Any, Dict, List, Optional
@@ -53,6 +55,32 @@ class MetricsCollector:
                 "max_allocated_gb": torch.cuda.max_memory_allocated() / 2 ** 30,
                 "hbm_used_fraction": 1.0 - free / total}
 
+    @staticmethod
+    def gpu_system_metrics(device_index: Optional[int] = None) -> Dict[str, float]:
+        """Measured device counters from the amdgpu driver's sysfs (what rocm-smi / amd-smi read):
+        ``gpu_busy_percent``, ``mem_busy_percent``, socket power (W) and edge/junction temperature
+        (C) of the card hosting ``device_index`` (matched by PCI address).  Empty when no AMD GPU is
+        visible (CPU runs).  The reference simulates these (experiment_runner.py:262-274)."""
+        if not torch.cuda.is_available():
+            return {}
+        idx = torch.cuda.current_device() if device_index is None else device_index
+        card = _drm_card_for(idx)
+        if card is None:
+            return {}
+        out: Dict[str, float] = {}
+        for key, fname in (("gpu_busy_percent", "gpu_busy_percent"), ("mem_busy_percent", "mem_busy_percent")):
+            v = _read_num(os.path.join(card, fname))
+            if v is not None:
+                out[key] = v
+        for hw in glob.glob(os.path.join(card, "hwmon", "hwmon*")):
+            for key, fname, scale in (("power_w", "power1_average", 1e-6), ("power_w", "power1_input", 1e-6),
+                                      ("temp_edge_c", "temp1_input", 1e-3), ("temp_junction_c", "temp2_input", 1e-3),
+                                      ("temp_mem_c", "temp3_input", 1e-3)):
+                v = _read_num(os.path.join(hw, fname))
+                if v is not None and key not in out:
+                    out[key] = v * scale
+        return out
+
     def get_summary(self) -> Dict[str, Any]:
         losses = [m["loss"] for m in self.batch_metrics if m.get("loss") is not None]
         times = [m["step_time"] for m in self.batch_metrics if m.get("step_time")]
@@ -79,3 +107,44 @@ class MetricsCollector:
         self.batch_metrics.clear()
         self.epoch_metrics.clear()
         self.counters.clear()
+
+
+def _read_num(path: str) -> Optional[float]:
+    try:
+        with open(path) as f:
+            return float(f.read().strip().split()[0])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+_CARD_CACHE: Dict[int, Optional[str]] = {}
+
+
+def _drm_card_for(device_index: int) -> Optional[str]:
+    """sysfs device directory of the DRM card whose PCI address matches the HIP device."""
+    if device_index in _CARD_CACHE:
+        return _CARD_CACHE[device_index]
+    found = None
+    try:
+        pr = torch.cuda.get_device_properties(device_index)
+        want = (int(getattr(pr, "pci_domain_id", 0)), int(pr.pci_bus_id), int(getattr(pr, "pci_device_id", 0)))
+    except Exception:  # noqa: BLE001
+        want = None
+    cards = sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))
+    for dev in cards:
+        if not os.path.exists(os.path.join(dev, "gpu_busy_percent")):
+            continue
+        addr = os.path.basename(os.path.realpath(dev))          # e.g. 0000:75:00.0
+        try:
+            dom, bus, rest = addr.split(":")
+            slot = int(rest.split(".")[0], 16)
+            key = (int(dom, 16), int(bus, 16), slot)
+        except ValueError:
+            continue
+        if want is not None and key == want:
+            found = dev
+            break
+    if found is None and want is None and cards:
+        found = cards[0]
+    _CARD_CACHE[device_index] = found
+    return found
