@@ -84,7 +84,9 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=64)
     ap.add_argument("--mbs", default="auto",
                     help="sequences per micro-batch, or 'auto' (pipeline-bubble vs GEMM-efficiency model)")
-    ap.add_argument("--no-verify", action="store_true", help="disable detection/verification (ablation)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="ablation: no output / gradient statistics, quantiles, z-scores or weight checksums "
+                         "(only a bare sum-of-squares pass for gradient clipping)")
     ap.add_argument("--lr", type=float, default=5e-5)
     ap.add_argument("--dp", type=int, default=1,
                     help="data-parallel pipeline replicas (default 1: the headline is MP = N stages)")
@@ -201,6 +203,7 @@ def run(args):
     cfg = EngineConfig(p2p_mode=p2p, num_nodes=N, micro_batches=M, seq_len=args.seq_len, data_parallel=dp,
                        adamw=AdamWConfig(lr=args.lr, weight_decay=0.01, max_grad_norm=1.0),
                        attack_detection=verify, gradient_verification=verify, quarantine=verify,
+                       param_integrity=verify,
                        reassign=False, trace_phases=bool(args.trace_phases))
     engine = PipelineEngine(model, cfg)
     del model
@@ -269,6 +272,8 @@ def run(args):
                        "parallelism": f"pp{stages}" + (f"xdp{dp}" if dp > 1 else ""),
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
                        "plan": engine.plan.describe(), "last_loss": engine.last_loss,
+                       "detections": len(engine.attack_history),
+                       "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        "reassignments": [{"step": r["step"], "from_nodes": r["from_nodes"],

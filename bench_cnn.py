@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=64)
     ap.add_argument("--micro-batches", type=int, default=0, help="0 = 1 per stage x 4 (pipelined), 1 at N=1")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--lr", type=float, default=None,
+                    help="AdamW lr (default 1e-3 for ResNets, 1e-4 for VGG: the 25088->4096->4096 classifier "
+                         "diverges at 1e-3 in fp32 on the CPU too, profiles/r2_vgg16_lr_cpu_fp32.json)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -61,7 +64,8 @@ def main():
     model = get_model(name, image_size=args.image_size, seed=1234)
     ncls = model.pipeline_layers()[-1].num_classes
     verify = not args.no_verify
-    cfg = EngineConfig(num_nodes=N, micro_batches=M, adamw=AdamWConfig(lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0),
+    lr = args.lr if args.lr is not None else (1e-4 if name.startswith("vgg") else 1e-3)
+    cfg = EngineConfig(num_nodes=N, micro_batches=M, adamw=AdamWConfig(lr=lr, weight_decay=1e-4, max_grad_norm=1.0),
                        attack_detection=verify, gradient_verification=verify, quarantine=verify, reassign=False)
     engine = PipelineEngine(model, cfg)
     del model
@@ -99,7 +103,7 @@ def main():
             "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16", "data": "synthetic images, random-init weights",
             "config": {"model": name, "global_batch": gb, "image_size": args.image_size, "micro_batches": M,
-                       "parallelism": f"pp{N}", "grad_verify": verify, "plan": engine.plan.describe(),
+                       "parallelism": f"pp{N}", "grad_verify": verify, "plan": engine.plan.describe(), "lr": lr,
                        "last_loss": engine.last_loss}}), flush=True)
     if world > 1:
         dist.barrier()

@@ -113,8 +113,64 @@ ENGINE_SCENARIOS = {
 }
 
 
+DATA_VOCAB = [0]
+WARMUP = [0]       # linear lr warm-up steps   # > 0: the Markov stream uses only this many token ids (learnable in a few hundred steps)
+
+
+def _batches(data: str, batch: int, seq_len: int, vocab: int, n: int, seed: int = 0):
+    """Training batches: ``random`` uniform tokens (flat loss, stationary gradients) or ``markov``
+    (a learnable order-1 Markov stream: the loss falls and gradients drift / correlate)."""
+    if data == "markov":
+        from trustworthy_dl.utils.data_loader import MarkovLanguageModeling
+        yield from MarkovLanguageModeling(batch, seq_len, DATA_VOCAB[0] or vocab, num_batches=n, seed=seed)
+        return
+    g = torch.Generator().manual_seed(seed)
+    for _ in range(n):
+        ids = torch.randint(0, vocab, (batch, seq_len + 1), generator=g)
+        yield {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+
+
+def _engine(device, model_name, stages, batch, mbs, seq_len, vocab, lr, attacker=None, robust="detrend",
+            reassign=False):
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.flat import AdamWConfig
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    from trustworthy_dl.utils.metrics import MetricsCollector
+    extra = {"vocab_size": vocab} if vocab != 50257 else {}
+    model = get_model(model_name, seq_len=seq_len, seed=11, **extra)
+    cfg = EngineConfig(num_nodes=stages, micro_batches=max(1, batch // mbs), seq_len=seq_len, device=device,
+                       adamw=AdamWConfig(lr=lr, weight_decay=0.01, max_grad_norm=1.0, warmup_steps=WARMUP[0]),
+                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=reassign,
+                       verifier={"robust_baseline": robust})
+    return PipelineEngine(model, cfg, attacker=attacker, metrics=MetricsCollector())
+
+
+def run_fp(device: str, model_name: str, stages: int, steps: int, warm: int, batch: int, mbs: int, seq_len: int,
+           vocab: int, data: str, lr: float, robust: str):
+    """False-positive rate of the engine's verdicts on CLEAN training (no attacker): flagged
+    (stage, step) pairs after the warm-up / all scored pairs, plus the loss curve."""
+    eng = _engine(device, model_name, stages, batch, mbs, seq_len, vocab, lr, robust=robust)
+    t0 = time.perf_counter()
+    for b in _batches(data, batch, seq_len, vocab, warm + steps):
+        eng.train_step(b)
+    eng.flush()
+    flags = [(a["step"], a["node_id"], a["attack_type"]) for a in eng.attack_history if a["step"] > warm]
+    losses = [m["loss"] for m in eng.metrics.batch_metrics if m.get("loss") is not None]
+    pairs = steps * stages
+    res = {"data": data, "data_vocab": DATA_VOCAB[0] or vocab, "lr": lr, "lr_warmup": WARMUP[0], "robust": robust,
+           "steps_scored": steps, "stages": stages, "false_positives": len(flags),
+           "fp_rate": round(len(flags) / pairs, 5), "flags": flags[:20],
+           "loss_first": round(losses[0], 4), "loss_at_warm": round(losses[warm - 1], 4), "loss_last": round(losses[-1], 4),
+           "loss_curve_every_25": [round(x, 4) for x in losses[::25]],
+           "final_trust": [round(eng.trust.get_trust_score(n), 3) for n in range(stages)],
+           "wall_s": round(time.perf_counter() - t0, 1)}
+    print(json.dumps({"fp": res}), flush=True)
+    return res
+
+
 def run_engine(device: str, model_name: str, stages: int, steps: int, warm: int, batch: int, mbs: int,
-               seq_len: int, scenarios, target: int, p_attack: float, vocab: int = 50257):
+               seq_len: int, scenarios, target: int, p_attack: float, vocab: int = 50257, data: str = "random",
+               lr: float = 1e-4, robust: str = "detrend"):
     from trustworthy_dl.attacks.adversarial_attacks import AdversarialAttacker, AttackConfig
     from trustworthy_dl.models import get_model
     from trustworthy_dl.parallel.flat import AdamWConfig
@@ -126,18 +182,10 @@ def run_engine(device: str, model_name: str, stages: int, steps: int, warm: int,
         attacker = AdversarialAttacker(AttackConfig(target_nodes=[target], start_step=warm, probability=p_attack,
                                                     seed=7, **kw))
         attacker.activate_attacks()
-        extra = {"vocab_size": vocab} if vocab != 50257 else {}
-        model = get_model(model_name, seq_len=seq_len, seed=11, **extra)
-        cfg = EngineConfig(num_nodes=stages, micro_batches=max(1, batch // mbs), seq_len=seq_len, device=device,
-                           adamw=AdamWConfig(lr=1e-4, weight_decay=0.01, max_grad_norm=1.0),
-                           attack_detection=True, gradient_verification=True, quarantine=True, reassign=False)
-        eng = PipelineEngine(model, cfg, attacker=attacker)
-        del model
-        g = torch.Generator().manual_seed(0)
+        eng = _engine(device, model_name, stages, batch, mbs, seq_len, vocab, lr, attacker=attacker, robust=robust)
         t0 = time.perf_counter()
-        for step in range(warm + steps):
-            ids = torch.randint(0, vocab, (batch, seq_len + 1), generator=g)
-            eng.train_step({"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()})
+        for b in _batches(data, batch, seq_len, vocab, warm + steps):
+            eng.train_step(b)
         eng.flush()
         m = attacker.detection_metrics()
         out[name] = {"tp": m["tp"], "fp": m["fp"], "fn": m["fn"], "precision": round(m["precision"], 3),
@@ -145,6 +193,7 @@ def run_engine(device: str, model_name: str, stages: int, steps: int, warm: int,
                      "mean_time_to_detect_steps": m["mean_time_to_detect_steps"],
                      "injections": len(attacker.injections), "final_loss": eng.last_loss,
                      "final_trust": [round(eng.trust.get_trust_score(n), 3) for n in range(stages)],
+                     "target_status": eng.trust.get_node_status(target).value,
                      "wall_s": round(time.perf_counter() - t0, 1)}
         print(json.dumps({name: out[name]}), flush=True)
         del eng
@@ -155,7 +204,12 @@ def run_engine(device: str, model_name: str, stages: int, steps: int, warm: int,
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--part", choices=["protocol", "engine", "all"], default="protocol")
+    ap.add_argument("--part", choices=["protocol", "engine", "fp", "all"], default="protocol")
+    ap.add_argument("--data", choices=["random", "markov"], default="markov")
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--robust", default="detrend", help="engine z-score baseline: detrend | 1 (median/MAD) | 0")
+    ap.add_argument("--data-vocab", type=int, default=0, help="Markov stream over this many token ids (0 = all)")
+    ap.add_argument("--lr-warmup", type=int, default=0)
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--model", default=None)
     ap.add_argument("--stages", type=int, default=None)
@@ -175,6 +229,15 @@ def main():
     if args.part in ("protocol", "all"):
         res["protocol"] = run_protocol(args.device)
         print(json.dumps({"protocol": res["protocol"]}), flush=True)
+    robust = args.robust if args.robust == "detrend" else int(args.robust)
+    DATA_VOCAB[0] = args.data_vocab
+    WARMUP[0] = args.lr_warmup
+    if args.part in ("fp", "all"):
+        model = args.model or ("gpt2-medium" if gpu else "gpt2-tiny")
+        stages = args.stages or (8 if gpu else 4)
+        res["fp"] = run_fp(args.device, model, stages, args.steps, args.warm, args.batch or (8 if gpu else 4),
+                           args.mbs or (4 if gpu else 2), args.seq_len or (1024 if gpu else 64),
+                           args.vocab or (50257 if gpu else 1024), args.data, args.lr, robust)
     if args.part in ("engine", "all"):
         model = args.model or ("gpt2-medium" if gpu else "gpt2-tiny")
         stages = args.stages or (8 if gpu else 4)
@@ -182,9 +245,10 @@ def main():
                                    args.batch or (8 if gpu else 4), args.mbs or (4 if gpu else 2),
                                    args.seq_len or (1024 if gpu else 64), args.scenarios.split(","),
                                    args.target if args.target is not None else stages // 2, args.p_attack,
-                                   args.vocab or (50257 if gpu else 1024))
+                                   args.vocab or (50257 if gpu else 1024), args.data, args.lr, robust)
         res["engine_config"] = {"model": model, "stages": stages, "steps": args.steps, "warm": args.warm,
-                                "p_attack": args.p_attack}
+                                "p_attack": args.p_attack, "data": args.data, "lr": args.lr, "robust": str(robust),
+                                "data_vocab": args.data_vocab, "lr_warmup": args.lr_warmup}
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)

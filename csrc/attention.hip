@@ -67,6 +67,13 @@ __device__ __forceinline__ bf16x8_t cvt8(const f32x16& v, int base) {
 
 constexpr int HD = 64;
 
+// Element offset of (row, col) in a "plain" [rows][64] bf16 image read with ds_read_b64_tr_b16:
+// the 64-B column half is XOR-flipped on every other row pair.  A transposed read takes 4 rows x
+// 64 B per 32-lane group; at the natural 128-B row stride rows r and r + 2 hit the same 16 banks
+// (2-way conflict on every read, PMC: 5.15 conflict cycles per LDS op in dK/dV).  With the flip the
+// 4 rows cover the 64 banks once.  Writers store 16-B chunks through the same map.
+__device__ __forceinline__ int swz_tr(int row, int col) { return row * HD + (col ^ (((row >> 1) & 1) << 5)); }
+
 // Workgroup -> (batch*head, block) with the nb blocks of one head on ONE XCD, dispatched back to
 // back (heaviest causal block first): the dispatcher sends workgroup L to XCD L % 8, so L = 8 j + x
 // puts stream position j of XCD x on head 8 (j / nb) + x.  The head's K/V (fwd, dQ) or Q/dO (dK/dV)
@@ -138,9 +145,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     };
     auto sstore = [&](int buf) {
         *(uint4*)(Ks[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
-        *(uint4*)(Vs[buf] + srow0 * HD + sch * 8) = vreg0;
+        *(uint4*)(Vs[buf] + swz_tr(srow0, sch * 8)) = vreg0;
         *(uint4*)(Ks[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
-        *(uint4*)(Vs[buf] + srow1 * HD + sch * 8) = vreg1;
+        *(uint4*)(Vs[buf] + swz_tr(srow1, sch * 8)) = vreg1;
     };
     gload(0);
     sstore(0);
@@ -210,8 +217,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const bf16x8_t pf = t == 0 ? (s2 == 0 ? p00 : p01) : (s2 == 0 ? p10 : p11);
                     const int kr = 32 * t + 16 * s2 + 4 * h + tq;
-                    const bf16x8_t v0 = tr_pair(V_ + kr * HD + tcol, V_ + (kr + 8) * HD + tcol);
-                    const bf16x8_t v1 = tr_pair(V_ + kr * HD + 32 + tcol, V_ + (kr + 8) * HD + 32 + tcol);
+                    const bf16x8_t v0 = tr_pair(V_ + swz_tr(kr, tcol), V_ + swz_tr(kr + 8, tcol));
+                    const bf16x8_t v1 = tr_pair(V_ + swz_tr(kr, 32 + tcol), V_ + swz_tr(kr + 8, 32 + tcol));
                     o0 = MFMA32(v0, pf, o0);
                     o1 = MFMA32(v1, pf, o1);
                 }
@@ -332,9 +339,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         const int row = srow + 32 * j;
         const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + row) * ldq + sch * 8);
         const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + row) * ldo + sch * 8);
-        *(uint4*)(Qs[0] + row * HD + sch * 8) = q;
+        *(uint4*)(Qs[0] + swz_tr(row, sch * 8)) = q;
         *(uint4*)(Qw[0] + row * HD + swz) = q;
-        *(uint4*)(dOs[0] + row * HD + sch * 8) = d;
+        *(uint4*)(dOs[0] + swz_tr(row, sch * 8)) = d;
         *(uint4*)(dOw[0] + row * HD + swz) = d;
     }
     if (tid < BQ) {
@@ -393,12 +400,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
                 const int qr = 16 * s2 + 4 * h + tq;
                 const bf16x8_t pb = s2 == 0 ? pb0 : pb1;
                 const bf16x8_t dsb = s2 == 0 ? db0 : db1;
-                const bf16x8_t ado0 = tr_pair(dOb + qr * HD + tcol, dOb + (qr + 8) * HD + tcol);
-                const bf16x8_t ado1 = tr_pair(dOb + qr * HD + 32 + tcol, dOb + (qr + 8) * HD + 32 + tcol);
+                const bf16x8_t ado0 = tr_pair(dOb + swz_tr(qr, tcol), dOb + swz_tr(qr + 8, tcol));
+                const bf16x8_t ado1 = tr_pair(dOb + swz_tr(qr, 32 + tcol), dOb + swz_tr(qr + 8, 32 + tcol));
                 dv0 = MFMA32(ado0, pb, dv0);
                 dv1 = MFMA32(ado1, pb, dv1);
-                const bf16x8_t aq0 = tr_pair(Qb + qr * HD + tcol, Qb + (qr + 8) * HD + tcol);
-                const bf16x8_t aq1 = tr_pair(Qb + qr * HD + 32 + tcol, Qb + (qr + 8) * HD + 32 + tcol);
+                const bf16x8_t aq0 = tr_pair(Qb + swz_tr(qr, tcol), Qb + swz_tr(qr + 8, tcol));
+                const bf16x8_t aq1 = tr_pair(Qb + swz_tr(qr, 32 + tcol), Qb + swz_tr(qr + 8, 32 + tcol));
                 dk0 = MFMA32(aq0, dsb, dk0);
                 dk1 = MFMA32(aq1, dsb, dk1);
             }
@@ -407,9 +414,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 const int row = srow + 32 * j;
-                *(uint4*)(Qs[buf ^ 1] + row * HD + sch * 8) = qn[j];
+                *(uint4*)(Qs[buf ^ 1] + swz_tr(row, sch * 8)) = qn[j];
                 *(uint4*)(Qw[buf ^ 1] + row * HD + swz) = qn[j];
-                *(uint4*)(dOs[buf ^ 1] + row * HD + sch * 8) = dn[j];
+                *(uint4*)(dOs[buf ^ 1] + swz_tr(row, sch * 8)) = dn[j];
                 *(uint4*)(dOw[buf ^ 1] + row * HD + swz) = dn[j];
             }
             if (tid < BQ) {
@@ -490,10 +497,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     };
     auto sstore = [&](int buf) {
         *(uint4*)(Kr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
-        *(uint4*)(Kp[buf] + srow0 * HD + sch * 8) = kreg0;
+        *(uint4*)(Kp[buf] + swz_tr(srow0, sch * 8)) = kreg0;
         *(uint4*)(Vr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = vreg0;
         *(uint4*)(Kr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
-        *(uint4*)(Kp[buf] + srow1 * HD + sch * 8) = kreg1;
+        *(uint4*)(Kp[buf] + swz_tr(srow1, sch * 8)) = kreg1;
         *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
     };
     gload(0);
@@ -544,8 +551,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const bf16x8_t ds = t == 0 ? (s2 == 0 ? d00 : d01) : (s2 == 0 ? d10 : d11);
                     const int kr = 32 * t + 16 * s2 + 4 * h + tq;
-                    const bf16x8_t a0 = tr_pair(Kp_ + kr * HD + tcol, Kp_ + (kr + 8) * HD + tcol);
-                    const bf16x8_t a1 = tr_pair(Kp_ + kr * HD + 32 + tcol, Kp_ + (kr + 8) * HD + 32 + tcol);
+                    const bf16x8_t a0 = tr_pair(Kp_ + swz_tr(kr, tcol), Kp_ + swz_tr(kr + 8, tcol));
+                    const bf16x8_t a1 = tr_pair(Kp_ + swz_tr(kr, 32 + tcol), Kp_ + swz_tr(kr + 8, 32 + tcol));
                     dq0 = MFMA32(a0, ds, dq0);
                     dq1 = MFMA32(a1, ds, dq1);
                 }

@@ -14,6 +14,7 @@
 #define NSTAT 12
 #define NHIST 2048
 #define MAXPART 1024
+#define REF_STRIDE 8   // K3: EMA-reference (cosine) chunks, one in REF_STRIDE
 
 struct Moments {  // central-moment partial, fp64
     double n, mean, m2, m3, m4, mn, mx, abssum;
@@ -211,13 +212,57 @@ __device__ float hist_quantile(const unsigned* hist, double total, double q, flo
     return hi;
 }
 
-__global__ void quantile_kernel(const unsigned* __restrict__ hist, const float* __restrict__ range, float* __restrict__ out) {
-    if (threadIdx.x >= 3) return;
-    double total = 0.0;
-    for (int b = 0; b < NHIST; ++b) total += hist[b];
+// Quantiles from the histogram, one block: every thread owns 8 consecutive bins, a block scan of
+// the per-thread counts gives each thread its cumulative offset, and the thread whose bins hold
+// rank k = q (total - 1) interpolates inside its bin (hist_quantile's convention).
+__global__ __launch_bounds__(256) void quantile_kernel(const unsigned* __restrict__ hist, const float* __restrict__ range,
+                                                       float* __restrict__ out) {
+    constexpr int PER = NHIST / 256;
+    __shared__ double scan[256];
+    const int t = threadIdx.x;
+    double c[PER], mine = 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        c[k] = hist[t * PER + k];
+        mine += c[k];
+    }
+    scan[t] = mine;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan (integers in doubles: exact)
+        const double v = t >= o ? scan[t - o] : 0.0;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    const double total = scan[255];
+    const double before = scan[t] - mine;
+    const float lo = range[0], hi = range[1];
     const double qs[3] = {0.5, 0.25, 0.75};
     const int slot[3] = {4, 7, 8};
-    out[slot[threadIdx.x]] = hist_quantile(hist, total, qs[threadIdx.x], range[0], range[1]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (total <= 0) {
+            if (t == 0) out[slot[q]] = 0.f;
+            continue;
+        }
+        if (!(hi > lo)) {
+            if (t == 0) out[slot[q]] = lo;
+            continue;
+        }
+        const double kq = qs[q] * (total - 1.0);
+        if (t == 255 && kq >= total) out[slot[q]] = hi;
+        if (kq < before || kq >= before + mine) continue;
+        const double w = (double)(hi - lo) / NHIST;
+        double cum = before;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            if (c[k] > 0 && kq < cum + c[k]) {
+                out[slot[q]] = (float)(lo + (t * PER + k + (kq - cum + 0.5) / c[k]) * w);
+                break;
+            }
+            cum += c[k];
+        }
+    }
 }
 
 // Workspace layout (bytes): [Moments x MAXPART][range 2 f32 | nonfinite f32 | pad][hist NHIST u32]
@@ -245,7 +290,7 @@ TDL_API int tdl_tensor_stats(const void* x, int dtype, int64_t n, float* out, vo
     moments_final_kernel<<<1, 256, 0, s>>>(part, g, out, range, hist);
     if (with_quantiles) {
         hist_kernel<<<g, 256, 0, s>>>(x, dtype, n, range, hist);
-        quantile_kernel<<<1, 64, 0, s>>>(hist, range, out);
+        quantile_kernel<<<1, 256, 0, s>>>(hist, range, out);
     }
     hipMemcpyAsync(out + NSTAT, nonfinite, sizeof(float), hipMemcpyDeviceToDevice, s);
     TDL_LAUNCH_CHECK();
@@ -254,16 +299,50 @@ TDL_API int tdl_tensor_stats(const void* x, int dtype, int64_t n, float* out, vo
 // ------------------------------------------------------------------ K3 segmented gradient stats
 // chunks: int64 [C][3] = (segment, start, end) with end - start <= CHUNK; ordered by segment.
 // seg_first: int32 [S + 1] first chunk of every segment.
-// part_seg: double [C][3] = (sum g^2, sum g*ref, sum ref^2) per chunk.
-// ref (nullable) is updated in place: ref <- beta*ref + (1-beta)*g  (ref_valid==0: ref <- g).
+// Three stages, every one of them parallel and deterministic (fixed reduction orders):
+//   partial  one block per chunk: moments + (sum g^2, sum g.ref, sum ref^2, #non-finite), EMA
+//            reference update in place (ref_valid==0: ref <- g).  Launched over any chunk range,
+//            so the engine can run it per layer on a side stream while the backward of earlier
+//            layers is still going (pipeline.py, verification overlap);
+//   segment  one wave per segment: merges its chunks -> norm, cosine, segment moments;
+//   summary  one block: merges the S segment moments -> TENSOR_STATS, norm summary, histogram range.
+// Workspace: [Moments x C][double x 5C][Moments x S][range 2f | nonfinite f | pad f][hist NHIST u32]
+struct GradWs {
+    Moments* part;
+    double* part_seg;
+    Moments* seg;
+    float* range;
+    float* nonfinite;
+    unsigned* hist;
+};
+
+__host__ __device__ inline GradWs grad_ws(void* ws, int C, int S) {
+    GradWs w;
+    w.part = (Moments*)ws;
+    w.part_seg = (double*)((char*)ws + sizeof(Moments) * (size_t)C);
+    w.seg = (Moments*)(w.part_seg + 5 * (size_t)C);
+    w.range = (float*)(w.seg + (size_t)S);
+    w.nonfinite = w.range + 2;
+    w.hist = (unsigned*)(w.range + 4);
+    return w;
+}
+
+TDL_API int64_t tdl_grad_stats_ws_bytes(int C, int S) {
+    return (int64_t)sizeof(Moments) * C + 40ll * C + (int64_t)sizeof(Moments) * S + 16 + 4 * NHIST;
+}
+
 __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restrict__ g, float* __restrict__ ref,
-                                                           const int64_t* __restrict__ chunks, int ref_valid, float beta,
-                                                           Moments* __restrict__ part, double* __restrict__ part_seg,
-                                                           float* __restrict__ nonfinite) {
+                                                           const int64_t* __restrict__ chunks, int c0, int ref_valid,
+                                                           float beta, Moments* __restrict__ part,
+                                                           double* __restrict__ part_seg) {
     __shared__ Moments sh[16];
     __shared__ float red[16];
-    const int c = blockIdx.x;
+    const int c = c0 + blockIdx.x;
     const int64_t start = chunks[3 * c + 1], end = chunks[3 * c + 2];
+    // the EMA reference (cosine feature) is kept on every REF_STRIDE-th chunk only: a 1/8 sample
+    // of a stage's parameters estimates the cosine to well within its step-to-step noise at an
+    // eighth of the reference traffic (read + write of an fp32 copy of the gradient)
+    if (ref && (c % REF_STRIDE) != 0) ref = nullptr;
     ThreadAcc acc;
     acc.init();
     float sq = 0.f, dot = 0.f, rsq = 0.f;
@@ -305,52 +384,88 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
     sq = block_sum(sq, red);
     dot = block_sum(dot, red);
     rsq = block_sum(rsq, red);
+    const float nb = block_sum((float)bad, red);
     if (threadIdx.x == 0) {
         part[c] = r;
-        part_seg[3 * c] = sq;
-        part_seg[3 * c + 1] = dot;
-        part_seg[3 * c + 2] = rsq;
+        part_seg[5 * c] = sq;
+        part_seg[5 * c + 1] = dot;
+        part_seg[5 * c + 2] = rsq;
+        part_seg[5 * c + 3] = nb;
+        part_seg[5 * c + 4] = ref ? sq : 0.0;   // |g|^2 over the reference-tracked chunks
     }
-    if (bad) atomicAdd(nonfinite, (float)bad);
+}
+
+// One wave per segment (4 per block): lanes stride over the segment's chunks in a fixed order,
+// then a fixed-order shuffle tree.  Writes norms / cos and the segment's merged moments.
+__global__ __launch_bounds__(256) void grad_segment_kernel(const Moments* __restrict__ part,
+                                                           const double* __restrict__ part_seg,
+                                                           const int* __restrict__ seg_first, int S, int ref_valid,
+                                                           float* __restrict__ out, Moments* __restrict__ seg,
+                                                           float* __restrict__ nonfinite) {
+    const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sg >= S) return;
+    Moments m;
+    m.n = 0.0; m.mean = m.m2 = m.m3 = m.m4 = 0.0; m.mn = INFINITY; m.mx = -INFINITY; m.abssum = 0.0;
+    double sq = 0.0, dot = 0.0, rsq = 0.0, bad = 0.0, sqt = 0.0;
+    for (int c = seg_first[sg] + lane; c < seg_first[sg + 1]; c += 64) {
+        merge(m, part[c]);
+        sq += part_seg[5 * c];
+        dot += part_seg[5 * c + 1];
+        rsq += part_seg[5 * c + 2];
+        bad += part_seg[5 * c + 3];
+        sqt += part_seg[5 * c + 4];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Moments other = shfl_xor_m(m, o);
+        if ((lane & o) == 0) merge(m, other); else { merge(other, m); m = other; }
+    }
+    sq = wave_sum_d(sq);
+    dot = wave_sum_d(dot);
+    rsq = wave_sum_d(rsq);
+    bad = wave_sum_d(bad);
+    sqt = wave_sum_d(sqt);
+    if (lane == 0) {
+        const double den = sqrt(sqt * rsq);
+        out[18 + sg] = (float)sqrt(sq);
+        // no tracked chunk in this segment (or no reference yet): no cosine (sentinel 2)
+        out[18 + S + sg] = !ref_valid ? 1.f : (den > 0.0 ? (float)(dot / den) : 2.f);
+        seg[sg] = m;
+        if (bad > 0) atomicAdd(nonfinite, (float)bad);  // integer counts: exact in any order
+    }
 }
 
 // out layout: [0..11] tensor stats, [12] num_gradients, [13] grad_norms_mean, [14] grad_norms_std,
 // [15] grad_norms_max, [16] cosine_similarity, [17] nonfinite, [18 .. 18+S) norms, [18+S .. 18+2S) cos.
-__global__ __launch_bounds__(256) void grad_final_kernel(const Moments* __restrict__ part, const double* __restrict__ part_seg,
-                                                         const int* __restrict__ seg_first, int C, int S, int ref_valid,
-                                                         float* __restrict__ out, float* __restrict__ range,
-                                                         unsigned* __restrict__ hist, const float* __restrict__ nonfinite) {
+__global__ __launch_bounds__(256) void grad_summary_kernel(const Moments* __restrict__ seg, int S,
+                                                           float* __restrict__ out, float* __restrict__ range,
+                                                           unsigned* __restrict__ hist, const float* __restrict__ nonfinite) {
     __shared__ Moments sh[16];
     __shared__ float red[16];
     Moments m;
     m.n = 0.0; m.mean = m.m2 = m.m3 = m.m4 = 0.0; m.mn = INFINITY; m.mx = -INFINITY; m.abssum = 0.0;
-    for (int i = threadIdx.x; i < C; i += blockDim.x) merge(m, part[i]);
+    for (int i = threadIdx.x; i < S; i += blockDim.x) merge(m, seg[i]);
     Moments r = block_merge(m, sh);
     if (threadIdx.x == 0) write_moment_stats(r, out, range);
     for (int i = threadIdx.x; i < NHIST; i += blockDim.x) hist[i] = 0u;
-    float* norms = out + 18;
-    float* coss = out + 18 + S;
-    float nsum = 0.f, nsq = 0.f, nmax = 0.f, csum = 0.f;
+    const float* norms = out + 18;
+    const float* coss = out + 18 + S;
+    float nsum = 0.f, nsq = 0.f, nmax = 0.f, csum = 0.f, cn = 0.f;
     for (int sgi = threadIdx.x; sgi < S; sgi += blockDim.x) {
-        double sq = 0.0, dot = 0.0, rsq = 0.0;
-        for (int c = seg_first[sgi]; c < seg_first[sgi + 1]; ++c) {
-            sq += part_seg[3 * c];
-            dot += part_seg[3 * c + 1];
-            rsq += part_seg[3 * c + 2];
-        }
-        const float nrm = (float)sqrt(sq);
-        const double den = sqrt(sq * rsq);
-        const float cs = (ref_valid && den > 0.0) ? (float)(dot / den) : 1.f;
-        norms[sgi] = nrm;
-        coss[sgi] = cs;
+        const float nrm = norms[sgi];
         nsum += nrm;
         nsq += nrm * nrm;
         nmax = fmaxf(nmax, nrm);
-        csum += cs;
+        if (coss[sgi] <= 1.5f) {
+            csum += coss[sgi];
+            cn += 1.f;
+        }
     }
     nsum = block_sum(nsum, red);
     nsq = block_sum(nsq, red);
     csum = block_sum(csum, red);
+    cn = block_sum(cn, red);
     nmax = block_max(nmax, red);
     if (threadIdx.x == 0) {
         const float mean = nsum / S;
@@ -358,28 +473,82 @@ __global__ __launch_bounds__(256) void grad_final_kernel(const Moments* __restri
         out[13] = mean;
         out[14] = sqrtf(fmaxf(nsq / S - mean * mean, 0.f));
         out[15] = nmax;
-        out[16] = csum / S;
+        out[16] = cn > 0.f ? csum / cn : 1.f;
         out[17] = nonfinite[0];
     }
 }
 
-// Workspace: [Moments x C][double x 3C][range 2f | nonfinite f | pad f][hist NHIST u32]; caller sizes it.
-TDL_API int tdl_grad_stats(const float* g, float* ref, const int64_t* table, int C, float* out, int64_t n, float beta,
-                           int S, void* ws, int ref_valid, int with_quantiles, hipStream_t s) {
-    Moments* part = (Moments*)ws;
-    double* part_seg = (double*)((char*)ws + sizeof(Moments) * (size_t)C);
-    float* range = (float*)(part_seg + 3 * (size_t)C);
-    float* nonfinite = range + 2;
-    unsigned* hist = (unsigned*)(range + 4);
+// Partial pass over chunks [c0, c1) (any order of disjoint ranges; every chunk exactly once per step).
+TDL_API int tdl_grad_stats_partial(const float* g, float* ref, const int64_t* table, int C, int S, int c0, int c1,
+                                   float beta, void* ws, int ref_valid, hipStream_t s) {
+    if (c0 < 0 || c1 > C || c0 > c1) return (int)hipErrorInvalidValue;
+    if (c1 == c0) return 0;
+    GradWs w = grad_ws(ws, C, S);
+    grad_partial_kernel<<<c1 - c0, 256, 0, s>>>(g, ref, table, c0, ref_valid, beta, w.part, w.part_seg);
+    TDL_LAUNCH_CHECK();
+}
+
+// Segment + summary (+ histogram quantiles) after every chunk's partial has run.
+TDL_API int tdl_grad_stats_final(const float* g, const int64_t* table, int C, float* out, int64_t n, int S, void* ws,
+                                 int ref_valid, int with_quantiles, hipStream_t s) {
+    GradWs w = grad_ws(ws, C, S);
     const int* seg_first = (const int*)(table + 3 * (size_t)C);
-    hipMemsetAsync(nonfinite, 0, sizeof(float), s);
-    grad_partial_kernel<<<C, 256, 0, s>>>(g, ref, table, ref_valid, beta, part, part_seg, nonfinite);
-    grad_final_kernel<<<1, 256, 0, s>>>(part, part_seg, seg_first, C, S, ref_valid, out, range, hist, nonfinite);
+    hipMemsetAsync(w.nonfinite, 0, sizeof(float) * 2, s);
+    grad_segment_kernel<<<(S + 3) / 4, 256, 0, s>>>(w.part, w.part_seg, seg_first, S, ref_valid, out, w.seg,
+                                                    w.nonfinite);
+    grad_summary_kernel<<<1, 256, 0, s>>>(w.seg, S, out, w.range, w.hist, w.nonfinite);
     if (with_quantiles) {
         const int hg = stat_grid(n);
-        hist_kernel<<<hg, 256, 0, s>>>(g, 0, n, range, hist);
-        quantile_kernel<<<1, 64, 0, s>>>(hist, range, out);
+        hist_kernel<<<hg, 256, 0, s>>>(g, 0, n, w.range, w.hist);
+        quantile_kernel<<<1, 256, 0, s>>>(w.hist, w.range, out);
     }
+    TDL_LAUNCH_CHECK();
+}
+
+TDL_API int tdl_grad_stats(const float* g, float* ref, const int64_t* table, int C, float* out, int64_t n, float beta,
+                           int S, void* ws, int ref_valid, int with_quantiles, hipStream_t s) {
+    int rc = tdl_grad_stats_partial(g, ref, table, C, S, 0, C, beta, ws, ref_valid, s);
+    if (rc) return rc;
+    return tdl_grad_stats_final(g, table, C, out, n, S, ws, ref_valid, with_quantiles, s);
+}
+
+// Bare clipping norm (verification off): sum over segments of w_s * ||g_s||^2, deterministic.
+// One block per chunk writes its weighted partial; one block sums them in a fixed order.
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const float* __restrict__ g, const int64_t* __restrict__ chunks,
+                                                            const float* __restrict__ seg_w, double* __restrict__ part) {
+    __shared__ float red[16];
+    const int c = blockIdx.x;
+    const int64_t start = chunks[3 * c + 1], end = chunks[3 * c + 2];
+    const int sgi = (int)chunks[3 * c];
+    float sq = 0.f;
+    int64_t vbeg = (start + 3) & ~(int64_t)3;
+    if (vbeg > end) vbeg = end;
+    const int64_t vend = vbeg + ((end - vbeg) & ~(int64_t)3);
+    for (int64_t i = start + threadIdx.x; i < vbeg; i += blockDim.x) sq += g[i] * g[i];
+    for (int64_t i = vbeg + 4 * (int64_t)threadIdx.x; i < vend; i += 4 * (int64_t)blockDim.x) {
+        const float4 v = *(const float4*)(g + i);
+        sq += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    for (int64_t i = vend + threadIdx.x; i < end; i += blockDim.x) sq += g[i] * g[i];
+    sq = block_sum(sq, red);
+    if (threadIdx.x == 0) part[c] = (double)sq * (double)seg_w[sgi];
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const double* __restrict__ part, int C, float* __restrict__ out) {
+    __shared__ double sh[4];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) v += part[i];
+    v = wave_sum_d(v);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = (float)(sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+TDL_API int tdl_grad_sumsq(const float* g, const int64_t* table, int C, const float* seg_w, double* ws, float* out,
+                           hipStream_t s) {
+    if (C <= 0) return (int)hipErrorInvalidValue;
+    sumsq_partial_kernel<<<C, 256, 0, s>>>(g, table, seg_w, ws);
+    sumsq_final_kernel<<<1, 256, 0, s>>>(ws, C, out);
     TDL_LAUNCH_CHECK();
 }
 
@@ -404,15 +573,27 @@ __device__ float wave_select(const float* v, int n, int r, int lane) {
 }
 
 // robust = 1: baseline over the `window` most recent entries, center = median, scale = 1.4826 * MAD
-//             (robust to the drift of real training and to earlier attacked samples);
+//             (robust to earlier attacked samples);
+// robust = 2: as 1 about a robust linear trend of the window (the drift of real training), with the
+//             scale floored at abs_floor + rel_floor * |center|;
 // robust = 0: reference mean / population std over the whole history window.
+// robust | 4: the decision statistic is the largest per-feature |z| (targeted feature sets) instead
+//             of the mean over features (the reference's 17-feature rule).
+__device__ __forceinline__ float wave_median(const float* v, int n, int lane) {
+    return (n & 1) ? wave_select(v, n, n / 2, lane)
+                   : 0.5f * (wave_select(v, n, n / 2 - 1, lane) + wave_select(v, n, n / 2, lane));
+}
+
 __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, int* __restrict__ state,
                                                      const float* __restrict__ cur, int K, int H, int warmup,
                                                      float z_decision, int window, int exclude_current,
-                                                     int max_quarantine, int robust, float* __restrict__ out) {
+                                                     int max_quarantine, int robust, float rel_floor,
+                                                     float abs_floor, float* __restrict__ out) {
     __shared__ float zs[64];
     __shared__ float col[4][128];
     __shared__ int cnt_sh;
+    const bool agg_max = (robust & 4) != 0;  // decision on the largest |z| instead of the mean
+    robust &= 3;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int count = state[0], head = state[1];
     if (!exclude_current) {  // reference order: append, then baseline over the window incl. current
@@ -433,16 +614,31 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
                 v[j] = ring[(size_t)idx * K + k];
             }
             __builtin_amdgcn_wave_barrier();
-            const float med = (wn & 1) ? wave_select(v, wn, wn / 2, lane)
-                                       : 0.5f * (wave_select(v, wn, wn / 2 - 1, lane) + wave_select(v, wn, wn / 2, lane));
+            float trend0 = 0.f;
+            if (robust == 2 && wn >= 8) {
+                // detrended baseline: a robust line through the medians of the recent and the older
+                // half of the window (slope per step); residuals about it give centre and scale, and
+                // the centre is the line's prediction for the current step.  A gradient statistic
+                // that drifts smoothly as the model learns is then not an outlier; a jump is.
+                const int h = wn / 2;
+                const float mr = wave_median(v, h, lane);
+                const float mo = wave_median(v + h, h, lane);
+                const float slope = (mr - mo) / (float)h;
+                const float tr = -1.f - 0.5f * (float)(h - 1);
+                __builtin_amdgcn_wave_barrier();
+                for (int j = lane; j < wn; j += 64) v[j] -= mr + slope * ((float)(-1 - j) - tr);
+                __builtin_amdgcn_wave_barrier();
+                trend0 = mr + slope * (0.f - tr);
+            }
+            const float med = wave_median(v, wn, lane);
             __builtin_amdgcn_wave_barrier();
             for (int j = lane; j < wn; j += 64) v[j] = fabsf(v[j] - med);
             __builtin_amdgcn_wave_barrier();
-            const float mad = (wn & 1) ? wave_select(v, wn, wn / 2, lane)
-                                       : 0.5f * (wave_select(v, wn, wn / 2 - 1, lane) + wave_select(v, wn, wn / 2, lane));
+            const float mad = wave_median(v, wn, lane);
             __builtin_amdgcn_wave_barrier();
-            center = med;
+            center = trend0 + med;
             scale = 1.4826f * mad;
+            if (robust == 2 && scale > 0.f) scale = fmaxf(scale, abs_floor + rel_floor * fabsf(center));
         } else {
             float s = 0.f;
             for (int h = lane; h < count; h += 64) s += ring[(size_t)h * K + k];
@@ -466,11 +662,11 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        float sum = 0.f;
+        float sum = 0.f, mx = 0.f;
         int nv = 0;
         for (int k = 0; k < K; ++k)
-            if (zs[k] >= 0.f) { sum += zs[k]; ++nv; }
-        const float mz = nv ? sum / nv : 0.f;
+            if (zs[k] >= 0.f) { sum += zs[k]; mx = fmaxf(mx, zs[k]); ++nv; }
+        const float mz = agg_max ? mx : (nv ? sum / nv : 0.f);
         const bool flag = ready && mz > z_decision;
         out[0] = flag ? 1.f : 0.f;
         out[1] = mz;
@@ -502,11 +698,11 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
 }
 
 TDL_API int tdl_zscore_detect(float* ring, int* state, const float* cur, int K, int H, int warmup, float z_decision,
-                              int window, int exclude_current, int max_quarantine, int robust, float* out,
-                              hipStream_t s) {
-    if (K > 64 || (robust && window > 128)) return (int)hipErrorInvalidValue;
+                              int window, int exclude_current, int max_quarantine, int robust, float rel_floor,
+                              float abs_floor, float* out, hipStream_t s) {
+    if (K > 64 || ((robust & 3) && window > 128)) return (int)hipErrorInvalidValue;
     zscore_kernel<<<1, 256, 0, s>>>(ring, state, cur, K, H, warmup, z_decision, window, exclude_current,
-                                    max_quarantine, robust, out);
+                                    max_quarantine, robust, rel_floor, abs_floor, out);
     TDL_LAUNCH_CHECK();
 }
 

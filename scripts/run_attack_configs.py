@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""BASELINE.json attack configurations 3 / 4 / 5, end to end in local mode (every stage on one GPU).
+
+    3  GPT-2-medium, 8 stages, gradient poisoning on one stage -> detection -> re-shard to 7
+    4  ResNet-50,    8 stages, parameter perturbation on one stage -> detection -> reassignment
+    5  GPT-2-medium, 8 stages, 2 Byzantine (activation-tampering) stages -> re-shard to 6
+
+Training data is the learnable synthetic stream (Markov tokens / class-conditional images), so
+the loss falls while the attack runs.  Per config one JSON record: detection precision / recall /
+F1 and time-to-detect (attacker ground truth vs the engine's per-stage verdicts), the re-shard
+wall time (ms, migration of fp32 master + AdamW moments), the plan before / after, final trust,
+and the loss curve across the re-shard.  The reference describes these configs
+(experiment_runner.py:84-112, README.md:85-92) but never runs a re-shard.
+
+    python scripts/run_attack_configs.py --configs 3,4,5 --out profiles/r2_attack_configs.jsonl
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from trustworthy_dl.attacks.adversarial_attacks import AdversarialAttacker, AttackConfig  # noqa: E402
+from trustworthy_dl.models import get_model  # noqa: E402
+from trustworthy_dl.parallel.flat import AdamWConfig  # noqa: E402
+from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine  # noqa: E402
+from trustworthy_dl.utils.data_loader import MarkovLanguageModeling, SyntheticImages  # noqa: E402
+from trustworthy_dl.utils.metrics import MetricsCollector  # noqa: E402
+
+CONFIGS = {
+    3: dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="scale",
+                                             gradient_scale=10.0), targets=[3], lr=1e-4),
+    4: dict(model="resnet50", attack=dict(attack_types=["model_poisoning"], intensity=0.05), targets=[4], lr=3e-4),
+    5: dict(model="gpt2-medium", attack=dict(attack_types=["byzantine"], intensity=0.5), targets=[2, 5], lr=1e-4),
+}
+
+
+def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, seq_len: int, p_attack: float,
+        small: bool = False):
+    c = dict(CONFIGS[cfg_id])
+    if small:   # CPU smoke: same flow on the tiny models
+        c["model"] = {"gpt2-medium": "gpt2-tiny", "resnet50": "resnet32"}[c["model"]]
+    att = AdversarialAttacker(AttackConfig(target_nodes=c["targets"], start_step=start, probability=p_attack, seed=3,
+                                           **c["attack"]))
+    att.activate_attacks()
+    gpt = c["model"].startswith("gpt2")
+    img = 32 if c["model"] == "resnet32" else 224
+    ncls = 10 if img == 32 else 1000
+    model = get_model(c["model"], seq_len=seq_len, seed=5) if gpt else \
+        (get_model(c["model"], seed=5) if img == 32 else get_model(c["model"], image_size=img, seed=5))
+    extra = {"seq_len": seq_len} if gpt else {}
+    cfg = EngineConfig(num_nodes=8, micro_batches=max(1, batch // mbs), device=device,
+                       adamw=AdamWConfig(lr=c["lr"], weight_decay=0.01, max_grad_norm=1.0, warmup_steps=20),
+                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=True, **extra)
+    eng = PipelineEngine(model, cfg, attacker=att, metrics=MetricsCollector())
+    del model
+    plan0 = eng.plan.describe()
+    data = (MarkovLanguageModeling(batch, seq_len, 8192, num_batches=steps, seed=1) if gpt else
+            SyntheticImages(batch, img, ncls, num_batches=steps, seed=1))
+    t0 = time.perf_counter()
+    for b in data:
+        eng.train_step(b)
+    eng.flush()
+    if device.startswith("cuda"):
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    m = att.detection_metrics()
+    losses = [(r["step"], round(r["loss"], 4)) for r in eng.metrics.batch_metrics if r.get("loss") is not None]
+    rs = eng.reassignment_history
+    first_attack = min(att.first_attack_step.values()) if att.first_attack_step else None
+    rec = {
+        "config": cfg_id, "model": c["model"], "attack": c["attack"], "targets": c["targets"],
+        "p_attack": p_attack, "attack_start_step": start, "first_attack_step": first_attack, "steps": steps,
+        "batch": batch, "micro_batch": mbs, "seq_len": seq_len if gpt else None, "device": device,
+        "data": "markov tokens (order 1, branching 4, 8192 ids)" if gpt else "class-conditional synthetic images",
+        "lr": c["lr"], "lr_warmup_steps": 20,
+        "detection": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in m.items()
+                      if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
+        "injections": len(att.injections),
+        "reshards": [{"step": r["step"], "from_nodes": r["from_nodes"], "to_nodes": r["to_nodes"],
+                      "migration_ms": round(1000 * r["migration_time"], 2),
+                      "estimated_ms": round(1000 * r["estimated_migration_time"], 2),
+                      "moved_params": r["moved_params"], "restored_from_shadow": r.get("restored_from_shadow"),
+                      "plan": r["plan"]} for r in rs],
+        "plan_before": plan0, "plan_after": eng.plan.describe(), "num_stages_after": eng.plan.num_stages,
+        "final_trust": [round(eng.trust.get_trust_score(n), 3) for n in range(8)],
+        "final_status": [eng.trust.get_node_status(n).value for n in range(8)],
+        "loss_curve": losses, "wall_s": round(wall, 1),
+    }
+    return rec
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="3,4,5")
+    ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--start", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--mbs", type=int, default=2)
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--p-attack", type=float, default=0.3)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--small", action="store_true", help="tiny models (CPU smoke of the same flow)")
+    args = ap.parse_args()
+    for cid in [int(x) for x in args.configs.split(",")]:
+        rec = run(cid, args.device, args.steps, args.start, args.batch, args.mbs, args.seq_len, args.p_attack,
+                  args.small)
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(line + "\n")
+        if args.device.startswith("cuda"):
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

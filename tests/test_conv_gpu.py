@@ -143,3 +143,32 @@ def test_resnet_engine_step_native():
         if dev.startswith("cuda"):
             assert eng.dtype == torch.bfloat16
     assert losses["cuda:0"] == pytest.approx(losses["cpu"], rel=5e-2)
+
+
+def test_vgg16_224_gpu_matches_cpu_fp32():
+    """VGG-16 (BN) at ImageNet shape, incl. the 25088->4096->4096->1000 classifier: the GPU bf16
+    engine (native conv kernels) follows the CPU fp32 engine step by step and the loss stays sane
+    (the r1 bench's loss of 99 was AdamW lr 1e-3 diverging on CPU fp32 as well:
+    profiles/r2_vgg16_lr_cpu_fp32.json)."""
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.flat import AdamWConfig
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    from trustworthy_dl.utils.metrics import MetricsCollector
+    g = torch.Generator().manual_seed(0)
+    batches = [{"input": torch.randn(4, 3, 224, 224, generator=g), "target": torch.randint(0, 1000, (4,), generator=g)}
+               for _ in range(2)]
+    traj = {}
+    for dev in ("cpu", "cuda:0"):
+        m = get_model("vgg16", num_classes=1000, image_size=224, seed=1)
+        eng = PipelineEngine(m, EngineConfig(num_nodes=1, micro_batches=1, device=dev, reassign=False,
+                                             adamw=AdamWConfig(lr=1e-4, weight_decay=1e-4, max_grad_norm=1.0)),
+                             metrics=MetricsCollector())
+        for i in range(3):
+            eng.train_step(batches[i % 2])
+        eng.flush()
+        traj[dev] = [r["loss"] for r in eng.metrics.batch_metrics]
+    cpu, gpu = traj["cpu"], traj["cuda:0"]
+    assert gpu[0] == pytest.approx(cpu[0], rel=2e-2)       # same forward at init
+    assert gpu[1] == pytest.approx(cpu[1], rel=1e-1)       # same first update
+    assert all(l < 9.0 for l in gpu), gpu                   # no divergence (ln 1000 = 6.9)
+    assert gpu[-1] < gpu[0]

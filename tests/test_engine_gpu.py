@@ -41,8 +41,8 @@ def test_native_library_loaded():
 
 
 def test_serialized_streams_match_overlapped():
-    _, l0, d0, w0 = _run(serialize_streams=False)
-    _, l1, d1, w1 = _run(serialize_streams=True)
+    _, l0, d0, w0 = _run(serialize_streams=False, output_check="first")
+    _, l1, d1, w1 = _run(serialize_streams=True, output_check="first")
     assert l0 == pytest.approx(l1, rel=1e-6)
     assert torch.allclose(d0, d1, rtol=1e-5, atol=1e-6), (d0 - d1).abs().max()
     # weights: fp32 atomics in the embedding / column-sum backward make the last bits run-order dependent
@@ -65,3 +65,28 @@ def test_phase_tracer_gpu():
     for k in ("fwd", "bwd_input", "verify", "optimizer", "step"):
         assert s.get(k, 0.0) > 0.0, (k, s)
     assert s["step"] >= s["fwd"] + s["optimizer"]
+
+
+def test_early_grad_stats_match_final_pass():
+    """Per-layer gradient statistics launched from the backward (side stream, overlapped) give the
+    digests of the single pass after the backward."""
+    _, l0, d0, w0 = _run(early_grad_stats=True, output_check="first")
+    _, l1, d1, w1 = _run(early_grad_stats=False, output_check="first")
+    assert l0 == pytest.approx(l1, rel=1e-6)
+    assert torch.allclose(d0, d1, rtol=1e-5, atol=1e-6), (d0 - d1).abs().max()
+
+
+def test_early_grad_stats_actually_split():
+    """The hooks fire: every stage's partial pass ran in more than one piece before finish."""
+    eng, _, _, _ = _run(steps=1, early_grad_stats=True, output_check="first")
+    counts = []
+    for st in eng.stages.values():
+        gs = st.verifier.grad_stats
+        orig = gs.partial
+        pieces = []
+        gs.partial = lambda g, c0, c1, stream=None, orig=orig, pieces=pieces: (pieces.append((c0, c1)),
+                                                                                 orig(g, c0, c1, stream))
+        counts.append(pieces)
+    eng.train_step(_batches(1, seed=5)[0])
+    eng.flush()
+    assert all(len(p) >= 2 for p in counts), counts

@@ -45,6 +45,7 @@ def _batches(n, bs=8, seed=0):
 
 def _engine(nodes=3, attacker=None, reassign=True, **kw):
     m = get_model("gpt2-tiny", seq_len=32, seed=0, vocab_size=1024)
+    kw.setdefault("verifier", {"warmup": 10})   # short detector warm-up: the attack scenarios start at step 12-25
     cfg = EngineConfig(num_nodes=nodes, micro_batches=2, seq_len=32, device="cpu",
                        adamw=AdamWConfig(lr=1e-3), reassign=reassign, **kw)
     return PipelineEngine(m, cfg, TrustManager(nodes), attacker=attacker, metrics=MetricsCollector(),

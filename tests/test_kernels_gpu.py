@@ -100,6 +100,27 @@ def test_flash_attention(T, H):
     assert _rel(qkv.grad, x.grad) < 3e-2
 
 
+def test_flash_attention_production_shape():
+    """The benched GPT-2-medium shape (H = 16, T = 1024, causal) at B = 4 against fp32 SDPA, per
+    gradient slice (dQ, dK, dV) with a relative Frobenius tolerance."""
+    from trustworthy_dl.ops import causal_attention
+    torch.manual_seed(1)
+    B, T, H, D = 4, 1024, 16, 64
+    qkv = (torch.randn(B, T, 3 * H * D, device=DEV)).bfloat16().requires_grad_(True)
+    o = causal_attention(qkv, H, True)
+    g = torch.randn_like(o)
+    o.backward(g)
+    x = qkv.detach().float().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, H * D)
+    ref.backward(g.float())
+    fro = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
+    assert fro(o, ref) < 1e-2
+    gq, gr = qkv.grad.view(B, T, 3, H * D), x.grad.view(B, T, 3, H * D)
+    for i, name in enumerate("qkv"):
+        assert fro(gq[:, :, i], gr[:, :, i]) < 2e-2, name
+
+
 def test_attention_rescale_branch():
     """Force the online-softmax running max to jump inside a row (rule 26)."""
     from trustworthy_dl.ops import causal_attention
@@ -222,14 +243,40 @@ def test_grad_stats_matches_cpu():
         assert torch.allclose(a[18:], b[18:], rtol=1e-3, atol=1e-4)
 
 
-def test_zscore_matches_cpu():
+def test_grad_stats_in_pieces_match_one_pass():
+    """Partial passes over arbitrary chunk ranges (the per-layer overlap path) + the final stages
+    give the single pass's result; the bare clipping sum of squares matches torch."""
+    from trustworthy_dl.ops.stats import CHUNK, FlatGradStats, FlatSumSq
+    sizes = [3 * CHUNK + 17, 5, 2 * CHUNK, 70000, 1]
+    n = sum(sizes)
+    a, b = FlatGradStats(sizes, DEV), FlatGradStats(sizes, DEV)
+    for step in range(3):
+        g = torch.randn(n, device=DEV)
+        g[123] = float("inf") if step == 2 else g[123]
+        ra = a.compute(g).clone()
+        lo, hi = b.chunk_range_of(1, 4)
+        b.partial(g, lo, hi)               # segments 1..3 early, the rest in compute()
+        rb = b.compute(g).clone()
+        assert torch.allclose(ra, rb, rtol=1e-6, atol=1e-7, equal_nan=True), (step, ra, rb)
+    w = torch.tensor([1.0, 0.0, 1.0, 0.5, 1.0], device=DEV)
+    g = torch.randn(n, device=DEV)
+    sq = FlatSumSq(sizes, DEV).compute(g, w)
+    ref = sum(float(wi) * float((x * x).sum()) for wi, x in zip(w, torch.split(g, sizes)))
+    assert float(sq) == pytest.approx(ref, rel=1e-5)
+
+
+@pytest.mark.parametrize("kw", [{}, {"robust": "detrend", "window": 32},
+                                {"robust": "detrend", "agg": "max", "abs_floor": 0.02, "rel_floor": 0.0,
+                                 "z_decision": 8.0, "max_quarantine": 5}])
+def test_zscore_matches_cpu(kw):
     from trustworthy_dl.ops.stats import DeviceZScore
     K = 17
-    dg = DeviceZScore(K, DEV, history=50, warmup=10)
-    dc = DeviceZScore(K, "cpu", history=50, warmup=10)
+    dg = DeviceZScore(K, DEV, history=50, warmup=10, **kw)
+    dc = DeviceZScore(K, "cpu", history=50, warmup=10, **kw)
     g = torch.Generator().manual_seed(1)
+    drift = torch.linspace(0, 3, K)
     for step in range(80):
-        cur = torch.randn(K, generator=g)
+        cur = torch.randn(K, generator=g) + drift * step / 20.0
         if step in (30, 31, 60):
             cur = cur * 20
         a = dg.observe(cur.to(DEV)).cpu()

@@ -96,7 +96,11 @@ _SIGNATURES = {
     # stats.hip
     "tdl_tensor_stats": [_P, _I, _L, _P, _P, _I, _P],
     "tdl_grad_stats": [_P, _P, _P, _I, _P, _L, _F, _I, _P, _I, _I, _P],
-    "tdl_zscore_detect": [_P, _P, _P, _I, _I, _I, _F, _I, _I, _I, _I, _P, _P],
+    "tdl_grad_stats_ws_bytes": [_I, _I],
+    "tdl_grad_stats_partial": [_P, _P, _P, _I, _I, _I, _I, _F, _P, _I, _P],
+    "tdl_grad_stats_final": [_P, _P, _I, _P, _L, _I, _P, _I, _I, _P],
+    "tdl_grad_sumsq": [_P, _P, _I, _P, _P, _P, _P],
+    "tdl_zscore_detect": [_P, _P, _P, _I, _I, _I, _F, _I, _I, _I, _I, _F, _F, _P, _P],
     "tdl_trust_update": [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _P],
     "tdl_kl_div_softmax": [_P, _P, _I, _I, _P, _P],
     "tdl_stats_workspace_bytes": [],

@@ -7,7 +7,7 @@ i.e. (max - min) / 2048); the CPU path is exact (numpy definitions).
 from __future__ import annotations
 
 import math
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -19,6 +19,7 @@ N_TENSOR_STATS = 12
 N_GRAD_STATS = 17
 NHIST = 2048
 CHUNK = 1 << 15
+REF_STRIDE = 8       # the EMA reference gradient is kept on one chunk in REF_STRIDE (csrc/stats.hip)
 
 _ws_cache = {}
 
@@ -86,7 +87,12 @@ def build_chunk_table(sizes: Sequence[int], device) -> torch.Tensor:
 
 
 class FlatGradStats:
-    """Segmented statistics over a stage's flat fp32 gradient (one segment per parameter)."""
+    """Segmented statistics over a stage's flat fp32 gradient (one segment per parameter).
+
+    ``compute`` runs the whole pass.  The engine can instead run the per-chunk partial pass in
+    pieces while the backward is still going (``partial(lo, hi)`` over chunk ranges, on the
+    verifier's side stream, as each layer's gradient becomes final: ``chunk_range_of``), and then
+    ``compute`` only adds the segment / summary / quantile stages."""
 
     def __init__(self, sizes: Sequence[int], device, ref_beta: float = 0.9, track_reference: bool = True):
         self.sizes = list(sizes)
@@ -97,46 +103,130 @@ class FlatGradStats:
         self.ref = torch.zeros(self.n, dtype=torch.float32, device=self.device) if track_reference else None
         self.ref_valid = False
         self.out = torch.zeros(18 + 2 * self.S, dtype=torch.float32, device=self.device)
+        # chunk ranges per segment (CPU mirror of the device table): first[s] .. first[s+1]
+        self.seg_first = [0]
+        for n in self.sizes:
+            self.seg_first.append(self.seg_first[-1] + (n + CHUNK - 1) // CHUNK)
+        self._done = 0               # chunks whose partial already ran this step (prefix-free count)
+        self._ranges: List[Tuple[int, int]] = []
         if self.device.type == "cuda":
             self.table, self.C = build_chunk_table(self.sizes, self.device)
-            nbytes = 64 * self.C + 24 * self.C + 16 + 4 * NHIST + 64
+            nbytes = int(_lib.lib().tdl_grad_stats_ws_bytes(self.C, self.S)) + 64
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        else:
+            self.C = self.seg_first[-1]
+
+    def chunk_range_of(self, seg_lo: int, seg_hi: int) -> Tuple[int, int]:
+        return self.seg_first[seg_lo], self.seg_first[seg_hi]
+
+    def partial(self, flat_grad: torch.Tensor, c0: int, c1: int, stream=None) -> None:
+        """Partial pass over chunks [c0, c1) (each chunk at most once per step)."""
+        if not flat_grad.is_cuda or c1 <= c0:
+            return
+        _lib.call("tdl_grad_stats_partial", ptr(flat_grad), ptr(self.ref), ptr(self.table), self.C, self.S, c0, c1,
+                  self.ref_beta, ptr(self.ws), int(self.ref_valid),
+                  stream.cuda_stream if stream is not None else stream_ptr(flat_grad.device))
+        self._ranges.append((c0, c1))
+        self._done += c1 - c0
 
     def compute(self, flat_grad: torch.Tensor, with_quantiles: bool = True) -> torch.Tensor:
         """Returns the device vector [18 + 2S]: GRAD_STATS(17), nonfinite, norms[S], cos[S]."""
         if flat_grad.is_cuda:
-            _lib.call("tdl_grad_stats", ptr(flat_grad), ptr(self.ref), ptr(self.table), self.C, ptr(self.out),
-                      self.n, self.ref_beta, self.S, ptr(self.ws), int(self.ref_valid), int(with_quantiles),
-                      stream_ptr(flat_grad.device))
+            dev = flat_grad.device
+            if self._done == 0:
+                _lib.call("tdl_grad_stats", ptr(flat_grad), ptr(self.ref), ptr(self.table), self.C, ptr(self.out),
+                          self.n, self.ref_beta, self.S, ptr(self.ws), int(self.ref_valid), int(with_quantiles),
+                          stream_ptr(dev))
+            else:
+                # the chunks no early partial covered (e.g. tied weights reduced after the backward)
+                covered = sorted(self._ranges)
+                pos = 0
+                for lo, hi in covered + [(self.C, self.C)]:
+                    if lo > pos:
+                        self.partial(flat_grad, pos, lo)
+                    pos = max(pos, hi)
+                if self._done != self.C:
+                    raise RuntimeError(f"grad stats: {self._done} chunk partials for {self.C} chunks")
+                _lib.call("tdl_grad_stats_final", ptr(flat_grad), ptr(self.table), self.C, ptr(self.out), self.n,
+                          self.S, ptr(self.ws), int(self.ref_valid), int(with_quantiles), stream_ptr(dev))
         else:
             self.out.copy_(self._cpu(flat_grad))
+        self._done = 0
+        self._ranges = []
         if self.ref is not None:
             self.ref_valid = True
         return self.out
 
+    def _tracked_mask(self) -> torch.Tensor:
+        """Elements whose EMA reference is kept (chunks c with c % REF_STRIDE == 0, as the kernel)."""
+        m = getattr(self, "_tmask", None)
+        if m is None:
+            m = torch.zeros(self.n, dtype=torch.bool)
+            off, c = 0, 0
+            for n in self.sizes:
+                st = off
+                while st < off + n:
+                    en = min(st + CHUNK, off + n)
+                    if c % REF_STRIDE == 0:
+                        m[st:en] = True
+                    c += 1
+                    st = en
+                off += n
+            self._tmask = m
+        return m
+
     def _cpu(self, g: torch.Tensor) -> torch.Tensor:
         st = _cpu_stats(g)
-        segs = torch.split(g.detach().float(), self.sizes)
+        gf = g.detach().float()
+        segs = torch.split(gf, self.sizes)
         norms = torch.stack([s.norm() for s in segs]) if segs else torch.zeros(0)
+        tm = self._tracked_mask()
         if self.ref is not None and self.ref_valid:
-            rsegs = torch.split(self.ref, self.sizes)
             cos = []
-            for a, b in zip(segs, rsegs):
-                den = float(a.norm() * b.norm())
-                cos.append(float((a * b).sum()) / den if den > 0 else 1.0)
+            for a, r, t in zip(segs, torch.split(self.ref, self.sizes), torch.split(tm, self.sizes)):
+                at, rt = a[t], r[t]
+                den = float(at.norm() * rt.norm())
+                cos.append(float((at * rt).sum()) / den if den > 0 else 2.0)
             cos = torch.tensor(cos)
         else:
             cos = torch.ones(self.S)
         if self.ref is not None:
-            gg = torch.nan_to_num(g.detach().float(), nan=0.0, posinf=0.0, neginf=0.0)
+            gg = torch.nan_to_num(gf, nan=0.0, posinf=0.0, neginf=0.0)
             if self.ref_valid:
-                self.ref.mul_(self.ref_beta).add_(gg, alpha=1 - self.ref_beta)
+                self.ref[tm] = self.ref[tm] * self.ref_beta + gg[tm] * (1 - self.ref_beta)
             else:
-                self.ref.copy_(gg)
+                self.ref[tm] = gg[tm]
+        valid = cos <= 1.5
+        cmean = float(cos[valid].mean()) if valid.any() else 1.0
         extra = torch.tensor([float(self.S), float(norms.mean()) if self.S else 0.0,
                               float(norms.std(unbiased=False)) if self.S else 0.0,
-                              float(norms.max()) if self.S else 0.0, float(cos.mean()) if self.S else 1.0])
+                              float(norms.max()) if self.S else 0.0, cmean if self.S else 1.0])
         return torch.cat([st[:12], extra, st[12:13], norms.float(), cos.float()])
+
+
+class FlatSumSq:
+    """Bare clipping norm for runs with verification off: sum_s w_s ||g_s||^2 over the flat
+    gradient's segments (one read of the gradient, no moments / reference / quantiles)."""
+
+    def __init__(self, sizes: Sequence[int], device):
+        self.sizes = list(sizes)
+        self.device = torch.device(device)
+        self.out = torch.zeros(1, dtype=torch.float32, device=self.device)
+        if self.device.type == "cuda" and self.sizes:
+            self.table, self.C = build_chunk_table(self.sizes, self.device)
+            self.ws = torch.empty(max(1, self.C), dtype=torch.float64, device=self.device)
+
+    def compute(self, flat_grad: torch.Tensor, seg_w: torch.Tensor) -> torch.Tensor:
+        if not self.sizes:
+            self.out.zero_()
+        elif flat_grad.is_cuda:
+            _lib.call("tdl_grad_sumsq", ptr(flat_grad), ptr(self.table), self.C, ptr(seg_w), ptr(self.ws),
+                      ptr(self.out), stream_ptr(flat_grad.device))
+        else:
+            segs = torch.split(flat_grad.detach().float(), self.sizes)
+            sq = torch.stack([(x * x).sum() for x in segs])
+            self.out.copy_((sq * seg_w[:len(self.sizes)].to(sq.device)).sum().reshape(1))
+        return self.out
 
 
 def grad_stats(grads: Sequence[torch.Tensor], reference: Optional[Sequence[torch.Tensor]] = None,
@@ -168,11 +258,20 @@ class DeviceZScore:
     """Device ring-buffer baseline + z-score decision for one monitored signal (K4)."""
 
     def __init__(self, k: int, device, history: int = 1000, warmup: int = 10, z_decision: float = 2.5,
-                 exclude_current: bool = True, max_quarantine: int = 50, robust: bool = True, window: int = 100):
-        """``robust``: median / 1.4826*MAD over the ``window`` most recent entries (default);
-        otherwise the reference's mean / population std over the whole ``history``."""
+                 exclude_current: bool = True, max_quarantine: int = 50, robust=True, window: int = 100,
+                 rel_floor: float = 0.02, agg: str = "mean", abs_floor: float = 0.0):
+        """``robust``: 1/True = median / 1.4826*MAD over the ``window`` most recent entries; 2 or
+        "detrend" = the same about a robust linear trend of the window (the drift of learning:
+        line through the medians of the window's recent and older halves), scale floored at
+        ``rel_floor`` * |centre|; 0/False = the reference's mean / population std over the whole
+        ``history``.  ``agg``: "mean" (the reference's rule: mean |z| over the features) or "max"
+        (largest |z|: for short, targeted feature vectors)."""
         self.k, self.history, self.warmup = k, history, warmup
-        self.robust, self.window = bool(robust), int(min(window, 128))
+        self.agg_max = agg == "max"
+        self.robust = 2 if robust == "detrend" else int(robust)
+        self.window = int(min(window, 128))
+        self.rel_floor = float(rel_floor)
+        self.abs_floor = float(abs_floor)
         self.z_decision = z_decision
         self.exclude_current = exclude_current
         self.max_quarantine = max_quarantine
@@ -187,7 +286,8 @@ class DeviceZScore:
         if self.device.type == "cuda":
             _lib.call("tdl_zscore_detect", ptr(self.ring), ptr(self.state), ptr(cur), self.k, self.history,
                       self.warmup, self.z_decision, self.window, int(self.exclude_current), self.max_quarantine,
-                      int(self.robust), ptr(self.out), stream_ptr(self.device))
+                      self.robust | (4 if self.agg_max else 0), self.rel_floor, self.abs_floor, ptr(self.out),
+                      stream_ptr(self.device))
         else:
             self._cpu(cur)
         return self.out
@@ -208,9 +308,21 @@ class DeviceZScore:
             if self.robust:
                 wn = min(count, self.window)
                 idx = [(head - 1 - j) % H for j in range(wn)]
-                hist = self.ring[idx]
-                mean = _lower_upper_median(hist)
-                sd = 1.4826 * _lower_upper_median((hist - mean).abs())
+                hist = self.ring[idx].clone()
+                trend0 = torch.zeros(self.k)
+                if self.robust == 2 and wn >= 8:
+                    h = wn // 2
+                    mr, mo = _lower_upper_median(hist[:h]), _lower_upper_median(hist[h:2 * h])
+                    slope = (mr - mo) / h
+                    tr = -1.0 - 0.5 * (h - 1)
+                    tau = torch.tensor([-1.0 - j for j in range(wn)])[:, None]
+                    hist = hist - (mr + slope * (tau - tr))
+                    trend0 = mr + slope * (0.0 - tr)
+                med = _lower_upper_median(hist)
+                mean = trend0 + med
+                sd = 1.4826 * _lower_upper_median((hist - med).abs())
+                if self.robust == 2:
+                    sd = torch.where(sd > 0, torch.maximum(sd, self.abs_floor + self.rel_floor * mean.abs()), sd)
             else:
                 hist = self.ring[:count]
                 mean = hist.mean(0)
@@ -220,7 +332,10 @@ class DeviceZScore:
                     c = float(cur[j])
                     zs[j] = abs((c - float(mean[j])) / float(sd[j])) if math.isfinite(c) else 1e6
         valid = zs >= 0
-        mz = float(zs[valid].mean()) if valid.any() else 0.0
+        if self.agg_max:
+            mz = float(zs[valid].max()) if valid.any() else 0.0
+        else:
+            mz = float(zs[valid].mean()) if valid.any() else 0.0
         flag = ready and mz > self.z_decision
         if self.exclude_current:
             if flag and qrun < self.max_quarantine:

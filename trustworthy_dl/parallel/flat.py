@@ -41,6 +41,12 @@ class AdamWConfig:
     eps: float = 1e-8
     weight_decay: float = 0.01
     max_grad_norm: float = 0.0  # 0 disables clipping
+    warmup_steps: int = 0       # linear learning-rate warm-up over this many optimizer steps
+
+    def lr_at(self, step: int) -> float:
+        if self.warmup_steps > 0 and step < self.warmup_steps:
+            return self.lr * step / self.warmup_steps
+        return self.lr
 
 
 class FlatParams:
@@ -100,6 +106,7 @@ class FlatParams:
         t = self.step_count
         b1, b2 = cfg.betas
         bc1, bc2 = 1.0 - b1 ** t, 1.0 - b2 ** t
+        lr = cfg.lr_at(t)
         groups = [(0, self.decay_numel, cfg.weight_decay), (self.decay_numel, self.numel, 0.0)]
         if self.device.type == "cuda":
             for lo, hi, wd in groups:
@@ -108,7 +115,7 @@ class FlatParams:
                     continue
                 _lib.call("tdl_adamw_flat", ptr(self.master[lo:]), ptr(self.exp_avg[lo:]), ptr(self.exp_avg_sq[lo:]),
                           ptr(self.grad[lo:]), ptr(None if self.data is self.master else self.data[lo:]),
-                          n, cfg.lr, b1, b2, cfg.eps, wd, bc1, bc2,
+                          n, lr, b1, b2, cfg.eps, wd, bc1, bc2,
                           ptr(ctrl), int(zero_grad), stream_ptr(self.device))
             bump_weight_generation()   # compute weights rewritten in place: forward-layout copies are stale
             return
@@ -122,8 +129,8 @@ class FlatParams:
                 m, v, p = self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], self.master[lo:hi]
                 m.mul_(b1).add_(g, alpha=1 - b1)
                 v.mul_(b2).addcmul_(g, g, value=1 - b2)
-                p.mul_(1 - cfg.lr * wd)
-                p.addcdiv_(m, (v.sqrt() / math.sqrt(bc2)).add_(cfg.eps), value=-cfg.lr / bc1)
+                p.mul_(1 - lr * wd)
+                p.addcdiv_(m, (v.sqrt() / math.sqrt(bc2)).add_(cfg.eps), value=-lr / bc1)
             if self.data is not self.master:
                 self.data.copy_(self.master)
         if zero_grad:

@@ -65,7 +65,11 @@ class EngineConfig:
     reassign: bool = True
     max_reassignment_attempts: int = 3
     min_stages: int = 1
-    output_check: str = "first"          # which micro-batch output is monitored: first|none
+    output_check: str = "random"         # which micro-batch output is monitored each step: "random" (a
+                                         # per-step choice from a private seeded RNG, so an attacker
+                                         # cannot predict which output is inspected) | "first" | "none"
+    early_grad_stats: bool = True        # start each layer's gradient statistics on the side stream
+                                         # as soon as its last-micro-batch backward is done
     compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
     defer_wgrad: bool = True             # B/W split: weight grads run after dx is posted upstream
     data_parallel: int = 1               # pipeline replicas (distributed): world = stages x replicas
@@ -76,6 +80,12 @@ class EngineConfig:
     shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
                                          # (0 = off); a compromised stage is restored from it, not from itself
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
+    global_event_fraction: float = 0.5   # gradient anomalies on >= this fraction of a replica's stages (>= 3
+                                         # stages) in one step = a pipeline-wide event (a loss spike of real
+                                         # training), not a Byzantine stage: the step's update is skipped, nobody
+                                         # is blamed, and blame stays off for ``global_event_grace`` steps while
+                                         # the detector baselines re-settle
+    global_event_grace: int = 8
     pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
     layer_granularity: str = "auto"      # "block" | "half" (GPT-2 attention / MLP halves as pipeline
                                          # units) | "auto": half when it lowers the slowest stage
@@ -142,6 +152,9 @@ class PipelineEngine:
         self._host_metrics: Dict[int, List[float]] = {}
         self._comm_wait = 0.0
         self._step_time = 0.0
+        # private per-process RNG for the monitored micro-batch (not derived from the data seed)
+        self._mon_rng = __import__("random").Random(int.from_bytes(os.urandom(8), "little"))
+        self._mon_idx = 0
 
         if cfg.device == "auto":
             if torch.cuda.is_available():
@@ -237,7 +250,29 @@ class PipelineEngine:
                        self._verifier_kwargs(), layers=layers)
             self.stages[node] = st
         self._set_clip_exclusions()
+        self._set_early_stats()
         self._build_comm()
+
+    def _set_early_stats(self):
+        """Per-layer gradient-statistics triggers (verification overlapped with the backward).
+        Tied weights are reduced across stages after the backward and simulated gradient attacks
+        rewrite the flat gradient after it: both stay with the final pass."""
+        if not self.cfg.early_grad_stats or (self.attacker is not None and hasattr(self.attacker, "on_gradients")):
+            return
+        # only where every parameter gradient is written by the layer's own backward into
+        # main_grad (the GPT-2 fused ops): a torch module's .grad is folded in by a separate
+        # accumulate hook whose order against the input-gradient hook is not fixed
+        if getattr(self.model, "family", "") != "gpt2" or self.device.type != "cuda":
+            return
+        tied = set()
+        for grp in self.ties:
+            for node, st in self.stages.items():
+                for li, attr in grp:
+                    prm = st.local_param(li, attr)
+                    if prm is not None:
+                        tied.add(id(prm))
+        for st in self.stages.values():
+            st.set_early_stats(tied)
 
     def _set_clip_exclusions(self):
         """Count every tied weight once in the global clipping norm: the stage owning the first
@@ -326,6 +361,11 @@ class PipelineEngine:
         self.t_weights = torch.tensor(self.trust.weights_vector(), dtype=torch.float32, device=dev)
         self.t_recovery = torch.full((N,), self.trust.recovery_rate, dtype=torch.float32, device=dev)
         self.t_flagrun = torch.zeros(N, dtype=torch.int32, device=dev)
+        # per replica: steps left in the grace window after a pipeline-wide anomaly
+        self.t_grace = torch.zeros(max(1, self.dp), dtype=torch.float32, device=dev)
+        # per node: weights failed the integrity check and have not been restored since (their
+        # downstream output anomalies are echoes of that, not new Byzantine stages)
+        self.t_taint = torch.zeros(N, dtype=torch.float32, device=dev)
 
     # ================================================================== helpers
     def my_stage(self) -> Optional[Stage]:
@@ -361,6 +401,8 @@ class PipelineEngine:
             inp, tgt = inp.chunk(self.dp, 0)[self.replica], tgt.chunk(self.dp, 0)[self.replica]
         inputs = split_micro(inp, M)
         targets = split_micro(tgt, M)
+        oc = self.cfg.output_check
+        self._mon_idx = -1 if oc == "none" else (self._mon_rng.randrange(M) if oc == "random" else 0)
         if self.distributed:
             loss = self._run_1f1b(inputs, targets, truth)
         else:
@@ -421,14 +463,15 @@ class PipelineEngine:
                 st = self.stages[node]
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
-                obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
+                watch = i == self._mon_idx
+                obs = st.output_observer() if watch else None
                 with self.tracer.phase("fwd"):
-                    y, mon = st.forward(x, labels, observe=obs)
+                    y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1)
                 if not st.computes_loss:
                     y = self._attack_output(node, y, truth)
-                    if i == 0:
+                    if watch:
                         mon = y
-                if i == 0 and mon is not None and self.cfg.output_check != "none":
+                if watch and mon is not None:
                     st.verifier.observe_output(mon)
                     if st.computes_loss and st.verifier.side is not None:
                         torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
@@ -455,6 +498,7 @@ class PipelineEngine:
         self._attack_params(node, st, truth)
         in_shape, out_shape = self._boundary_shapes(st, inputs[0])
         act_dtype = self.dtype
+        defer_w = self.cfg.defer_wgrad and not first
         warm = min(S - s - 1, M)
         rem = M - warm
         in_q: deque = deque()
@@ -473,23 +517,22 @@ class PipelineEngine:
             if not first:
                 x.requires_grad_(True)
             labels = targets[i].to(st.device, non_blocking=True) if last else None
-            obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
-            y, mon = st.forward(x, labels, observe=obs)
+            watch = i == self._mon_idx
+            obs = st.output_observer() if watch else None
+            y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1 and not defer_w)
             if last:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()
             else:
                 y = self._attack_output(node, y, truth)
-                if i == 0:
+                if watch:
                     mon = y
-            if i == 0 and mon is not None and self.cfg.output_check != "none":
+            if watch and mon is not None:
                 st.verifier.observe_output(mon)
                 if last and st.verifier.side is not None:
                     # the CE backward rewrites the logits buffer in place
                     torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
             return y
-
-        defer_w = self.cfg.defer_wgrad and not first
 
         def bwd(x, y, dy):
             """Input-gradient backward; the weight-gradient GEMMs are queued (ops.layers
@@ -610,16 +653,17 @@ class PipelineEngine:
             if not first:
                 x.requires_grad_(True)
             labels = targets[i].to(st.device, non_blocking=True) if last else None
-            obs = st.output_observer() if (i == 0 and self.cfg.output_check != "none") else None
-            y, mon = st.forward(x, labels, observe=obs)
+            watch = i == self._mon_idx
+            obs = st.output_observer() if watch else None
+            y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1 and not defer_w)
             if last:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()
             else:
                 y = self._attack_output(node, y, truth)
-                if i == 0:
+                if watch:
                     mon = y
-            if i == 0 and mon is not None and self.cfg.output_check != "none":
+            if watch and mon is not None:
                 st.verifier.observe_output(mon)
                 if last and st.verifier.side is not None:
                     torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
@@ -790,10 +834,17 @@ class PipelineEngine:
         present_nodes = self.all_ranks()
         idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
         raw = blame.to(torch.int32)
-        # a single flag quarantines that step's update; k consecutive flags compromise the node
+        # a single flag quarantines that step's update; k consecutive flags compromise the node;
+        # a failed weight-integrity check (weights rewritten outside the optimizer) is definitive
+        # evidence and compromises at once
         self.t_flagrun.copy_((self.t_flagrun + 1) * raw)
-        flags = (self.t_flagrun >= max(1, self.cfg.compromise_after)).to(torch.int32)
-        metrics = D[:, SV.D_METRICS:SV.D_METRICS + 6].contiguous()
+        flags = torch.maximum((self.t_flagrun >= max(1, self.cfg.compromise_after)).to(torch.int32),
+                              (D[:, SV.D_PARAM_FLAG] > 0).to(torch.int32) * raw)
+        # every blamed step also costs trust through the metrics (worst output deviation, no
+        # gradient consistency), so isolated detections accumulate instead of being forgotten
+        metrics = D[:, SV.D_METRICS:SV.D_METRICS + 6].clone()
+        metrics[:, 0] = torch.maximum(metrics[:, 0], blame)
+        metrics[:, 1] = metrics[:, 1] * (1.0 - blame)
         if len(present_nodes) == N:
             dstats.trust_update(self.t_values, self.t_counts, self.t_status, metrics, self.t_weights,
                                 self.trust.trust_threshold, self.cfg.trust_decay_per_step, 1.0,
@@ -863,15 +914,38 @@ class PipelineEngine:
         of, gf, pf = D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG], D[:, SV.D_PARAM_FLAG]
         blame = torch.zeros_like(of)
         evidence = torch.zeros_like(of)
-        for idx in self._replica_orders():
+        self.t_taint.copy_(torch.maximum(self.t_taint, (pf > 0).float()))
+        for r, idx in enumerate(self._replica_orders()):
             o, g, p = of[idx], gf[idx], pf[idx]
+            taint = self.t_taint[idx]
             ev = torch.maximum(o.max(), p.max())
             if self.cfg.attribute_flags:
-                first = o * (torch.cumsum(o, 0) == 1).float()
-                blame[idx] = torch.maximum(torch.maximum(p, first), g * (1.0 - ev))
+                # earliest anomalous stage; a stage with tampered (integrity-failed, not yet
+                # restored) weights counts as anomalous, so the output echoes it causes downstream
+                # are neither blamed nor skip the step (its own flag already compromised it)
+                a = torch.maximum(o, taint)
+                head = (torch.cumsum(a, 0) == 1).float() * a
+                first = head * o * (1.0 - taint)
+                b = torch.maximum(torch.maximum(p, first), g * (1.0 - ev))
+                ev = torch.maximum(p.max(), (head * o * (1.0 - taint)).max())
             else:
-                blame[idx] = torch.maximum(torch.maximum(o, g), p)
-            evidence[idx] = ev.expand(idx.numel())
+                b = torch.maximum(torch.maximum(o, g), p)
+            n = idx.numel()
+            if self.cfg.global_event_fraction > 0 and n >= 3:
+                # pipeline-wide gradient anomaly (every stage's norm jumps together in a loss spike):
+                # skip the update, blame nobody, and keep output / gradient blame off for a grace
+                # window; integrity (parameter) evidence is never suppressed
+                # (with an output anomaly in the replica the gradient flags are echoes of a tampered
+                # forward instead, attributed to its earliest stage above)
+                glob = (g.sum() >= max(2.0, math.ceil(self.cfg.global_event_fraction * n))).float() * (1.0 - o.max())
+                gr = self.t_grace[r:r + 1]
+                gr.copy_(torch.maximum(gr - 1.0, torch.zeros_like(gr)) * (1.0 - glob)
+                         + glob * float(self.cfg.global_event_grace))
+                quiet = torch.maximum(glob, (gr > 0).float())
+                b = torch.maximum(p, b * (1.0 - quiet))
+                ev = torch.maximum(torch.maximum(p.max(), o.max() * (1.0 - quiet)), glob)
+            blame[idx] = b
+            evidence[idx] = ev.expand(n)
         return blame, evidence
 
     # ================================================================== heartbeat -> OFFLINE
@@ -1116,6 +1190,9 @@ class PipelineEngine:
         moved = self._migrate(new_plan, restore=list(restored))
         dt = time.perf_counter() - t0
         self.excluded = sorted(set(self.excluded) | set(compromised))
+        for c in compromised:     # the tampered weights now live nowhere (restored or re-placed)
+            if c < self.t_taint.numel():
+                self.t_taint[c] = 0.0
         to_nodes = sorted({new_plan.owner_of_layer(li) for li in range(self.num_layers)
                            if self._old_owner.get(li) in compromised})
         rec = {"from_node": compromised[0], "from_nodes": list(compromised), "to_node": to_nodes[0] if to_nodes else None,
@@ -1211,6 +1288,7 @@ class PipelineEngine:
                 if src != dst:
                     moved += self._layer_numel(li)
         old_verifiers = {n: st.verifier for n, st in self.stages.items()}
+        old_ranges = {n: tuple(st.layer_range) for n, st in self.stages.items()}
         for st in self.stages.values():
             st.remove_hooks()
         self.plan = new_plan
@@ -1222,9 +1300,11 @@ class PipelineEngine:
             st.flat.step_count = step_count
             if st.flat.data is not st.flat.master:
                 st.flat.data.copy_(st.flat.master)
+            # detector baselines describe the layers a stage held: carry them over only when the
+            # stage kept exactly its layers (a stage that took over layers starts a fresh warm-up)
             ov = old_verifiers.get(node)
-            if ov is not None and ov.S == st.verifier.S:
-                st.verifier.load_state_dict(ov.state_dict())
+            if ov is not None and old_ranges.get(node) == tuple(st.layer_range) and ov.S == st.verifier.S:
+                st.verifier.adopt(ov)
         self._shape_cache = {}
         self._reset_shadows()                # the snapshot ring follows the plan: re-taken next interval
         return moved
@@ -1391,6 +1471,7 @@ class PipelineEngine:
                     return ent[aj]
             raise KeyError(f"checkpoint holds no {kind[:-1]} '{attr}' of layer {li}")
 
+        self.t_taint.zero_()      # weights replaced from a checkpoint
         for node, st in self.stages.items():
             a, _ = st.layer_range
             for i, name in enumerate(st.flat.names):
@@ -1410,6 +1491,7 @@ class PipelineEngine:
 
     def load_stage_states(self, model_sd: Dict[int, Dict], optim_sd: Dict[int, Dict],
                           verifier_sd: Optional[Dict[int, Dict]] = None):
+        self.t_taint.zero_()      # weights replaced from a checkpoint
         missing = [n for n in self.stages if n not in optim_sd and n not in model_sd]
         if missing:
             raise KeyError(f"checkpoint holds no state for local stage node(s) {missing}")

@@ -95,29 +95,70 @@ class Stage:
             return r
         from ..models.gpt2 import FusedHalfPair, GPT2HalfBlock
         layers, out, i = list(self.module), [], 0
+        self._runner_layer_idx: List[List[int]] = []
         while i < len(layers):
             a = layers[i]
             b = layers[i + 1] if i + 1 < len(layers) else None
             if (isinstance(a, GPT2HalfBlock) and isinstance(b, GPT2HalfBlock) and a.part == "attn"
                     and b.part == "mlp" and a.block_index == b.block_index):
                 out.append(FusedHalfPair(a, b))
+                self._runner_layer_idx.append([i, i + 1])
                 i += 2
             else:
                 out.append(a)
+                self._runner_layer_idx.append([i])
                 i += 1
         self._runner_cache = out
         return out
 
-    def forward(self, x, labels=None, observe=None):
+    # ---------------------------------------------------------------- verification overlap
+    def set_early_stats(self, excluded_ids=()) -> None:
+        """Prepare the per-layer gradient-statistics triggers: for each stage-local layer, the runs
+        of flat segments (parameters) it owns.  Parameters in ``excluded_ids`` (tied weights, whose
+        gradient changes in the tied all-reduce after the backward) are left to the final pass."""
+        ex = set(excluded_ids)
+        per_layer: Dict[int, List[int]] = {}
+        for j, (name, q) in enumerate(zip(self.flat.names, self.flat.params)):
+            if id(q) in ex:
+                continue
+            per_layer.setdefault(int(name.split(".", 1)[0]), []).append(j)
+        self._layer_seg_runs = {}
+        for li, segs in per_layer.items():
+            runs, lo = [], segs[0]
+            for a, b in zip(segs, segs[1:] + [None]):
+                if b != a + 1:
+                    runs.append((lo, a + 1))
+                    lo = b
+            self._layer_seg_runs[li] = runs
+
+    def _grad_ready(self, runner_idx: int):
+        """Autograd hook body: runner ``runner_idx``'s backward (incl. weight gradients) of the
+        step's last micro-batch is done -> its layers' gradient statistics can start."""
+        runs = []
+        for li in self._runner_layer_idx[runner_idx]:
+            runs += self._layer_seg_runs.get(li, [])
+        if runs:
+            self.verifier.grad_ready(self.flat.grad, runs)
+
+    def forward(self, x, labels=None, observe=None, arm_grad_stats: bool = False):
         """Returns (output, monitored_activation).  Loss stages return the (scalar) loss.
 
         ``observe``: optional output monitor.  A loss layer that owns its monitored tensor (the
         fused LM head: logits are rewritten into dlogits in place) is handed it and calls it at the
-        right moment; the returned monitored activation is then None (already observed)."""
+        right moment; the returned monitored activation is then None (already observed).
+
+        ``arm_grad_stats`` (the step's last micro-batch, weight gradients not deferred): hook every
+        layer input so that layer's gradient statistics start on the verifier's side stream as
+        soon as its backward is done, overlapping the backward of the layers before it."""
         layers = self._runners()
-        for layer in layers[:-1]:
+        arm = arm_grad_stats and getattr(self, "_layer_seg_runs", None) is not None
+        for k, layer in enumerate(layers[:-1]):
+            if arm and x.requires_grad:
+                x.register_hook(lambda g, k=k: self._grad_ready(k))
             x = layer(x)
         last = layers[-1]
+        if arm and x.requires_grad:
+            x.register_hook(lambda g, k=len(layers) - 1: self._grad_ready(k))
         if self.computes_loss:
             mon = x if len(layers) > 1 else None
             if mon is None and observe is not None and getattr(last, "accepts_observer", False):

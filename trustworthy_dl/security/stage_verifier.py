@@ -34,12 +34,13 @@ DIGEST = 24
 
 
 class StageVerifier:
-    def __init__(self, param_sizes: Sequence[int], device, *, history: int = 1000, warmup: int = 10,
-                 z_decision: float = 2.5, exclude_current: bool = True, max_quarantine: int = 50,
+    def __init__(self, param_sizes: Sequence[int], device, *, history: int = 1000, warmup: int = 20,
+                 z_decision: float = 2.5, exclude_current: bool = True, max_quarantine: int = 2,
                  ema_beta: float = 0.8, symmetric_consistency: bool = True, quarantine: bool = True,
                  output_detection: bool = True, gradient_verification: bool = True,
                  consistency_tolerance: float = 2.0, deviation_deadzone: float = 0.25,
-                 robust_baseline: bool = True, baseline_window: int = 100, serialize_streams: bool = False):
+                 robust_baseline="detrend", baseline_window: int = 64, serialize_streams: bool = False,
+                 features: str = "targeted", z_grad: float = 8.0, z_out: float = 8.0, sign_flip_cos: float = -0.4):
         """``consistency_tolerance`` / ``deviation_deadzone`` make the trust metrics tolerate the
         legitimate drift of training (gradient norms routinely move 2x within a few steps early in
         training): a norm ratio r scores min(1, tol * min(r, 1/r)), an output deviation d scores
@@ -53,11 +54,29 @@ class StageVerifier:
         self.symmetric = symmetric_consistency
         self.beta = ema_beta
         self.warmup = warmup
-        kw = dict(history=history, warmup=warmup, z_decision=z_decision, exclude_current=exclude_current,
-                  max_quarantine=max_quarantine, robust=robust_baseline, window=baseline_window)
-        self.out_det = S.DeviceZScore(12, self.device, **kw)
-        self.grad_det = S.DeviceZScore(17, self.device, **kw)
+        self.features = features
+        if features == "reference":
+            # the reference's decision rule: mean |z| over the 17 gradient / 12 output statistics
+            kw = dict(history=history, warmup=warmup, z_decision=z_decision, exclude_current=exclude_current,
+                      max_quarantine=max_quarantine, robust=robust_baseline, window=baseline_window)
+            self.out_det = S.DeviceZScore(12, self.device, **kw)
+            self.grad_det = S.DeviceZScore(17, self.device, **kw)
+        else:
+            # targeted: a few scale-free signals an attack must move — log gradient norm, log of
+            # the largest per-parameter norm, log element std; output mean, log std, log |max| —
+            # each against a detrended median / MAD baseline (the drift of learning), decision on
+            # the largest |z|, scale floored at 5 % per step.  The cosine to the EMA reference
+            # gradient is too autocorrelated for a z-score (it swings from -0.2 to 0.97 within a
+            # few clean steps after a loss spike, MI355X trace r2): sign flips are caught by an
+            # absolute rule instead (mean cosine < sign_flip_cos once the baseline is warm).
+            kw = dict(history=history, warmup=warmup, exclude_current=exclude_current,
+                      max_quarantine=max_quarantine, robust=robust_baseline, window=baseline_window,
+                      agg="max", rel_floor=0.0, abs_floor=0.05)
+            self.out_det = S.DeviceZScore(3, self.device, z_decision=z_out, **kw)
+            self.grad_det = S.DeviceZScore(3, self.device, z_decision=z_grad, **kw)
+        self.sign_flip_cos = float(sign_flip_cos)
         self.grad_stats = S.FlatGradStats(param_sizes, self.device) if len(param_sizes) else None
+        self.sumsq = S.FlatSumSq(param_sizes, self.device)
         self.S = len(param_sizes)
         z = lambda *shape: torch.zeros(*shape, dtype=torch.float32, device=self.device)  # noqa: E731
         self.out_stats = z(13)
@@ -69,6 +88,7 @@ class StageVerifier:
         self.ctrl[0] = 1.0
         self.digest = z(DIGEST)
         self._have_out = False
+        self._skip_grad_once = False
         # ``serialize_streams`` (debug): run the statistics on the compute stream instead of the side
         # stream; with identical inputs the digests must match the overlapped run bit for bit (an
         # ordering bug between the two streams shows up as a difference; tests/test_kernels_gpu.py)
@@ -91,6 +111,25 @@ class StageVerifier:
         self._have_out = True
 
     # ---------------------------------------------------------------- gradient path + digest
+    @property
+    def verify_on(self) -> bool:
+        return self.output_detection or self.gradient_verification
+
+    @torch.no_grad()
+    def grad_ready(self, flat_grad: torch.Tensor, seg_runs):
+        """Segments (parameters) whose gradient is final for this step: run their K3 partial pass
+        now, on the side stream after the compute stream's current point (overlaps the rest of
+        the backward).  ``finish_step`` completes the pass."""
+        if self.grad_stats is None or not self.verify_on or not flat_grad.is_cuda:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        stream = self.side if self.side is not None else cur
+        if self.side is not None:
+            self.side.wait_stream(cur)
+        for lo, hi in seg_runs:
+            c0, c1 = self.grad_stats.chunk_range_of(lo, hi)
+            self.grad_stats.partial(flat_grad, c0, c1, stream=stream)
+
     @torch.no_grad()
     def finish_step(self, flat_grad: Optional[torch.Tensor], loss: Optional[torch.Tensor],
                     host_metrics: Sequence[float], attack_truth: bool, stage_id: int) -> torch.Tensor:
@@ -105,7 +144,7 @@ class StageVerifier:
             d[D_LOSS] = loss.detach().float().reshape(())
         # ---- output anomaly
         if self.output_detection and self._have_out:
-            res = self.out_det.observe(self.out_stats[:12])
+            res = self.out_det.observe(self._out_features())
             d[D_OUT_FLAG] = res[0]
             d[D_OUT_Z] = res[1]
             d[D_OUT_CONF] = res[2]
@@ -126,7 +165,12 @@ class StageVerifier:
             d[D_NONFINITE] += self.out_stats[12]
         # ---- gradient verification
         gflag = None
-        if self.grad_stats is not None and flat_grad is not None:
+        bare = not self.verify_on
+        if bare and self.grad_stats is not None and flat_grad is not None:
+            # verification off: no statistics, quantiles or reference — only the clipping norm
+            d[D_GRAD_SUMSQ] = self.sumsq.compute(flat_grad, self.clip_w)[0]
+            d[D_METRICS + 1] = 1.0
+        elif self.grad_stats is not None and flat_grad is not None:
             g = self.grad_stats.compute(flat_grad)
             Sn = self.S
             norms = g[18:18 + Sn]
@@ -134,10 +178,16 @@ class StageVerifier:
             d[D_GRAD_L2] = g[10]
             d[D_GRAD_COS] = g[16]
             d[D_NONFINITE] += g[17]
-            if self.gradient_verification:
-                res = self.grad_det.observe(g[:17])
+            if self.gradient_verification and self._skip_grad_once:
+                self._skip_grad_once = False   # baselines restored without the EMA reference
+            elif self.gradient_verification:
+                res = self.grad_det.observe(self._grad_features(g))
                 gflag = res[0:1]
-                d[D_GRAD_FLAG] = res[0]
+                if self.features != "reference":
+                    # sign flip: the gradient points against its own recent history
+                    warm = (self.norm_n >= self.warmup).float()
+                    gflag = torch.maximum(gflag, (g[16:17] < self.sign_flip_cos).float() * warm)
+                d[D_GRAD_FLAG] = gflag[0]
                 d[D_GRAD_Z] = res[1]
                 d[D_GRAD_CONF] = res[2]
             ready = (self.norm_n >= self.warmup).float()
@@ -171,10 +221,22 @@ class StageVerifier:
             self.ctrl[1] = 0.0
         # clipping norm contribution: the gradient this stage will actually apply (a quarantined
         # update is skipped, so it must not shrink the honest stages' updates through the clip scale)
-        if self.grad_stats is not None and flat_grad is not None:
+        if self.grad_stats is not None and flat_grad is not None and not bare:
             d[D_GRAD_SUMSQ] = sumsq * (1.0 - self.ctrl[1])
         self._have_out = False
         return d
+
+    def _grad_features(self, g: torch.Tensor) -> torch.Tensor:
+        if self.features == "reference":
+            return g[:17]
+        lg = lambda v: torch.log(torch.clamp(v, min=1e-30))  # noqa: E731
+        return torch.stack([lg(g[10]), lg(g[15]), lg(g[1])])
+
+    def _out_features(self) -> torch.Tensor:
+        o = self.out_stats
+        if self.features == "reference":
+            return o[:12]
+        return torch.stack([o[0], torch.log(torch.clamp(o[1], min=1e-30)), torch.log(torch.clamp(o[11], min=1e-30))])
 
     def set_clip_weights(self, weights: Sequence[float]):
         """Per-parameter weights (1 = counted, 0 = counted on another stage) for the digest's
@@ -190,6 +252,17 @@ class StageVerifier:
         else:
             self.ctrl[0] = 1.0
 
+    def adopt(self, other: "StageVerifier"):
+        """Take over another verifier's detector state for the same parameters (a stage rebuilt
+        around unchanged layers): baselines, EMAs and the EMA reference gradient of the cosine
+        feature (without it the first cosine after a rebuild reads 1.0 and looks like an attack)."""
+        self.load_state_dict(other.state_dict())
+        self._skip_grad_once = False
+        if self.grad_stats is not None and other.grad_stats is not None and other.grad_stats.ref is not None \
+                and self.grad_stats.ref is not None and other.grad_stats.ref.shape == self.grad_stats.ref.shape:
+            self.grad_stats.ref = other.grad_stats.ref.to(self.device)
+            self.grad_stats.ref_valid = other.grad_stats.ref_valid
+
     def state_dict(self):
         return {k: v.detach().cpu() for k, v in {
             "out_ring": self.out_det.ring, "out_state": self.out_det.state,
@@ -204,3 +277,6 @@ class StageVerifier:
                      ("norm_ema", self.norm_ema), ("norm_n", self.norm_n)):
             if k in sd and sd[k].shape == t.shape:
                 t.copy_(sd[k])
+        # the EMA reference gradient is not checkpointed: its first cosine after a load reads 1.0,
+        # so that one gradient observation is not scored against the restored baseline
+        self._skip_grad_once = True

@@ -1,7 +1,7 @@
 """``get_dataloader(name, split, batch_size)`` (experiment_runner.py:100-110; phantom in the reference).
 
 Datasets: ``openwebtext`` (README.md:80) / any ``*text*`` name -> token streams for language
-modelling; ``cifar10`` (README.md:102) -> 3x32x32 images, 10 classes; ``imagenet`` ->
+modelling; ``markov`` -> a learnable synthetic token stream (order-k Markov chain); ``cifar10`` (README.md:102) -> 3x32x32 images, 10 classes; ``imagenet`` ->
 3x224x224 images, 1000 classes.  There is no network access in this environment, so every
 loader yields *synthetic* data of the right shape (documented in the batch's ``"synthetic"``
 flag): deterministic per (seed, split, index).  A local directory of ``.npy`` token shards or
@@ -54,6 +54,67 @@ class SyntheticLanguageModeling:
             yield b
 
 
+class MarkovLanguageModeling:
+    """Learnable synthetic token stream: an order-``order`` Markov chain over the vocabulary.
+
+    Each context (the previous ``order`` tokens) has ``branching`` successor tokens, picked by a
+    fixed hash of the context and the chain's seed, with Zipf-like probabilities.  A language
+    model can learn it — the loss falls from ln(V) towards the chain's entropy (about 1.2 nats for
+    the default branching 4) — so gradients drift and correlate from step to step the way real
+    training's do, unlike uniform random tokens whose loss and gradients stay flat.  Used to
+    measure detection false-positive rates under learning (bench_detection.py --data markov).
+    Deterministic per (seed, split, batch index)."""
+
+    _PROBS = {2: [0.7, 0.3], 3: [0.6, 0.3, 0.1], 4: [0.6, 0.25, 0.1, 0.05]}
+
+    def __init__(self, batch_size: int, seq_len: int = 1024, vocab_size: int = 50257, num_batches: int = 100,
+                 seed: int = 0, split: str = "train", order: int = 1, branching: int = 4, pin_memory: bool = False):
+        self.batch_size, self.seq_len, self.vocab_size = batch_size, seq_len, vocab_size
+        self.num_batches = num_batches
+        self.chain_seed = seed                      # the chain itself is the same for every split
+        self.seed = seed + (0 if split == "train" else 10_000)
+        self.order = max(1, int(order))
+        probs = self._PROBS.get(branching) or list(np.full(branching, 1.0 / branching))
+        self.cum = np.cumsum(np.asarray(probs, dtype=np.float64))
+        self.cum[-1] = 1.0
+        self.pin = pin_memory and torch.cuda.is_available()
+
+    def entropy(self) -> float:
+        p = np.diff(np.concatenate([[0.0], self.cum]))
+        return float(-(p * np.log(p)).sum())
+
+    def successor(self, ctx: np.ndarray, k: np.ndarray) -> np.ndarray:
+        """Successor ``k`` of each context row (uint64 hash of the context tokens and the seed)."""
+        h = np.full(ctx.shape[0], (self.chain_seed * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & (2 ** 64 - 1),
+                    dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            for j in range(ctx.shape[1]):
+                h = (h ^ ctx[:, j].astype(np.uint64)) * np.uint64(0x100000001B3)
+                h ^= h >> np.uint64(29)
+            h = (h + k.astype(np.uint64) * np.uint64(0xBF58476D1CE4E5B9)) * np.uint64(0x94D049BB133111EB)
+            h ^= h >> np.uint64(31)
+        return (h % np.uint64(self.vocab_size)).astype(np.int64)
+
+    def __len__(self):
+        return self.num_batches
+
+    def __iter__(self):
+        for i in range(self.num_batches):
+            rng = np.random.default_rng(self.seed * 100_003 + i)
+            B, T = self.batch_size, self.seq_len + 1
+            ids = np.empty((B, T), dtype=np.int64)
+            ids[:, :self.order] = rng.integers(0, self.vocab_size, (B, self.order))
+            u = rng.random((B, T))
+            for t in range(self.order, T):
+                k = np.searchsorted(self.cum, u[:, t], side="right")
+                ids[:, t] = self.successor(ids[:, t - self.order:t], k)
+            ids = torch.from_numpy(ids)
+            b = {"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()}
+            if self.pin:
+                b = {k_: v.pin_memory() for k_, v in b.items()}
+            yield b
+
+
 class SyntheticImages:
     """Class-conditional Gaussian images (learnable signal, so loss decreases)."""
 
@@ -87,6 +148,8 @@ def get_dataloader(dataset_name: str, split: str = "train", batch_size: int = 32
                    token_file: Optional[str] = None, token_bytes: int = 2, rank: int = 0, world: int = 1):
     name = dataset_name.lower()
     nb = num_batches if num_batches is not None else (100 if split == "train" else 10)
+    if name in ("markov", "markov-lm", "synthetic-markov"):
+        return MarkovLanguageModeling(batch_size, seq_len, vocab_size, nb, seed, split, pin_memory=pin_memory)
     if "text" in name or name in ("openwebtext", "wikitext", "tokens", "lm"):
         if native or token_file:
             from ..runtime.native import NativeTokenLoader
