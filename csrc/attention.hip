@@ -35,6 +35,15 @@ static int dkdv_ns() {
     return ns;
 }
 
+// dK/dV register prefetch depth (tiles ahead): TDL_ATTN_DKDV_PF=1|2 (default 2).
+static int dkdv_pf() {
+    static int pf = [] {
+        const char* e = std::getenv("TDL_ATTN_DKDV_PF");
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    return pf;
+}
+
 static int attn_nbh_arg(int nbh) {
     const char* e = std::getenv("TDL_ATTN_MAP");
     return (e && std::strcmp(e, "xcd") == 0) ? -nbh : nbh;
@@ -290,7 +299,7 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 // the LDS (64 KB, still 2 workgroups per CU) but measures slower (see dkdv_ns).
 // Products per 32-row sub-tile and wave: S = Q.K^T, dP = dO.V^T (row-read A, K/V fragments
 // resident in registers), dV^T += dO^T.P and dK^T += Q^T.dS (tr-read A, S/dP accumulators as B).
-template <bool CAUSAL, int NS>
+template <bool CAUSAL, int NS, int PF>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                                             bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
@@ -350,21 +359,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     }
     __syncthreads();
 
+    // register staging of the next tile(s): PF = 1 loads tile t+1 during tile t; PF = 2 loads
+    // tile t+2 during tile t (tile t+1 already sits in registers), so a load has two tiles of
+    // compute (~1.5k cycles) to land instead of one (PMC: 47 % of wave cycles waiting)
+    uint4 qn[NS], dn[NS];
+    float ln = 0.f, dln = 0.f;
+    auto load_tile = [&](int t0, uint4 (&q)[NS], uint4 (&d)[NS], float& l, float& dl) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            q[j] = *(const uint4*)(qbase + (size_t)(t0 + srow + 32 * j) * ldq + sch * 8);
+            d[j] = *(const uint4*)(dobase + (size_t)(t0 + srow + 32 * j) * ldo + sch * 8);
+        }
+        if (tid < BQ) {
+            l = lse_row[t0 + tid] * LOG2E;
+            dl = delta_row[t0 + tid];
+        }
+    };
+    if (PF == 2 && q_start + BQ < T) load_tile(q_start + BQ, qn, dn, ln, dln);
     int buf = 0;
     for (int qt = q_start; qt < T; qt += BQ) {
         const bool has_next = qt + BQ < T;
-        uint4 qn[NS], dn[NS];
-        float ln = 0.f, dln = 0.f;
-        if (has_next) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                qn[j] = *(const uint4*)(qbase + (size_t)(qt + BQ + srow + 32 * j) * ldq + sch * 8);
-                dn[j] = *(const uint4*)(dobase + (size_t)(qt + BQ + srow + 32 * j) * ldo + sch * 8);
-            }
-            if (tid < BQ) {
-                ln = lse_row[qt + BQ + tid] * LOG2E;
-                dln = delta_row[qt + BQ + tid];
-            }
+        uint4 qf[NS], df[NS];
+        float lf = 0.f, dlf = 0.f;
+        if (PF == 2) {
+            if (qt + 2 * BQ < T) load_tile(qt + 2 * BQ, qf, df, lf, dlf);
+        } else if (has_next) {
+            load_tile(qt + BQ, qn, dn, ln, dln);
         }
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -426,6 +446,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         }
         __syncthreads();
         buf ^= 1;
+        if (PF == 2) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                qn[j] = qf[j];
+                dn[j] = df[j];
+            }
+            ln = lf;
+            dln = dlf;
+        }
     }
     bf16_t* dkrow = dqkv + ((size_t)b * T + kj) * ldq + H * HD + hd * HD;
     bf16_t* dvrow = dkrow + H * HD;
@@ -582,12 +611,14 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     auto dQKV = (bf16_t*)dqkv;
     const int nb = attn_nbh_arg(B * H);
     if (causal) {
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else attn_bwd_dkdv_kernel<true, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
         attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
     } else {
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else attn_bwd_dkdv_kernel<false, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<false, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        else attn_bwd_dkdv_kernel<false, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
         attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
     }
     TDL_LAUNCH_CHECK();

@@ -128,15 +128,30 @@ class _NaNAttacker:
         return False
 
 
+class _SignFlipAttacker:
+    """Negates node 1's gradient every step (its norm and statistics stay normal)."""
+
+    def on_gradients(self, node, grad, step):
+        if node == 1:
+            grad.neg_()
+            return True
+        return False
+
+
 def _attack_worker(rank, world, port, out_path, kind="scale"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = _engine(1, 2, dp=3)
-    eng.attacker = _ScaleAttacker() if kind == "scale" else _NaNAttacker()
+    eng.attacker = {"scale": _ScaleAttacker, "nan": _NaNAttacker, "sign_flip": _SignFlipAttacker}[kind]()
     excluded = []
-    for b in _batches(3, 12):
+    if kind == "sign_flip":   # replicas must share a learning signal for a direction test: Markov tokens
+        from trustworthy_dl.utils.data_loader import MarkovLanguageModeling
+        batches = list(MarkovLanguageModeling(12, 32, 64, num_batches=3, seed=2))
+    else:
+        batches = _batches(3, 12)
+    for b in batches:
         eng.train_step(b)
         excluded.append([int(v) for v in eng._dp_excluded.tolist()])
     eng.flush()
@@ -148,10 +163,11 @@ def _attack_worker(rank, world, port, out_path, kind="scale"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["scale", "nan"])
+@pytest.mark.parametrize("kind", ["scale", "nan", "sign_flip"])
 def test_dp3_robust_aggregation_excludes_poisoned_replica(kind):
-    """x50 gradients or NaN/Inf gradients on one replica: it is left out of the mean and every
-    replica (the poisoned one included) ends with the same finite weights."""
+    """x50 gradients, NaN/Inf gradients or a sign-flipped gradient (caught only by the cross-replica
+    direction check) on one replica: it is left out of the mean and every replica (the poisoned
+    one included) ends with the same finite weights."""
     import math
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "res")

@@ -327,7 +327,7 @@ def test_quarantined_stage_does_not_shrink_clip_scale():
     atk.activate_attacks()
     m = get_model("gpt2-tiny", seq_len=32, seed=0, vocab_size=1024)
     cfg = EngineConfig(num_nodes=3, micro_batches=2, seq_len=32, device="cpu", layer_granularity="block",
-                       adamw=AdamWConfig(lr=1e-3, max_grad_norm=1.0), reassign=False)
+                       adamw=AdamWConfig(lr=1e-3, max_grad_norm=1.0), reassign=False, verifier={"warmup": 10})
     eng = PipelineEngine(m, cfg, TrustManager(3), attacker=atk, metrics=MetricsCollector(), detector=AttackDetector())
     from trustworthy_dl.security import stage_verifier as SV
     scales = []

@@ -75,6 +75,8 @@ class EngineConfig:
     data_parallel: int = 1               # pipeline replicas (distributed): world = stages x replicas
     robust_aggregation: bool = True      # DP: flagged / outlier replicas are left out of the gradient mean
     outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
+    direction_margin: float = 0.2        # DP (>= 3 replicas): cosine to the other replicas' sum below 0 and
+                                         # this far below the median = outlier (sign flips)
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
@@ -1008,6 +1010,8 @@ class PipelineEngine:
             ratio = norms / torch.clamp(med, min=1e-30)
             tau = float(self.cfg.outlier_ratio)
             bad = torch.maximum(bad, ((ratio > tau) | (ratio < 1.0 / tau)).float())
+            if st is not None and self.cfg.robust_aggregation:
+                bad = torch.maximum(bad, self._dp_direction_outliers(st, len(ranks), bad[ranks.index(self.rank)]))
         if not self.cfg.robust_aggregation:
             bad = torch.zeros_like(bad)
         ok = 1.0 - bad
@@ -1026,6 +1030,32 @@ class PipelineEngine:
         self._dp_excluded = bad
         dist.all_reduce(sq)
         return (sq / self.dp).reshape(())
+
+    def _dp_direction_outliers(self, st: Stage, n: int, bad_me: torch.Tensor) -> torch.Tensor:
+        """Cross-replica direction check (the reference's ``detect_byzantine_behavior`` Gram-matrix
+        idea, attack_detector.py:143-162, on a sketch): every replica takes the same strided 1/64
+        sample of its flat gradient, one small all-reduce sums the unit-normalised samples of the
+        replicas not already excluded, and each replica's cosine to the SUM OF THE OTHERS is
+        all-gathered.  A replica pointing against its peers (a sign
+        flip, which no per-replica statistic sees) is an outlier: cosine < 0 and more than
+        ``direction_margin`` below the replicas' median.  Device-side, no host sync."""
+        g = st.flat.grad
+        if getattr(self, "_dp_sidx", None) is None or self._dp_sidx.device != g.device:
+            self._dp_sidx = torch.arange(0, g.numel(), 64, device=g.device)
+        sub = torch.nan_to_num(g.index_select(0, self._dp_sidx), nan=0.0, posinf=0.0, neginf=0.0)
+        # unit directions, replicas already excluded (flag / non-finite / norm outlier) left out of
+        # the reference: a x50 replica must not define "the others' direction"
+        unit = sub / torch.clamp(sub.norm(), min=1e-30)
+        contrib = unit * (1.0 - bad_me)
+        tot = contrib.clone()
+        dist.all_reduce(tot, group=self.dp_group)
+        others = tot - contrib
+        cos = ((unit * others).sum() / torch.clamp(others.norm(), min=1e-30)).reshape(1)
+        allc = [torch.zeros_like(cos) for _ in range(n)]
+        dist.all_gather(allc, cos, group=self.dp_group)
+        c = torch.cat(allc)
+        self._dp_cos = c
+        return ((c < 0) & (c < c.median() - float(self.cfg.direction_margin))).float()
 
     @torch.no_grad()
     def _audit_params(self):
