@@ -62,13 +62,43 @@ def main():
     def dg_fused():
         return gemm.matmul(dy, wp.t(), epi="dgelu", aux=pre_fused, colsum=db)
 
+    from trustworthy_dl.ops import blaslt
+    pre_bl = torch.empty_like(pre_lib)
+    db_bl = torch.zeros(4 * C, device=dev)
+
+    def fc_blaslt():
+        y = torch.empty_like(pre_lib)
+        assert blaslt.gemm_colmajor(0, 0, 4 * C, M, C, 1.0, wfc, 4 * C, h2, C, 0.0, y, 4 * C, y, 4 * C,
+                                    blaslt.EPI_GELU_AUX_BIAS, bfc, pre_bl, 4 * C), "GELU_AUX_BIAS unsupported"
+        return y
+
+    def dg_blaslt():
+        d = torch.empty_like(pre_lib)
+        # dpre[M, 4C] = (dy[M, C] @ Wp^T) * gelu'(pre), bias grad of the result into db_bl
+        assert blaslt.gemm_colmajor(1, 0, 4 * C, M, C, 1.0, wp, C, dy, C, 0.0, d, 4 * C, d, 4 * C,
+                                    208, db_bl, pre_bl, 4 * C), "DGELU_BGRAD unsupported"
+        return d
+
     # numerics: both paths against each other (fp32 reference checks live in tests/test_gemm_gpu.py)
     f1, f2 = fc_lib(), fc_fused()
     err_fc = float((f1.float() - f2.float()).abs().max() / f1.float().abs().max())
     d1, d2 = dg_lib(), dg_fused()
     err_dg = float((d1.float() - d2.float()).abs().max() / d1.float().abs().max())
-    for name, lib_fn, fused_fn, err, fl in (("fc_fwd_gelu", fc_lib, fc_fused, err_fc, 2.0 * M * C * 4 * C),
-                                            ("proj_dgrad_dgelu", dg_lib, dg_fused, err_dg, 2.0 * M * C * 4 * C)):
+    f3 = fc_blaslt()
+    err_fc_bl = float((f1.float() - f3.float()).abs().max() / f1.float().abs().max())
+    d3 = None
+    try:
+        d3 = dg_blaslt()
+        err_dg_bl = float((d1.float() - d3.float()).abs().max() / d1.float().abs().max())
+    except AssertionError as e:
+        print(json.dumps({"note": str(e)}), flush=True)
+        err_dg_bl = None
+    cases = [("fc_fwd_gelu", fc_lib, fc_fused, err_fc, 2.0 * M * C * 4 * C),
+             ("proj_dgrad_dgelu", dg_lib, dg_fused, err_dg, 2.0 * M * C * 4 * C),
+             ("fc_fwd_gelu_blaslt_epilogue", fc_lib, fc_blaslt, err_fc_bl, 2.0 * M * C * 4 * C)]
+    if d3 is not None:
+        cases.append(("proj_dgrad_dgelu_blaslt_epilogue", dg_lib, dg_blaslt, err_dg_bl, 2.0 * M * C * 4 * C))
+    for name, lib_fn, fused_fn, err, fl in cases:
         t_l, t_f = [], []
         lib_fn(); fused_fn()
         for _ in range(args.rounds):

@@ -4,8 +4,9 @@ Datasets: ``openwebtext`` (README.md:80) / any ``*text*`` name -> token streams 
 modelling; ``markov`` -> a learnable synthetic token stream (order-k Markov chain); ``cifar10`` (README.md:102) -> 3x32x32 images, 10 classes; ``imagenet`` ->
 3x224x224 images, 1000 classes.  There is no network access in this environment, so every
 loader yields *synthetic* data of the right shape (documented in the batch's ``"synthetic"``
-flag): deterministic per (seed, split, index).  A local directory of ``.npy`` token shards or
-a torchvision-style CIFAR folder can be plugged in through ``data_dir``.
+flag): deterministic per (seed, split, index).  Real data plugs in through ``data_dir``: ``.npy``
+token shards for language modelling, the CIFAR-10/100 binary release or ``{split}_images.npy`` +
+``{split}_labels.npy`` arrays for images (``ImageArrays``; nothing is unpickled).
 Batches are dicts ``{"input": Tensor, "target": Tensor}`` (distributed_trainer.py:395, 398).
 
 ``native=True`` (language modelling) switches to the C++ loader (runtime/native.py,
@@ -115,6 +116,70 @@ class MarkovLanguageModeling:
             yield b
 
 
+class ImageArrays:
+    """Real image data from disk, no pickles:
+
+    * the CIFAR-10/100 *binary* release (``data_batch_{1..5}.bin`` / ``test_batch.bin``, or
+      ``train.bin`` / ``test.bin`` for CIFAR-100): records of label byte(s) + 3072 pixel bytes;
+    * ``{split}_images.npy`` (uint8 [N, H, W, 3] or [N, 3, H, W]) + ``{split}_labels.npy``.
+
+    Images are normalised per channel (CIFAR mean / std) and shuffled per epoch (seeded)."""
+
+    _MEAN = np.array([0.4914, 0.4822, 0.4465], dtype=np.float32)
+    _STD = np.array([0.2470, 0.2435, 0.2616], dtype=np.float32)
+
+    def __init__(self, data_dir: str, batch_size: int, split: str = "train", num_batches: Optional[int] = None,
+                 seed: int = 0, num_classes: int = 10, pin_memory: bool = False):
+        self.batch_size, self.seed, self.num_classes = batch_size, seed, num_classes
+        self.pin = pin_memory and torch.cuda.is_available()
+        x, y = self._load(data_dir, split, num_classes)
+        if x is None:
+            raise FileNotFoundError(f"no CIFAR binary batches or {split}_images.npy in {data_dir}")
+        self.x, self.y = x, y
+        full = len(self.y) // batch_size
+        self.num_batches = min(full, num_batches) if num_batches else full
+
+    @staticmethod
+    def _load(d: str, split: str, ncls: int):
+        npy = os.path.join(d, f"{split}_images.npy")
+        if os.path.exists(npy):
+            x = np.load(npy, allow_pickle=False)
+            y = np.load(os.path.join(d, f"{split}_labels.npy"), allow_pickle=False).astype(np.int64)
+            if x.ndim == 4 and x.shape[-1] == 3:
+                x = x.transpose(0, 3, 1, 2)
+            return np.ascontiguousarray(x), y
+        if ncls == 100:
+            files = [os.path.join(d, "train.bin" if split == "train" else "test.bin")]
+            rec, lab_off = 3074, 1           # coarse label, fine label, pixels
+        else:
+            files = ([os.path.join(d, f"data_batch_{i}.bin") for i in range(1, 6)] if split == "train"
+                     else [os.path.join(d, "test_batch.bin")])
+            rec, lab_off = 3073, 0
+        files = [f for f in files if os.path.exists(f)]
+        if not files:
+            return None, None
+        raw = np.concatenate([np.fromfile(f, dtype=np.uint8) for f in files])
+        raw = raw[: len(raw) // rec * rec].reshape(-1, rec)
+        y = raw[:, lab_off].astype(np.int64)
+        x = raw[:, rec - 3072:].reshape(-1, 3, 32, 32)
+        return x, y
+
+    def __len__(self):
+        return self.num_batches
+
+    def __iter__(self):
+        order = np.random.default_rng(self.seed).permutation(len(self.y))
+        mean = self._MEAN[:, None, None]
+        std = self._STD[:, None, None]
+        for i in range(self.num_batches):
+            idx = order[i * self.batch_size:(i + 1) * self.batch_size]
+            x = (self.x[idx].astype(np.float32) / 255.0 - mean) / std
+            b = {"input": torch.from_numpy(x), "target": torch.from_numpy(self.y[idx])}
+            if self.pin:
+                b = {k: v.pin_memory() for k, v in b.items()}
+            yield b
+
+
 class SyntheticImages:
     """Class-conditional Gaussian images (learnable signal, so loss decreases)."""
 
@@ -157,10 +222,13 @@ def get_dataloader(dataset_name: str, split: str = "train", batch_size: int = 32
                                      token_bytes=token_bytes, seed=seed + (0 if split == "train" else 10_000),
                                      num_batches=nb, rank=rank, world=world, pin_memory=pin_memory or None)
         return SyntheticLanguageModeling(batch_size, seq_len, vocab_size, nb, seed, split, data_dir, pin_memory)
-    if name in ("cifar10", "cifar-10", "cifar"):
-        return SyntheticImages(batch_size, 32, 10, nb, seed, split, pin_memory)
-    if name in ("cifar100", "cifar-100"):
-        return SyntheticImages(batch_size, 32, 100, nb, seed, split, pin_memory)
+    if name in ("cifar10", "cifar-10", "cifar", "cifar100", "cifar-100"):
+        ncls = 100 if "100" in name else 10
+        if data_dir:
+            return ImageArrays(data_dir, batch_size, split, num_batches, seed, ncls, pin_memory)
+        return SyntheticImages(batch_size, 32, ncls, nb, seed, split, pin_memory)
     if name in ("imagenet", "imagenet1k", "imagenet-1k"):
+        if data_dir:
+            return ImageArrays(data_dir, batch_size, split, num_batches, seed, 1000, pin_memory)
         return SyntheticImages(batch_size, 224, 1000, nb, seed, split, pin_memory)
     raise ValueError(f"unknown dataset {dataset_name!r}")
