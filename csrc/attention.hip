@@ -310,9 +310,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t Qw[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t dOw[2][BQ * HD];
-    __shared__ float lse_s[2][BQ], delta_s[2][BQ];  // lse pre-scaled by log2(e)
+    __shared__ __attribute__((aligned(16))) float lse_s[2][BQ];  // lse pre-scaled by log2(e)
+    __shared__ __attribute__((aligned(16))) float delta_s[2][BQ];
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile-level branches stay scalar
     int bh, kbi;
     // causal dK/dV: key block 0 sees every query -> it is the heavy one; reverse the LPT order
     head_xcd_map(blockIdx.x, nbh, T / BK, CAUSAL, bh, kbi);
@@ -405,13 +407,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
                 sacc = MFMA32(aq, kf[s], sacc);
                 dpacc = MFMA32(ad, vf[s], dpacc);
             }
+            // the causal mask matters only on the tiles that straddle this wave's diagonal (a few
+            // of T / 32): elsewhere the per-element compare + select is dropped (VALU-bound loop)
+            // lse / delta of the lane's 16 query rows: 4 groups of 4 consecutive rows -> 4 + 4
+            // 16-byte LDS reads instead of 32 scalar ones
+            float lsv[16], dlv[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                float p = fast_exp2(fmaf(sacc[i], sl2, -lsb[ql]));
-                if (CAUSAL && kj > qs + ql) p = 0.f;
-                sacc[i] = p;
-                dpacc[i] = p * (dpacc[i] - dlb[ql]);
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const float4 a = *(const float4*)(lsb + 8 * g4 + 4 * h);
+                const float4 c = *(const float4*)(dlb + 8 * g4 + 4 * h);
+                lsv[4 * g4] = a.x; lsv[4 * g4 + 1] = a.y; lsv[4 * g4 + 2] = a.z; lsv[4 * g4 + 3] = a.w;
+                dlv[4 * g4] = c.x; dlv[4 * g4 + 1] = c.y; dlv[4 * g4 + 2] = c.z; dlv[4 * g4 + 3] = c.w;
+            }
+            if (CAUSAL && qs < k0 + 31) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
+                    float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
+                    if (kj > qs + ql) p = 0.f;
+                    sacc[i] = p;
+                    dpacc[i] = p * (dpacc[i] - dlv[i]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
+                    sacc[i] = p;
+                    dpacc[i] = p * (dpacc[i] - dlv[i]);
+                }
             }
             const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
             const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
