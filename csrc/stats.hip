@@ -870,3 +870,73 @@ TDL_API int tdl_checksum_bf16(const void* x, int64_t n, double* ws, double* out,
     checksum_final_kernel<<<1, 256, 0, s>>>(ws, nb > 0 ? nb : 1, out);
     TDL_LAUNCH_CHECK();
 }
+
+// ------------------------------------------------------------------ K6 cosine Gram matrix
+// N x N cosine similarity of N flat vectors of length D (node output digests / replica sketches,
+// attack_detector.py:143-162 + 365-379), N <= 16, read IN PLACE through a pointer table (no
+// stacked copy).  Phase 1: every block takes a strided share of D and accumulates all N(N+1)/2
+// pair dot products in fp64 registers-per-thread, block-reduced in a fixed order into its slot of
+// `part`.  Phase 2: one block sums the slots per pair in block order and normalises.  Deterministic.
+#define GRAM_MAXN 16
+#define GRAM_PAIRS (GRAM_MAXN * (GRAM_MAXN + 1) / 2)
+struct GramPtrs {
+    const void* p[GRAM_MAXN];
+};
+
+__global__ __launch_bounds__(256) void gram_partial_kernel(GramPtrs ptrs, int N, int64_t D, int dtype,
+                                                           double* __restrict__ part) {
+    __shared__ double red[4];
+    const int npairs = N * (N + 1) / 2;
+    for (int pr = 0; pr < npairs; ++pr) {
+        // pair index -> (i, j), i <= j
+        int i = 0, rem = pr;
+        while (rem >= N - i) { rem -= N - i; ++i; }
+        const int j = i + rem;
+        double acc = 0.0;
+        for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < D; k += (int64_t)gridDim.x * blockDim.x) {
+            const float a = dtype == 1 ? bf2f(((const bf16_t*)ptrs.p[i])[k]) : ((const float*)ptrs.p[i])[k];
+            const float b = dtype == 1 ? bf2f(((const bf16_t*)ptrs.p[j])[k]) : ((const float*)ptrs.p[j])[k];
+            acc += (double)a * (double)b;
+        }
+        acc = wave_sum_d(acc);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) part[(size_t)blockIdx.x * GRAM_PAIRS + pr] = red[0] + red[1] + red[2] + red[3];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void gram_final_kernel(const double* __restrict__ part, int nblk, int N,
+                                                         float* __restrict__ out) {
+    __shared__ double dots[GRAM_PAIRS];
+    const int npairs = N * (N + 1) / 2;
+    for (int pr = threadIdx.x; pr < npairs; pr += blockDim.x) {
+        double s = 0.0;
+        for (int b = 0; b < nblk; ++b) s += part[(size_t)b * GRAM_PAIRS + pr];
+        dots[pr] = s;
+    }
+    __syncthreads();
+    for (int pr = threadIdx.x; pr < npairs; pr += blockDim.x) {
+        int i = 0, rem = pr;
+        while (rem >= N - i) { rem -= N - i; ++i; }
+        const int j = i + rem;
+        auto diag = [&](int a) { return a * N - a * (a - 1) / 2; };  // pair index of (a, a)
+        const double den = sqrt(dots[diag(i)] * dots[diag(j)]);
+        const float c = den > 0.0 ? (float)(dots[pr] / den) : 0.f;
+        out[i * N + j] = c;
+        out[j * N + i] = c;
+    }
+}
+
+TDL_API int64_t tdl_gram_ws_bytes() { return (int64_t)sizeof(double) * 512 * GRAM_PAIRS; }
+
+TDL_API int tdl_cosine_gram(const void* const* ptrs, int N, int64_t D, int dtype, float* out, void* ws, hipStream_t s) {
+    if (N < 1 || N > GRAM_MAXN || D <= 0) return (int)hipErrorInvalidValue;
+    GramPtrs gp{};
+    for (int i = 0; i < N; ++i) gp.p[i] = ptrs[i];
+    int64_t nb = (D + 256 * 8 - 1) / (256 * 8);
+    const int nblk = (int)(nb < 1 ? 1 : (nb > 512 ? 512 : nb));
+    gram_partial_kernel<<<nblk, 256, 0, s>>>(gp, N, D, dtype, (double*)ws);
+    gram_final_kernel<<<1, 256, 0, s>>>((const double*)ws, nblk, N, out);
+    TDL_LAUNCH_CHECK();
+}

@@ -555,3 +555,18 @@ def test_xent_fused_rows_vs_fp32(V, ld):
     d = buf.float()
     assert _rel(d[:, :V], ref_d) < 1e-2
     assert torch.all(d[:, V:] == 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n", [2, 5, 16])
+def test_cosine_gram_native_matches_torch(n, dtype):
+    """K6: N x N cosine Gram of N flat vectors read in place (attack_detector.py:143-162)."""
+    from trustworthy_dl.ops.stats import cosine_gram
+    torch.manual_seed(n)
+    base = torch.randn(300_001, device=DEV)
+    xs = [(base * (i % 3 - 1 + 0.3) + torch.randn(300_001, device=DEV) * 0.5).to(dtype) for i in range(n)]
+    g = cosine_gram(xs)
+    X = torch.stack([x.double().cpu() for x in xs])
+    ref = (X @ X.t()) / (X.norm(dim=1)[:, None] * X.norm(dim=1)[None, :])
+    assert torch.allclose(g.double().cpu(), ref, atol=1e-5), (g, ref)
+    assert torch.equal(cosine_gram(xs), g)   # deterministic

@@ -100,6 +100,8 @@ _SIGNATURES = {
     "tdl_grad_stats_partial": [_P, _P, _P, _I, _I, _I, _I, _F, _P, _I, _P],
     "tdl_grad_stats_final": [_P, _P, _I, _P, _L, _I, _P, _I, _I, _P],
     "tdl_grad_sumsq": [_P, _P, _I, _P, _P, _P, _P],
+    "tdl_gram_ws_bytes": [],
+    "tdl_cosine_gram": [_P, _I, _L, _I, _P, _P, _P],
     "tdl_zscore_detect": [_P, _P, _P, _I, _I, _I, _F, _I, _I, _I, _I, _F, _F, _P, _P],
     "tdl_trust_update": [_P, _P, _P, _P, _P, _P, _P, _I, _F, _F, _F, _P],
     "tdl_kl_div_softmax": [_P, _P, _I, _I, _P, _P],

@@ -6,6 +6,7 @@ i.e. (max - min) / 2048); the CPU path is exact (numpy definitions).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import List, Optional, Sequence, Tuple
 
@@ -391,7 +392,23 @@ def kl_div_softmax(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 
 
 def cosine_gram(xs: List[torch.Tensor]) -> torch.Tensor:
-    """N x N cosine similarity of flattened tensors (MFMA GEMM via hipBLASLt on GPU)."""
+    """N x N cosine similarity of flattened tensors (K6).  GPU: the native two-phase kernel reads
+    the N tensors in place through a pointer table (no stacked copy; fp64 accumulation, fixed
+    reduction order); CPU / unusual inputs: the torch reference."""
+    n = len(xs)
+    if n and all(x.is_cuda for x in xs) and n <= 16:
+        flat = [x.detach().reshape(-1) for x in xs]
+        D = flat[0].numel()
+        dt = flat[0].dtype
+        if dt in (torch.float32, torch.bfloat16) and all(f.numel() == D and f.dtype == dt and f.is_contiguous()
+                                                          for f in flat):
+            dev = flat[0].device
+            out = torch.empty(n, n, dtype=torch.float32, device=dev)
+            ws = _workspace(dev, int(_lib.lib().tdl_gram_ws_bytes()))
+            table = (ctypes.c_void_p * n)(*[f.data_ptr() for f in flat])
+            _lib.call("tdl_cosine_gram", ctypes.cast(table, ctypes.c_void_p), n, D, _lib.DTYPE_CODE[dt], ptr(out),
+                      ptr(ws), stream_ptr(dev))
+            return out
     X = torch.stack([x.detach().float().reshape(-1) for x in xs])
     nrm = X.norm(dim=1).clamp(min=1e-30)
     G = X @ X.t()
