@@ -920,6 +920,216 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
     }
 }
 
+
+// ============================================================================ ping-pong kernel
+// 256 x 256 x 64 tile, 8 waves as 2 (m) x 4 (n), 128 x 64 per wave (as gemm_kernel), but the two
+// wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7; one wave of each per SIMD) run STAGGERED by one
+// barrier: while one wave of a SIMD runs its 16-MFMA cluster, its partner issues the next phase's
+// fragment reads and LDS-DMA copies, so the copy-issue cost (the limiter of gemm_kernel /
+// gemm_persistent8: profiles/r2_gemm_variants.jsonl) hides behind the partner's MFMAs
+// (cdna_hip_programming.md, "The 256² 8-phase template").
+//
+// A K step is four phases, one output quadrant (4 m-tiles x 2 n-tiles x K 64 = 16 MFMAs) each:
+//   P1 q(mh0, nh0): read A(mh0), B(nh0)   issue UB1(t+1)
+//   P2 q(mh0, nh1): read B(nh1)           issue UA1(t+1)
+//   P3 q(mh1, nh1): read A(mh1)           issue UA0(t+2)
+//   P4 q(mh1, nh0): (B(nh0) still held)   issue UB0(t+2)
+// LDS holds each operand tile as quarter units of 128 rows x 64 k (16 KiB, same swizzled 128-B
+// rows as gemm_kernel), double-buffered PER UNIT (t & 1):
+//   UA0 = A rows {0-63, 128-191} (each group's m-half 0), UA1 = A rows {64-127, 192-255},
+//   UB0 = B rows {64 wc + 0..31}, UB1 = B rows {64 wc + 32..63}.
+// Ordering (global phase index g; group 0 reads phase g between barriers 2g-2 and 2g-1, group 1
+// between 2g-1 and 2g; both retire their reads with lgkmcnt(0) after the next barrier):
+//   WAR: a copy issued in phase g may overwrite data last read in phase <= g-2 — each unit of
+//        tile t+1 / t+2 above overwrites its tile-(t-1) / tile-t copy >= 2 phases after that read;
+//   RAW: each wave keeps the copies of its last 4 phases in flight (s_waitcnt vmcnt(2 x issued
+//        copies in phases g-3..g) before phase g's first barrier), so a unit issued in phase g is
+//        readable from phase g+5 on — every unit is read >= 5 phases after its issue.
+template <bool TA, bool TB, int EPI, int ABL = 0>
+__global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
+    // ABL (timing-only ablations, wrong results): 1 = no copies in the K loop, 2 = no fragment
+    // reads in the K loop, 4 = no waits / barriers in the K loop, 8 = no epilogue stores
+    static_assert(!TA && !TB, "ping-pong kernel: k-contiguous operands only");
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // [buf 2][UA0 UA1 UB0 UB1][16 KiB]
+    constexpr int UNIT = 16384, BUF = 4 * UNIT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    const int wg = xcd_remap(blockIdx.x, p.tiles);
+    const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = blockIdx.y * p.k_per_split;
+    const int nk = p.k_per_split / BK;  // >= 2 (host)
+
+    // copy lanes: piece = 8 rows x 128 B; lane -> row lr, LDS slot (lane & 7) holds global chunk ch
+    const int lr = lane >> 3, ch = (lane & 7) ^ lr;
+    // A unit mh, piece i (rows 64 i + 8 w + lr of the unit) = A row mh*64 + 128 i + 8 w + lr
+    const uint32_t a_off = (uint32_t)((8 * w + lr) * p.lda + 8 * ch) * 2u;
+    const uint32_t a_dmh = 64u * (uint32_t)p.lda * 2u, a_di = 128u * (uint32_t)p.lda * 2u;
+    // B unit nh, piece i = B row 64 (2 i + (w >> 2)) + 32 nh + 8 (w & 3) + lr
+    const uint32_t b_off = (uint32_t)((64 * (w >> 2) + 8 * (w & 3) + lr) * p.ldb + 8 * ch) * 2u;
+    const uint32_t b_dnh = 32u * (uint32_t)p.ldb * 2u, b_di = 128u * (uint32_t)p.ldb * 2u;
+    auto rsrc = [&](const bf16_t* G, int ld, int r0, int rmax, int k0) {
+        const long long rem = ((long long)(rmax - r0) * ld - k0) * 2;
+        return make_rsrc(G + (size_t)r0 * ld + k0, rem);
+    };
+    // unit u (0 UA0, 1 UA1, 2 UB0, 3 UB1) of K step t -> LDS buffer t & 1
+    auto issue = [&](int u, int t) {
+        const int k0 = kbeg + t * BK;
+        char* dst = smem + (t & 1) * BUF + u * UNIT + w * 1024;
+        const bool isA = u < 2;
+        const __amdgpu_buffer_rsrc_t r = isA ? rsrc(p.A, p.lda, m0, p.M, k0) : rsrc(p.B, p.ldb, n0, p.N, k0);
+        uint32_t o = isA ? a_off + (uint32_t)u * a_dmh : b_off + (uint32_t)(u - 2) * b_dnh;
+        const uint32_t di = isA ? a_di : b_di;
+        asm volatile("" : "+v"(o));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, o, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(dst + 8 * 1024), 16, o + di, 0, 0, 0);
+    };
+    auto frag_ = [&](const char* U, int r, int ks) {
+        const int c = 4 * ks + (lane >> 4);
+        return *(const bf16x8_t*)(U + r * 128 + ((c ^ (r & 7)) << 4));
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t FA[4][2], FB0[2][2], FB1[2][2];
+
+    auto readA = [&](int buf, int mh) {
+        const char* U = smem + buf * BUF + mh * UNIT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) FA[i][ks] = frag_(U, wr * 64 + 16 * i + (lane & 15), ks);
+    };
+    auto readB = [&](bf16x8_t (&F)[2][2], int buf, int nh) {
+        const char* U = smem + buf * BUF + (2 + nh) * UNIT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) F[j][ks] = frag_(U, wc * 32 + 16 * j + (lane & 15), ks);
+    };
+    auto quad = [&](const bf16x8_t (&F)[2][2], int mh, int nh) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[4 * mh + i][2 * nh + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[j][ks], FA[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
+    };
+    auto wait_vm = [&](int n) {
+        switch (n) {  // wave-uniform compile-time in practice (unrolled phases)
+            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        }
+    };
+    // one phase: [reads] [copies] vmcnt(n) barrier lgkmcnt(0) | MFMA cluster | barrier
+    auto phase_sync = [&](int n) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(ABL & 4)) {
+            wait_vm(n);
+            __builtin_amdgcn_s_barrier();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+    };
+    auto phase_end = [&]() {
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // K step t with this step's / the previous step's issue masks (bit q-1: phase q issues)
+    auto step = [&](int t, auto pmc, auto mc) {
+        constexpr int PM = decltype(pmc)::value, MK = decltype(mc)::value;
+        auto vm = [](int q) {  // copies allowed in flight before phase q's barrier: phases q-3..q
+            int n = 0;
+            for (int d = 0; d < 4; ++d) {
+                const int x = q - d;  // <= 0: phase x + 4 of the previous step
+                n += (x >= 1 ? (MK >> (x - 1)) & 1 : (PM >> (x + 3)) & 1) ? 2 : 0;
+            }
+            return n;
+        };
+        const int cur = t & 1;
+        constexpr bool RD = !(ABL & 2), CP = !(ABL & 1);
+        // P1
+        if (RD) readA(cur, 0);
+        if (RD) readB(FB0, cur, 0);
+        if (CP && (MK & 1)) issue(3, t + 1);
+        phase_sync(vm(1));
+        quad(FB0, 0, 0);
+        phase_end();
+        // P2
+        if (RD) readB(FB1, cur, 1);
+        if (CP && (MK & 2)) issue(1, t + 1);
+        phase_sync(vm(2));
+        quad(FB1, 0, 1);
+        phase_end();
+        // P3
+        if (RD) readA(cur, 1);
+        if (CP && (MK & 4)) issue(0, t + 2);
+        phase_sync(vm(3));
+        quad(FB1, 1, 1);
+        phase_end();
+        // P4
+        if (CP && (MK & 8)) issue(2, t + 2);
+        phase_sync(vm(4));
+        quad(FB0, 1, 0);
+        phase_end();
+    };
+
+    if (p.rotate > 1 && blockIdx.x < (unsigned)p.splits) {
+        // desynchronise the first round of workgroups (later rounds inherit the offsets), so the
+        // CUs' epilogue store bursts do not all land at the same time (p.splits = CU count here)
+        const int n = (int)((blockIdx.x >> 3) & 15) * p.rotate;
+        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+    // prologue: UA0(0) UB0(0) UB1(0) UA1(0) UA0(1) UB0(1) (the copies of "phases" -5..0)
+    issue(0, 0);
+    issue(2, 0);
+    issue(3, 0);
+    issue(1, 0);
+    issue(0, 1);
+    issue(2, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // UA0(0), UB0(0) landed
+    __builtin_amdgcn_s_barrier();
+    if (wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+    if (ABL & 2) {
+        readA(0, 0);
+        readB(FB0, 0, 0);
+        readB(FB1, 0, 1);
+    }
+    using I15 = std::integral_constant<int, 15>;
+    using I3 = std::integral_constant<int, 3>;
+    using I0 = std::integral_constant<int, 0>;
+    int t = 0;
+#pragma clang loop unroll(disable)
+    for (; t < nk - 2; ++t) step(t, I15{}, I15{});
+    step(t, I15{}, I3{});      // t = nk-2: P3 / P4 have no step t+2
+    step(t + 1, I3{}, I0{});   // t = nk-1: nothing left to stage
+
+    if (ABL & 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else {
+        auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
+        GemmParams q = p;
+        if (ABL & 16) q.M = 0;  // ablation: every store falls outside the buffer (issued, dropped)
+        epilogue_store<EPI, 4>(q, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
+    }
+    if (!wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
+}
+
 }  // namespace
 
 // C = epilogue(A x B^T) (see the header for the storage flags and epilogue codes).
@@ -930,7 +1140,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
 // schedule (default: the fastest of these on MI355X, profiles/r2_gemm_variants.jsonl), 1 = its plain
 // schedule, 2..9 = its NT bf16 schedule variants, 11 = the persistent 4-wave kernel, 12 = the
 // persistent 8-wave kernel (register-staged producer), 13..18 its timing-only ablations, 19 = 12
-// without the per-XCD K rotation (11..19: NT bf16 only).
+// without the per-XCD K rotation (11..19: NT bf16 only), 20 = the ping-pong kernel (NT, every
+// epilogue), 21..28 its timing-only ablations (NT bf16).
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -976,6 +1187,40 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         TDL_LAUNCH_CHECK();
     }
     const dim3 grid(p.tiles, split);
+    if (variant >= 21 && variant <= 28 && !ta && !tb && epi == 0 && kps / BK >= 2) {  // pp ablations
+        switch (variant) {
+            case 21: gemm_pp<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;   // no copies
+            case 22: gemm_pp<false, false, 0, 2><<<grid, NTHR, 0, s>>>(p); break;   // no frag reads
+            case 23: gemm_pp<false, false, 0, 3><<<grid, NTHR, 0, s>>>(p); break;   // MFMA + sync
+            case 24: gemm_pp<false, false, 0, 7><<<grid, NTHR, 0, s>>>(p); break;   // MFMA only
+            case 25: gemm_pp<false, false, 0, 8><<<grid, NTHR, 0, s>>>(p); break;   // no epilogue
+            case 26: gemm_pp<false, false, 0, 15><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only, no epilogue
+            case 28: gemm_pp<false, false, 0, 16><<<grid, NTHR, 0, s>>>(p); break;  // stores dropped
+            default: gemm_pp<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;   // no sync
+        }
+        TDL_LAUNCH_CHECK();
+    }
+    if (variant >= 29 && variant <= 34 && !ta && !tb && split == 1 && kps / BK >= 2) {  // start-delay sweep
+        p.rotate = 1 << (variant - 28);  // sleep units of 64 cycles per delay level (16 levels)
+        p.splits = num_cus();
+        switch (epi) {
+            case 0: gemm_pp<false, false, 0><<<grid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, 1><<<grid, NTHR, 0, s>>>(p); break;
+        }
+        TDL_LAUNCH_CHECK();
+    }
+    if (variant == 20 && !ta && !tb && kps / BK >= 2) {  // ping-pong kernel (NT)
+        switch (epi) {
+            case 0: gemm_pp<false, false, 0><<<grid, NTHR, 0, s>>>(p); break;
+            case 1: gemm_pp<false, false, 1><<<grid, NTHR, 0, s>>>(p); break;
+            case 2: gemm_pp<false, false, 2><<<grid, NTHR, 0, s>>>(p); break;
+            case 3: gemm_pp<false, false, 3><<<grid, NTHR, 0, s>>>(p); break;
+            case 4: gemm_pp<false, false, 4><<<grid, NTHR, 0, s>>>(p); break;
+            case 5: gemm_pp<false, false, 5><<<grid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, 6><<<grid, NTHR, 0, s>>>(p); break;
+        }
+        TDL_LAUNCH_CHECK();
+    }
     if (variant >= 2 && variant <= 9) {  // schedule variants of the 8-wave kernel (NT, bf16 out only)
         if (ta || tb || epi != 0) return (int)hipErrorInvalidValue;
         switch (variant) {

@@ -74,6 +74,35 @@ def test_bias_gelu_resadd_dgelu():
     assert _rel(colsum, gr.sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 200, 128), (520, 1032, 1024), (4096, 512, 192)])
+def test_pingpong_variant_epilogues(M, N, K):
+    """tdl_gemm variant 20 (staggered two-group ping-pong schedule, NT operands) against fp32 torch,
+    ragged M / N, the shortest K it takes (two K steps) and every epilogue it shares."""
+    from trustworthy_dl.ops import gemm
+    x = _rand(M, K)
+    wt = _rand(N, K, scale=0.1)        # [N, K] storage: NT (forward with the W^T copy / dgrad)
+    bias = _rand(N, scale=0.5)
+    ref = x.float() @ wt.float().t()
+    old = gemm.VARIANT
+    gemm.VARIANT = 20
+    try:
+        y = gemm.matmul(x, wt.t(), bias=bias)
+        assert _rel(y, ref + bias.float()) < 1e-2
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        f = gemm.matmul(x, wt.t(), bias=bias, epi="gelu", aux=pre)
+        assert _rel(pre, ref + bias.float()) < 1e-2
+        assert _rel(f, F.gelu(ref + bias.float(), approximate="tanh")) < 1e-2
+        res = _rand(M, N)
+        out = res.clone()
+        gemm.matmul(x, wt.t(), out=out, epi="resadd")
+        assert _rel(out, res.float() + ref) < 1e-2
+        acc = torch.ones(M, N, device=DEV)
+        gemm._launch(x, wt.t(), acc, N, "f32acc")
+        assert _rel(acc, ref + 1.0) < 1e-4
+    finally:
+        gemm.VARIANT = old
+
+
 @pytest.mark.parametrize("mode,split", [("slab", None), ("atomic", 4), ("slab", 1), ("slab", 3)])
 def test_wgrad_f32(mode, split):
     from trustworthy_dl.ops import gemm

@@ -27,7 +27,8 @@ EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f3
 BK = 64
 # A/B switch for benchmarks: 0 = shipped kernel (8-wave, pipelined), 1 = plain (unpipelined)
 # schedule, >= 2 = schedule variants / persistent kernels of tdl_gemm (NT, bf16 out only; some are
-# timing-only ablations: csrc/gemm.hip tdl_gemm)
+# timing-only ablations), 20 = the staggered ping-pong kernel (NT, every epilogue), 21..28 its
+# timing-only ablations (csrc/gemm.hip tdl_gemm; profiles/r2_gemm_pingpong_ablation.jsonl)
 VARIANT = 0
 
 
