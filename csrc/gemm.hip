@@ -1086,12 +1086,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         phase_end();
     };
 
-    if (p.rotate > 1 && blockIdx.x < (unsigned)p.splits) {
-        // desynchronise the first round of workgroups (later rounds inherit the offsets), so the
-        // CUs' epilogue store bursts do not all land at the same time (p.splits = CU count here)
-        const int n = (int)((blockIdx.x >> 3) & 15) * p.rotate;
-        for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
-    }
     // prologue: UA0(0) UB0(0) UB1(0) UA1(0) UA0(1) UB0(1) (the copies of "phases" -5..0)
     issue(0, 0);
     issue(2, 0);
@@ -1197,15 +1191,6 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
             case 26: gemm_pp<false, false, 0, 15><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only, no epilogue
             case 28: gemm_pp<false, false, 0, 16><<<grid, NTHR, 0, s>>>(p); break;  // stores dropped
             default: gemm_pp<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;   // no sync
-        }
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant >= 29 && variant <= 34 && !ta && !tb && split == 1 && kps / BK >= 2) {  // start-delay sweep
-        p.rotate = 1 << (variant - 28);  // sleep units of 64 cycles per delay level (16 levels)
-        p.splits = num_cus();
-        switch (epi) {
-            case 0: gemm_pp<false, false, 0><<<grid, NTHR, 0, s>>>(p); break;
-            default: gemm_pp<false, false, 1><<<grid, NTHR, 0, s>>>(p); break;
         }
         TDL_LAUNCH_CHECK();
     }
