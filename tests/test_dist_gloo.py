@@ -148,7 +148,9 @@ def _reshard_worker(rank, world, port, out_path):
     eng.cfg.shadow_interval = 2
     rec = _reshard_run(eng, _make_batches("gpt2-tiny", 6, 8), rank == 1)
     res = {"rank": rank, "sums": _layer_sums(eng), "restored": {str(k): v for k, v in rec["restored_from_shadow"].items()},
-           "plan": eng.plan.ranks, "last_loss": eng.last_loss}
+           "plan": eng.plan.ranks, "last_loss": eng.last_loss, "link_measured": eng.link_meter.measured(),
+           "link_bw": eng.link_meter.bytes_per_s(), "est": rec["estimated_migration_time"],
+           "moved": rec["moved_params"]}
     with open(f"{out_path}.{rank}", "w") as f:
         json.dump(res, f)
     dist.barrier()
@@ -171,6 +173,10 @@ def test_distributed_reshard_restores_from_shadow_and_matches_local():
     got = {}
     for r in res:
         assert r["restored"] == {"1": 4} and r["plan"] == [0, 2]
+        # the migration estimate comes from this job's measured transfers (shadow snapshots), not
+        # from the prior, and is consistent with it: moved params x 12 B / measured B/s
+        assert r["link_measured"] and r["link_bw"] != 2e9
+        assert r["est"] == pytest.approx(r["moved"] * 12 / r["link_bw"] + 1e-3, rel=0.5)
         got.update({int(k): v for k, v in r["sums"].items()})
     assert rec["restored_from_shadow"] == {1: 4}
     assert sorted(got) == sorted(ref)

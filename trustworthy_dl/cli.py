@@ -33,6 +33,9 @@ def main(argv=None):
     p.add_argument("--attack", action="store_true")
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--heartbeat", type=float, default=None, help="seconds between liveness beats (0 = off)")
+    p.add_argument("--heartbeat-timeout", type=float, default=None, help="silence (s) after which a peer is OFFLINE")
+    p.add_argument("--checkpoint-interval", type=int, default=None, help="optimizer steps between checkpoints")
+    p.add_argument("--dtype", type=str, default=None, choices=["bf16", "fp32"], help="compute dtype")
     p.add_argument("--abort-on-offline", action="store_true",
                    help="exit non-zero when a peer goes OFFLINE; restart the job with --resume latest "
                         "on the surviving ranks (the checkpoint is re-planned over them)")
@@ -48,6 +51,8 @@ def main(argv=None):
             "num_epochs": a.epochs, "batch_size": a.batch_size, "learning_rate": a.lr, "seq_len": a.seq_len,
             "micro_batches": a.micro_batches, "batches_per_epoch": a.batches_per_epoch,
             "checkpoint_dir": a.checkpoint_dir, "device": a.device, "heartbeat_interval": a.heartbeat,
+            "heartbeat_timeout": a.heartbeat_timeout, "checkpoint_interval": a.checkpoint_interval,
+            "compute_dtype": a.dtype,
             "abort_on_offline": True if a.abort_on_offline else None}
     if a.config:
         cfg, atk, _ = load_config(a.config, over)

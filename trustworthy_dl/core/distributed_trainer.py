@@ -26,6 +26,7 @@ from ..config import TrainingConfig
 from ..models import get_model
 from ..parallel.flat import AdamWConfig
 from ..parallel.pipeline import EngineConfig, PipelineEngine
+from ..runtime import faults
 from ..security.attack_detection import AttackDetector
 from ..security.gradient_verification import GradientVerifier
 from ..utils.metrics import MetricsCollector
@@ -70,6 +71,7 @@ class DistributedTrainer:
         self.config = config
         self.training_state = TrainingState.INITIALIZING
         self.current_epoch = 0
+        self.epoch_batch = 0          # batches of current_epoch already trained (resume position)
         self.trust_manager = trust_manager or TrustManager(num_nodes=config.num_nodes,
                                                            trust_threshold=config.trust_threshold)
         self.node_monitor = NodeMonitor()
@@ -322,10 +324,16 @@ class DistributedTrainer:
         self.engine.epoch = epoch
         losses = []
         limit = self.config.batches_per_epoch
+        skip, self.epoch_batch = self.epoch_batch, 0  # resumed mid-epoch: those batches are done
         for batch_idx, batch in enumerate(dataloader):
             if limit is not None and batch_idx >= limit:
                 break
+            if batch_idx < skip:
+                self.epoch_batch = batch_idx + 1
+                continue
             loss = self.engine.train_step(batch)
+            self.epoch_batch = batch_idx + 1
+            faults.maybe_inject(self.engine.rank, self.global_step, self.engine.heartbeat)
             if loss is not None:
                 losses.append(loss)
             if self.engine.state_flags.get("under_attack") and self.training_state == TrainingState.TRAINING:
@@ -337,6 +345,7 @@ class DistributedTrainer:
         last = self.engine.flush()
         if last is not None and (not losses or losses[-1] != last):
             losses.append(last)
+        self.epoch_batch = 0
         self._sync_partitions()
         avg = float(np.mean(losses)) if losses else float("nan")
         logger.info("Epoch %d completed. Average loss: %.4f", epoch, avg)
@@ -364,7 +373,8 @@ class DistributedTrainer:
         logger.info("Starting training for %d epochs", num_epochs)
         self.training_state = TrainingState.TRAINING
         history = []
-        for epoch in range(num_epochs):
+        # a resumed job continues at the saved epoch (and, inside it, after the saved batch)
+        for epoch in range(self.current_epoch, num_epochs):
             avg = self.train_epoch(train_dataloader, epoch)
             rec = {"epoch": epoch, "train_loss": avg}
             if val_dataloader is not None:

@@ -99,11 +99,84 @@ def broadcast_ints(values: Optional[Sequence[int]], src: int, device, max_len: i
     return [int(v) for v in buf[1:1 + n].tolist()]
 
 
-def batched_transfer(sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]], group=None):
+class LinkMeter:
+    """Measured point-to-point throughput of this rank's own bulk transfers (shadow snapshots and
+    re-shard migrations: SURVEY 2.7 P5), replacing the reference's fixed 1 GiB/s + 2 s guess
+    (distributed_trainer.py:354-365) in ``estimate_migration_time``.
+
+    A sample is (bytes on the busiest peer link, seconds).  On GPU the interval is bracketed by HIP
+    events on the current stream and harvested lazily (``event.query()``), so measuring never
+    blocks the host; on CPU (gloo) the transfer is synchronous and wall time is used."""
+
+    def __init__(self, prior_bytes_per_s: float, keep: int = 16):
+        self.prior = float(prior_bytes_per_s)
+        self.keep = keep
+        self.samples: List[Tuple[float, float]] = []
+        self._pending: List[Tuple[object, object, float]] = []
+
+    def begin(self, device: torch.device):
+        if device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ("cuda", ev)
+        return ("host", time.perf_counter())
+
+    def end(self, token, link_bytes: float):
+        if link_bytes <= 0:
+            return
+        kind, start = token
+        if kind == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._pending.append((start, ev, float(link_bytes)))
+        else:
+            self._add(float(link_bytes), time.perf_counter() - start)
+
+    def _add(self, nbytes: float, seconds: float):
+        if seconds > 0:
+            self.samples.append((nbytes, seconds))
+            del self.samples[:-self.keep]
+
+    def _harvest(self):
+        left = []
+        for start, stop, nbytes in self._pending:
+            if stop.query():
+                self._add(nbytes, start.elapsed_time(stop) * 1e-3)
+            else:
+                left.append((start, stop, nbytes))
+        self._pending = left
+
+    def bytes_per_s(self) -> float:
+        """Per-link throughput: total bytes / total seconds of the recent samples (large transfers
+        dominate, as they should for a migration estimate); the prior until something was measured."""
+        self._harvest()
+        if not self.samples:
+            return self.prior
+        return sum(b for b, _ in self.samples) / sum(t for _, t in self.samples)
+
+    def measured(self) -> bool:
+        self._harvest()
+        return bool(self.samples)
+
+
+def _link_bytes(sends, recvs) -> float:
+    per_peer = {}
+    for t, peer in list(sends) + list(recvs):
+        per_peer[peer] = per_peer.get(peer, 0) + t.numel() * t.element_size()
+    return float(max(per_peer.values())) if per_peer else 0.0
+
+
+def batched_transfer(sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]], group=None,
+                     meter: Optional[LinkMeter] = None):
     """Post every send and receive of a redistribution in ONE group (RCCL runs them on all xGMI
-    links concurrently; the ordering problem of pairwise blocking send/recv disappears)."""
+    links concurrently; the ordering problem of pairwise blocking send/recv disappears).  With a
+    ``meter`` the transfer's throughput on its busiest link is recorded."""
     ops = [dist.P2POp(dist.isend, t.contiguous(), peer, group) for t, peer in sends]
     ops += [dist.P2POp(dist.irecv, t, peer, group) for t, peer in recvs]
     if ops:
+        dev = (sends or recvs)[0][0].device
+        tok = meter.begin(dev) if meter is not None else None
         for r in dist.batch_isend_irecv(ops):
             r.wait()
+        if meter is not None:
+            meter.end(tok, _link_bytes(sends, recvs))

@@ -38,7 +38,7 @@ from ..ops import stats as dstats
 from ..ops.layers import bump_weight_generation
 from ..ops.layers import defer_weight_grads
 from ..runtime.tracing import PhaseTracer
-from .comm import P2PComm, all_gather_rows, batched_transfer, broadcast_ints
+from .comm import LinkMeter, P2PComm, all_gather_rows, batched_transfer, broadcast_ints
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
 from .stage import Stage, tied_groups
@@ -68,6 +68,7 @@ class EngineConfig:
     output_check: str = "random"         # which micro-batch output is monitored each step: "random" (a
                                          # per-step choice from a private seeded RNG, so an attacker
                                          # cannot predict which output is inspected) | "first" | "none"
+    monitor_seed: Optional[int] = None   # seed of that RNG (None: from os.urandom; tests pin it)
     early_grad_stats: bool = True        # start each layer's gradient statistics on the side stream
                                          # as soon as its last-micro-batch backward is done
     compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
@@ -155,7 +156,8 @@ class PipelineEngine:
         self._comm_wait = 0.0
         self._step_time = 0.0
         # private per-process RNG for the monitored micro-batch (not derived from the data seed)
-        self._mon_rng = __import__("random").Random(int.from_bytes(os.urandom(8), "little"))
+        seed = cfg.monitor_seed if cfg.monitor_seed is not None else int.from_bytes(os.urandom(8), "little")
+        self._mon_rng = __import__("random").Random(seed)
         self._mon_idx = 0
 
         if cfg.device == "auto":
@@ -178,6 +180,7 @@ class PipelineEngine:
         self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
         self._init_trust_state()
         self._build()
+        self.link_meter = LinkMeter(150e9 if self.device.type == "cuda" else 2e9)
         self.heartbeat = None
         self.node_events: List[Dict] = []
         self.quarantine_on_evidence = cfg.quarantine and cfg.pipeline_quarantine
@@ -1186,9 +1189,12 @@ class PipelineEngine:
 
     # ================================================================== re-sharding (task reassignment)
     def estimate_migration_time(self, layer_numel: int, links: int = 1) -> float:
-        """Measured-model estimate: xGMI ~ 150 GB/s per link (vs the reference's 1 GiB/s + 2 s,
-        distributed_trainer.py:354-365).  fp32 master + 2 AdamW moments = 12 B/param."""
-        bw = 150e9 * max(1, links) if self.device.type == "cuda" else 2e9
+        """Seconds to move ``layer_numel`` parameters' fp32 master + 2 AdamW moments (12 B/param)
+        over ``links`` peer links at the per-link throughput MEASURED on this job's own bulk
+        transfers (shadow snapshots, earlier migrations: ``comm.LinkMeter``); before the first
+        measurement, a prior of one xGMI link (~150 GB/s; gloo: 2 GB/s).  The reference uses a fixed
+        1 GiB/s + 2 s (distributed_trainer.py:354-365)."""
+        bw = self.link_meter.bytes_per_s() * max(1, links)
         return layer_numel * 12 / bw + 1e-3
 
     def reassign(self, compromised: Sequence[int], step: Optional[int] = None):
@@ -1306,7 +1312,7 @@ class PipelineEngine:
                     packed[li] = buf
                 if src != dst:
                     moved += self._layer_numel(li)
-            batched_transfer(sends, recvs)
+            batched_transfer(sends, recvs, meter=self.link_meter)
             step_t = torch.tensor([float(step_count)], device=self.device)
             dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
             step_count = int(step_t.item())
@@ -1389,7 +1395,7 @@ class PipelineEngine:
             vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
             buf = torch.empty(sum(self._packed_numel(li) for li in range(a, b)), dtype=torch.float32,
                               device=self.device)
-            batched_transfer([(vec, self._shadow_holder(self.rank))], [(buf, pred)])
+            batched_transfer([(vec, self._shadow_holder(self.rank))], [(buf, pred)], meter=self.link_meter)
             self._shadow_pend[pred] = (step, buf)
         else:
             for node, st in self.stages.items():

@@ -41,6 +41,20 @@ class HeartbeatMonitor:
         self._thread: Optional[threading.Thread] = None
         self.events = []
 
+    def _report_offline(self):
+        """Tell the elastic supervisor (runtime/elastic.py) whom this rank saw go silent: the vote
+        that separates the lost ranks from the ones that merely went down with them."""
+        d = os.environ.get("TDL_ELASTIC_REPORT_DIR")
+        if not d:
+            return
+        try:
+            import json
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, f"offline.rank{self.rank}.json"), "w") as f:
+                json.dump(sorted(self._offline), f)
+        except OSError as exc:
+            logger.error("heartbeat: could not write the offline report: %s", exc)
+
     def _key(self, r: int) -> str:
         return f"{self.prefix}/{r}"
 
@@ -71,6 +85,7 @@ class HeartbeatMonitor:
                         self.on_offline(r)
                     if self.abort_on_offline:
                         logger.error("heartbeat: aborting (fail-fast) so the elastic launcher can restart")
+                        self._report_offline()
                         os._exit(17)
                 self._last_change.setdefault(r, now)
 

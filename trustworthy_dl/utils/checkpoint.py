@@ -36,6 +36,7 @@ def _base_dict(trainer) -> Dict:
     e = trainer.engine
     return {
         "epoch": trainer.current_epoch,
+        "epoch_batch": int(getattr(trainer, "epoch_batch", 0)),  # batches of `epoch` already trained
         "global_step": e.global_step,
         "trust_scores": {i: trainer.trust_manager.get_trust_score(i) for i in range(trainer.config.num_nodes)},
         "attack_history": _jsonable(e.attack_history),
@@ -47,6 +48,13 @@ def _base_dict(trainer) -> Dict:
         "detector": _jsonable(trainer.attack_detector.state_dict()),
         "config": _jsonable(asdict(trainer.config)),
     }
+
+
+def _atomic_save(obj, path: str):
+    """write-then-rename: a process killed mid-write never leaves a truncated file under `path`"""
+    tmp = f"{path}.tmp{os.getpid()}"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
 
 
 def save_checkpoint(trainer, path: Optional[str] = None) -> str:
@@ -61,16 +69,19 @@ def save_checkpoint(trainer, path: Optional[str] = None) -> str:
     if not e.distributed:
         ck = _base_dict(trainer)
         ck.update(parts)
-        torch.save(ck, path)
+        _atomic_save(ck, path)
     else:
         shard = path.replace(".pt", f".rank{e.rank}.pt")
-        torch.save({"rank": e.rank, **parts}, shard)
+        _atomic_save({"rank": e.rank, **parts}, shard)
+        ck = _base_dict(trainer) if e.rank == 0 else None
+        # the manifest is written only once every shard is on disk (a rank lost mid-save leaves no
+        # manifest, so `latest_checkpoint` falls back to the previous complete checkpoint)
+        dist.barrier()
         if e.rank == 0:
-            ck = _base_dict(trainer)
             ck["model_partitions"] = {}
             ck["optimizers"] = {}
             ck["shards"] = [os.path.basename(path.replace(".pt", f".rank{r}.pt")) for r in range(e.world)]
-            torch.save(ck, path)
+            _atomic_save(ck, path)
         dist.barrier()
     logger.info("Checkpoint saved: %s", path)
     return path
@@ -207,6 +218,7 @@ def load_checkpoint(trainer, path: str):
                 "to_nodes": list(new_plan.ranks)})
     e.global_step = int(ck["global_step"])
     trainer.current_epoch = int(ck["epoch"])
+    trainer.epoch_batch = int(ck.get("epoch_batch", 0))
     hist = list(ck.get("reassignment_history", []))
     e.attack_history[:] = list(ck.get("attack_history", []))
     e.reassignment_history[:] = hist + [r for r in e.reassignment_history if r.get("event") == "resume_replan"]
@@ -217,8 +229,20 @@ def load_checkpoint(trainer, path: str):
     logger.info("Checkpoint loaded: %s (step %d, plan %s)", path, e.global_step, e.plan.describe())
 
 
+def is_complete(path: str) -> bool:
+    """A manifest whose listed shards all exist (or a local single-file checkpoint)."""
+    try:
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+    except Exception as exc:  # truncated / unreadable
+        logger.warning("checkpoint %s unreadable: %s", path, exc)
+        return False
+    return all(os.path.exists(os.path.join(os.path.dirname(path), sh)) for sh in ck.get("shards", []))
+
+
 def latest_checkpoint(ckdir: str) -> Optional[str]:
-    files = [f for f in glob.glob(os.path.join(ckdir, "checkpoint_step_*.pt")) if ".rank" not in f]
-    if not files:
-        return None
-    return max(files, key=lambda f: int(f.rsplit("_", 1)[1].split(".")[0]))
+    """Newest COMPLETE checkpoint in ``ckdir`` (every listed shard present), or None."""
+    files = [f for f in glob.glob(os.path.join(ckdir, "checkpoint_step_*.pt")) if ".rank" not in f and ".tmp" not in f]
+    for f in sorted(files, key=lambda f: int(f.rsplit("_", 1)[1].split(".")[0]), reverse=True):
+        if is_complete(f):
+            return f
+    return None
