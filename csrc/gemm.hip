@@ -949,7 +949,6 @@ template <bool TA, bool TB, int EPI, int ABL = 0>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     // ABL (timing-only ablations, wrong results): 1 = no copies in the K loop, 2 = no fragment
     // reads in the K loop, 4 = no waits / barriers in the K loop, 8 = no epilogue stores
-    static_assert(!TA && !TB, "ping-pong kernel: k-contiguous operands only");
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // [buf 2][UA0 UA1 UB0 UB1][16 KiB]
     constexpr int UNIT = 16384, BUF = 4 * UNIT;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -961,15 +960,43 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     const int kbeg = blockIdx.y * p.k_per_split;
     const int nk = p.k_per_split / BK;  // >= 2 (host)
 
-    // copy lanes: piece = 8 rows x 128 B; lane -> row lr, LDS slot (lane & 7) holds global chunk ch
-    const int lr = lane >> 3, ch = (lane & 7) ^ lr;
-    // A unit mh, piece i (rows 64 i + 8 w + lr of the unit) = A row mh*64 + 128 i + 8 w + lr
-    const uint32_t a_off = (uint32_t)((8 * w + lr) * p.lda + 8 * ch) * 2u;
-    const uint32_t a_dmh = 64u * (uint32_t)p.lda * 2u, a_di = 128u * (uint32_t)p.lda * 2u;
-    // B unit nh, piece i = B row 64 (2 i + (w >> 2)) + 32 nh + 8 (w & 3) + lr
-    const uint32_t b_off = (uint32_t)((64 * (w >> 2) + 8 * (w & 3) + lr) * p.ldb + 8 * ch) * 2u;
-    const uint32_t b_dnh = 32u * (uint32_t)p.ldb * 2u, b_di = 128u * (uint32_t)p.ldb * 2u;
-    auto rsrc = [&](const bf16_t* G, int ld, int r0, int rmax, int k0) {
+    // Per-lane byte offsets of piece 0 of each unit (piece 1 adds the uniform di_a / di_b).
+    //  k-contiguous operand: unit image [128 unit-rows][64 k], 128-B rows, 16-B chunk c of row r at
+    //    c ^ (r & 7); piece = 8 rows; wave w copies unit-rows 8 w + (lane >> 3) (+ 64 for piece 1).
+    //    A unit mh: unit-row u -> A row mh*64 + u (+ 64 when u >= 64)
+    //    B unit nh: unit-row u -> B row 64 (u >> 5) + 32 nh + (u & 31)
+    //  row-contiguous operand (TA / TB: stored [K][ld]): unit image [64 k][128 unit-rows], 256-B
+    //    k-rows (one LDS bank row), 32-B window v of k-row k stored at v ^ fsw(k) (conflict-free
+    //    ds_read_b64_tr_b16: the 8 k-rows a 32-lane half reads land in 8 distinct windows); piece =
+    //    4 k-rows; wave w copies k-rows 4 w + (lane >> 4) (+ 32 for piece 1); a lane's 16-B chunk c
+    //    holds unit-rows 8c..8c+7, clamped into [0, rmax - 8] for ragged M / N.
+    uint32_t uoff[4];
+    uint32_t di_a, di_b;
+    {
+        const int lr = lane >> 3, ch = (lane & 7) ^ lr;
+        const int kr = 4 * w + (lane >> 4);
+        const int cs = (lane & 15) ^ (((lane >> 4) | ((w & 2) << 1)) << 1);  // chunk whose slot is lane & 15
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool isA = u < 2;
+            const bool tr = isA ? TA : TB;
+            const int ld = isA ? p.lda : p.ldb;
+            const int h = isA ? u : u - 2;
+            if (!tr) {
+                const int row = isA ? h * 64 + 8 * w + lr : 64 * (w >> 2) + 32 * h + 8 * (w & 3) + lr;
+                uoff[u] = (uint32_t)(row * ld + 8 * ch) * 2u;
+            } else {
+                const int r0 = isA ? m0 : n0, rmax = isA ? p.M : p.N;
+                int col = isA ? h * 64 + 8 * cs + (cs >= 8 ? 64 : 0) : 64 * (cs >> 2) + 32 * h + 8 * (cs & 3);
+                col = r0 + col + 8 <= rmax ? col : rmax - 8 - r0;
+                uoff[u] = (uint32_t)(kr * ld + col) * 2u;
+            }
+        }
+        di_a = TA ? 32u * (uint32_t)p.lda * 2u : 128u * (uint32_t)p.lda * 2u;
+        di_b = TB ? 32u * (uint32_t)p.ldb * 2u : 128u * (uint32_t)p.ldb * 2u;
+    }
+    auto rsrc = [&](const bf16_t* G, int ld, int r0, int rmax, int k0, bool tr) {
+        if (tr) return make_rsrc(G + (size_t)k0 * ld + r0, 0x7fffffffll);
         const long long rem = ((long long)(rmax - r0) * ld - k0) * 2;
         return make_rsrc(G + (size_t)r0 * ld + k0, rem);
     };
@@ -978,16 +1005,29 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         const int k0 = kbeg + t * BK;
         char* dst = smem + (t & 1) * BUF + u * UNIT + w * 1024;
         const bool isA = u < 2;
-        const __amdgpu_buffer_rsrc_t r = isA ? rsrc(p.A, p.lda, m0, p.M, k0) : rsrc(p.B, p.ldb, n0, p.N, k0);
-        uint32_t o = isA ? a_off + (uint32_t)u * a_dmh : b_off + (uint32_t)(u - 2) * b_dnh;
-        const uint32_t di = isA ? a_di : b_di;
+        const __amdgpu_buffer_rsrc_t r = isA ? rsrc(p.A, p.lda, m0, p.M, k0, TA) : rsrc(p.B, p.ldb, n0, p.N, k0, TB);
+        uint32_t o = uoff[u];
+        const uint32_t di = isA ? di_a : di_b;
         asm volatile("" : "+v"(o));
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, o, 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(dst + 8 * 1024), 16, o + di, 0, 0, 0);
     };
-    auto frag_ = [&](const char* U, int r, int ks) {
-        const int c = 4 * ks + (lane >> 4);
-        return *(const bf16x8_t*)(U + r * 128 + ((c ^ (r & 7)) << 4));
+    // MFMA operand fragment (16 unit-rows from rb x 32 k) of a unit: lane l gets unit-row
+    // rb + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7
+    auto frag_ = [&](const char* U, int rb, int ks, auto trc) -> bf16x8_t {
+        if constexpr (!decltype(trc)::value) {
+            const int r = rb + (lane & 15);
+            const int c = 4 * ks + (lane >> 4);
+            return *(const bf16x8_t*)(U + r * 128 + ((c ^ (r & 7)) << 4));
+        } else {
+            // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group supplies k-row q, columns 4p..4p+3
+            const int q = (lane & 15) >> 2, pp = lane & 3;
+            const int col = rb + 4 * pp;
+            const int kb = 32 * ks + 8 * (lane >> 4) + q, k2 = kb + 4;
+            const short4_t x = tr_read(U + kb * 256 + ((((col >> 3) ^ (fsw(kb) << 1))) << 4) + ((col & 7) << 1));
+            const short4_t y = tr_read(U + k2 * 256 + ((((col >> 3) ^ (fsw(k2) << 1))) << 4) + ((col & 7) << 1));
+            return __builtin_bit_cast(bf16x8_t, (short8_t)__builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
     };
 
     f32x4 acc[8][4];
@@ -1002,14 +1042,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) FA[i][ks] = frag_(U, wr * 64 + 16 * i + (lane & 15), ks);
+            for (int ks = 0; ks < 2; ++ks) FA[i][ks] = frag_(U, wr * 64 + 16 * i, ks, std::integral_constant<bool, TA>{});
     };
     auto readB = [&](bf16x8_t (&F)[2][2], int buf, int nh) {
         const char* U = smem + buf * BUF + (2 + nh) * UNIT;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks) F[j][ks] = frag_(U, wc * 32 + 16 * j + (lane & 15), ks);
+            for (int ks = 0; ks < 2; ++ks) F[j][ks] = frag_(U, wc * 32 + 16 * j, ks, std::integral_constant<bool, TB>{});
     };
     auto quad = [&](const bf16x8_t (&F)[2][2], int mh, int nh) {
 #pragma unroll
@@ -1194,16 +1234,24 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         }
         TDL_LAUNCH_CHECK();
     }
-    if (variant == 20 && !ta && !tb && kps / BK >= 2) {  // ping-pong kernel (NT)
-        switch (epi) {
-            case 0: gemm_pp<false, false, 0><<<grid, NTHR, 0, s>>>(p); break;
-            case 1: gemm_pp<false, false, 1><<<grid, NTHR, 0, s>>>(p); break;
-            case 2: gemm_pp<false, false, 2><<<grid, NTHR, 0, s>>>(p); break;
-            case 3: gemm_pp<false, false, 3><<<grid, NTHR, 0, s>>>(p); break;
-            case 4: gemm_pp<false, false, 4><<<grid, NTHR, 0, s>>>(p); break;
-            case 5: gemm_pp<false, false, 5><<<grid, NTHR, 0, s>>>(p); break;
-            default: gemm_pp<false, false, 6><<<grid, NTHR, 0, s>>>(p); break;
-        }
+    if (variant == 20 && kps / BK >= 2) {  // ping-pong kernel
+#define PP_LAUNCH(TA_, TB_, E_) gemm_pp<TA_, TB_, E_><<<grid, NTHR, 0, s>>>(p)
+#define PP_EPI(TA_, TB_)                       \
+    switch (epi) {                             \
+        case 0: PP_LAUNCH(TA_, TB_, 0); break; \
+        case 1: PP_LAUNCH(TA_, TB_, 1); break; \
+        case 2: PP_LAUNCH(TA_, TB_, 2); break; \
+        case 3: PP_LAUNCH(TA_, TB_, 3); break; \
+        case 4: PP_LAUNCH(TA_, TB_, 4); break; \
+        case 5: PP_LAUNCH(TA_, TB_, 5); break; \
+        default: PP_LAUNCH(TA_, TB_, 6); break; \
+    }
+        if (!ta && !tb) { PP_EPI(false, false) }
+        else if (!ta && tb) { PP_EPI(false, true) }
+        else if (ta && !tb) { PP_EPI(true, false) }
+        else { PP_EPI(true, true) }
+#undef PP_EPI
+#undef PP_LAUNCH
         TDL_LAUNCH_CHECK();
     }
     if (variant >= 2 && variant <= 9) {  // schedule variants of the 8-wave kernel (NT, bf16 out only)

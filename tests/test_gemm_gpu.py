@@ -74,6 +74,28 @@ def test_bias_gelu_resadd_dgelu():
     assert _rel(colsum, gr.sum(0)) < 2e-2
 
 
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (776, 1032, 320)])
+def test_pingpong_variant_layouts(ta, tb, M, N, K):
+    """variant 20 on all four operand storage forms (transposed units read with ds_read_b64_tr_b16),
+    ragged M / N, plus an fp32 split-K weight-gradient accumulation (TA = TB = 1, slabs)."""
+    from trustworthy_dl.ops import gemm
+    a = _view(_rand(M, K), ta)
+    b = _view(_rand(K, N, scale=0.1), tb)
+    old = gemm.VARIANT
+    gemm.VARIANT = 20
+    try:
+        out = gemm.matmul(a, b)
+        assert _rel(out, a.float() @ b.float()) < 1e-2, (ta, tb, M, N, K)
+        if ta and tb:
+            acc = torch.ones(M, N, device=DEV)
+            gemm.matmul_f32_acc(acc, a, b, split=2, mode="slab")
+            assert _rel(acc, a.float() @ b.float() + 1.0) < 1e-4
+    finally:
+        gemm.VARIANT = old
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 200, 128), (520, 1032, 1024), (4096, 512, 192)])
 def test_pingpong_variant_epilogues(M, N, K):
     """tdl_gemm variant 20 (staggered two-group ping-pong schedule, NT operands) against fp32 torch,
