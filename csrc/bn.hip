@@ -124,10 +124,14 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
 
 // ---------------------------------------------------------------- backward pass 1: reductions
 // block = 256 threads = RPB rows x VPB channel-vectors; grid (row chunks, channel-vector groups)
+// ReLU mask: from the stored output (out), or — for a BN whose output was never materialised (its
+// apply + ReLU folded into the next convolution's operand load) — recomputed from x with the same
+// per-channel scale / shift the convolution used (pro = [scale | shift]).
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
                                                                 const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                                 const float* __restrict__ rstd, float* __restrict__ sums,
-                                                                int64_t M, int C, int rows_per_block, int relu) {
+                                                                int64_t M, int C, int rows_per_block, int relu,
+                                                                const float* __restrict__ pro) {
     __shared__ float red[2][256][8];
     const int CV = C >> 3;
     const int VPB = CV < 256 ? CV : 256;
@@ -138,11 +142,13 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
     float sg[8] = {}, sgx[8] = {};
     if (r0 < RPB && cv < CV) {
         const int c0 = cv * 8;
-        float mu[8], rs[8];
+        float mu[8], rs[8], psc[8], psh[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             mu[e] = mean[c0 + e];
             rs[e] = rstd[c0 + e];
+            psc[e] = pro ? pro[c0 + e] : 0.f;
+            psh[e] = pro ? pro[C + c0 + e] : 0.f;
         }
         const int64_t rbeg = (int64_t)blockIdx.x * rows_per_block;
         const int64_t rend = rbeg + rows_per_block < M ? rbeg + rows_per_block : M;
@@ -158,18 +164,21 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
                 const int64_t v = (ok ? rr : r) * CV + cv;
                 dq[u] = ok ? ((const uint4*)dout)[v] : make_uint4(0, 0, 0, 0);
                 xq[u] = ((const uint4*)x)[v];
-                oq[u] = relu ? ((const uint4*)out)[v] : make_uint4(0, 0, 0, 0);
+                oq[u] = (relu && out) ? ((const uint4*)out)[v] : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 float dv[8], xv[8];
                 unpack8(dq[u], dv);
                 unpack8(xq[u], xv);
-                if (relu) {
+                if (relu && out) {
                     float ov[8];
                     unpack8(oq[u], ov);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) dv[e] = ov[e] > 0.f ? dv[e] : 0.f;
+                } else if (relu) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) dv[e] = fmaf(xv[e], psc[e], psh[e]) > 0.f ? dv[e] : 0.f;
                 }
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
@@ -207,7 +216,8 @@ __global__ __launch_bounds__(256) void bn_act_bwd_dx_kernel(const bf16_t* __rest
                                                             const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, const bf16_t* __restrict__ gamma,
                                                             const float* __restrict__ sums, bf16_t* __restrict__ dx,
-                                                            bf16_t* __restrict__ dres, int64_t M, int C, int relu) {
+                                                            bf16_t* __restrict__ dres, int64_t M, int C, int relu,
+                                                            const float* __restrict__ pro) {
     const int CV = C >> 3;
     const float invM = 1.f / (float)M;
     const int64_t nvec = M * CV;
@@ -217,11 +227,14 @@ __global__ __launch_bounds__(256) void bn_act_bwd_dx_kernel(const bf16_t* __rest
         unpack8(((const uint4*)dout)[v], dv);
         unpack8(((const uint4*)x)[v], xv);
         unpack8(*(const uint4*)(gamma + c0), g);
-        if (relu) {
+        if (relu && out) {
             float ov[8];
             unpack8(((const uint4*)out)[v], ov);
 #pragma unroll
             for (int e = 0; e < 8; ++e) dv[e] = ov[e] > 0.f ? dv[e] : 0.f;
+        } else if (relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dv[e] = fmaf(xv[e], pro[c0 + e], pro[C + c0 + e]) > 0.f ? dv[e] : 0.f;
         }
         if (dres) ((uint4*)dres)[v] = pack8(dv);
         float o[8];
@@ -251,6 +264,36 @@ __global__ __launch_bounds__(256) void bn_fold_kernel(float* __restrict__ rep, f
     }
 }
 
+// Training statistics of a BN whose apply + ReLU is folded into the next convolution: mean / rstd
+// (saved for backward), running-statistics update, the per-channel fold pro = [gamma * rstd |
+// beta - mean * gamma * rstd] (fp32), and the zeroed backward reduction buffer — no pass over the
+// activations at all.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, const bf16_t* __restrict__ gamma,
+                                                          const bf16_t* __restrict__ beta, float* __restrict__ save_mean,
+                                                          float* __restrict__ save_rstd, float* __restrict__ upd_mean,
+                                                          float* __restrict__ upd_var, float* __restrict__ pro,
+                                                          float* __restrict__ zero_buf, int64_t zero_n, int64_t M, int C,
+                                                          float eps, float momentum) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += (int64_t)gridDim.x * blockDim.x)
+        zero_buf[i] = 0.f;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float invM = 1.f / (float)M;
+    const float mean = stats[c] * invM;
+    const float var = fmaxf(stats[C + c] * invM - mean * mean, 0.f);
+    const float rs = rsqrtf(var + eps);
+    save_mean[c] = mean;
+    save_rstd[c] = rs;
+    if (upd_mean) {
+        const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        upd_mean[c] = (1.f - momentum) * upd_mean[c] + momentum * mean;
+        upd_var[c] = (1.f - momentum) * upd_var[c] + momentum * unbiased;
+    }
+    const float sc = rs * bf2f(gamma[c]);
+    pro[c] = sc;
+    pro[C + c] = bf2f(beta[c]) - mean * sc;
+}
+
 int grid_for(int64_t nvec) {
     int64_t g = (nvec + 255) / 256;
     if (g > 4096) g = 4096;
@@ -277,11 +320,25 @@ TDL_API int tdl_bn_act_fwd(const void* x, const float* stats, const float* run_m
     TDL_LAUNCH_CHECK();
 }
 
-// sums: the forward's bwd_ws (zeroed there).  dgamma/dbeta: fp32 accumulators (+=) or null.
-TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
+// stats [2C] (sum, sumsq) -> save_mean / save_rstd [C], running stats (or null), pro [2C], and
+// bwd_ws (tdl_bn_bwd_ws_floats(C)) zeroed for the backward.
+TDL_API int tdl_bn_finalize(const float* stats, const void* gamma, const void* beta, float* save_mean, float* save_rstd,
+                            float* upd_mean, float* upd_var, float* pro, float* bwd_ws, int64_t M, int C, float eps,
+                            float momentum, hipStream_t s) {
+    if (C % 8 != 0 || stats == nullptr || pro == nullptr || bwd_ws == nullptr) return (int)hipErrorInvalidValue;
+    const int64_t zn = (int64_t)NREP * 2 * C;
+    int g = (int)((zn + 255) / 256);
+    const int gc = (C + 255) / 256;
+    if (g < gc) g = gc;
+    bn_finalize_kernel<<<g, 256, 0, s>>>(stats, (const bf16_t*)gamma, (const bf16_t*)beta, save_mean, save_rstd,
+                                         upd_mean, upd_var, pro, bwd_ws, zn, M, C, eps, momentum);
+    TDL_LAUNCH_CHECK();
+}
+
+static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
                            const void* gamma, float* sums, void* dx, void* dres, float* dgamma, float* dbeta, int64_t M,
-                           int C, int relu, hipStream_t s) {
-    if (C % 8 != 0) return (int)hipErrorInvalidValue;
+                           int C, int relu, const float* pro, hipStream_t s) {
+    if (C % 8 != 0 || (relu && out == nullptr && pro == nullptr)) return (int)hipErrorInvalidValue;
     const int CV = C / 8;
     const int VPB = CV < 256 ? CV : 256;
     const int RPB = 256 / VPB;
@@ -293,10 +350,24 @@ TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, con
     rows_per_block = (rows_per_block + RPB - 1) / RPB * RPB;
     const dim3 grid((unsigned)((M + rows_per_block - 1) / rows_per_block), gy);
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
-                                                  sums, M, C, (int)rows_per_block, relu);
+                                                  sums, M, C, (int)rows_per_block, relu, pro);
     bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
     bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
         (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,
-        sums + (size_t)NREP * 2 * C, (bf16_t*)dx, (bf16_t*)dres, M, C, relu);
+        sums + (size_t)NREP * 2 * C, (bf16_t*)dx, (bf16_t*)dres, M, C, relu, pro);
     TDL_LAUNCH_CHECK();
+}
+
+// sums: the forward's bwd_ws (zeroed there).  dgamma/dbeta: fp32 accumulators (+=) or null.
+TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
+                           const void* gamma, float* sums, void* dx, void* dres, float* dgamma, float* dbeta, int64_t M,
+                           int C, int relu, hipStream_t s) {
+    return bn_act_bwd_impl(dout, out, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, M, C, relu, nullptr, s);
+}
+
+// Backward of a folded BN (+ ReLU): no stored output, the mask is recomputed from x with pro.
+TDL_API int tdl_bn_act_bwd_pro(const void* dout, const void* x, const float* mean, const float* rstd, const void* gamma,
+                               const float* pro, float* sums, void* dx, float* dgamma, float* dbeta, int64_t M, int C,
+                               int relu, hipStream_t s) {
+    return bn_act_bwd_impl(dout, nullptr, x, mean, rstd, gamma, sums, dx, nullptr, dgamma, dbeta, M, C, relu, pro, s);
 }

@@ -63,10 +63,29 @@ constexpr int BM = 128;  // m (pixels) per workgroup
 constexpr int BK = 64;   // k per step
 
 // ============================================================================ conv_nt (fwd / dgrad)
-template <int BCO, bool TRANSPOSED, bool STATS>
+// BatchNorm-apply + ReLU of the PREVIOUS layer folded into an activation operand load: the staged
+// 8-channel vector of pre-BN values y becomes relu(y * scale[c] + shift[c]) (pro = [scale[C] |
+// shift[C]], fp32, from tdl_bn_finalize), rounded to bf16 exactly as a materialised BN output would
+// be.  Zero padding stays zero (only in-range taps are transformed).
+__device__ __forceinline__ void pro_load(const float* __restrict__ pro, int C, int c, float* sc, float* sh) {
+    const float4 a = *(const float4*)(pro + c), b = *(const float4*)(pro + c + 4);
+    const float4 e = *(const float4*)(pro + C + c), f = *(const float4*)(pro + C + c + 4);
+    sc[0] = a.x, sc[1] = a.y, sc[2] = a.z, sc[3] = a.w, sc[4] = b.x, sc[5] = b.y, sc[6] = b.z, sc[7] = b.w;
+    sh[0] = e.x, sh[1] = e.y, sh[2] = e.z, sh[3] = e.w, sh[4] = f.x, sh[5] = f.y, sh[6] = f.z, sh[7] = f.w;
+}
+__device__ __forceinline__ uint4 pro_apply(uint4 v, const float* sc, const float* sh) {
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sh[e]), 0.f);
+    return pack8(f);
+}
+
+template <int BCO, bool TRANSPOSED, bool STATS, bool PRO = false>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restrict__ act, const bf16_t* __restrict__ wk,
                                                          bf16_t* __restrict__ out, float* __restrict__ part,
-                                                         ConvDims d) {
+                                                         ConvDims d, const float* __restrict__ pro) {
+    static_assert(!(PRO && TRANSPOSED), "the BN prologue applies to forward activations only");
     constexpr int TCO = BCO / 64;   // 32-row cout tiles per wave (waves are 2 x 2)
     constexpr int AROWS = BCO / 32; // weight rows staged per thread (BCO rows x 8 chunks / 256 threads)
     __shared__ __attribute__((aligned(16))) bf16_t As[2][BCO * BK];
@@ -99,6 +118,11 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
         }
     }
     uint4 areg[AROWS], breg[4];
+    // BN prologue state of the staged tile: the transform is applied when the tile is written to
+    // LDS (after the current tile's MFMAs), not at load time, so the global loads stay in flight
+    // behind the MFMAs; only in-range taps are transformed (padding stays zero)
+    float psc[8], psh[8];
+    uint32_t bok = 0;
     auto gload = [&](int k0) {
         const int kk = k0 + 8 * sch;
         const bool kin = kk < K;
@@ -114,6 +138,8 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
             const int co = co0 + srow + 32 * i;
             areg[i] = (kin && co < d.Cout) ? *(const uint4*)(wk + (size_t)co * K + kk) : make_uint4(0, 0, 0, 0);
         }
+        if (PRO && kin) pro_load(pro, d.Cin, c, psc, psh);
+        bok = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             uint4 v = make_uint4(0, 0, 0, 0);
@@ -130,7 +156,10 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                     x = b_x[i] + s;
                     ok = (unsigned)y < (unsigned)d.Hin && (unsigned)x < (unsigned)d.Win;
                 }
-                if (ok) v = *(const uint4*)(act + (((size_t)b_img[i] * d.Hin + y) * d.Win + x) * d.Cin + c);
+                if (ok) {
+                    v = *(const uint4*)(act + (((size_t)b_img[i] * d.Hin + y) * d.Win + x) * d.Cin + c);
+                    bok |= 1u << i;
+                }
             }
             breg[i] = v;
         }
@@ -145,7 +174,8 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = srow + 32 * i;
-            *(uint4*)(Bs[buf] + row * BK + ((sch ^ ((row >> 1) & 7)) << 3)) = breg[i];
+            const uint4 v = (PRO && ((bok >> i) & 1u)) ? pro_apply(breg[i], psc, psh) : breg[i];
+            *(uint4*)(Bs[buf] + row * BK + ((sch ^ ((row >> 1) & 7)) << 3)) = v;
         }
     };
 
@@ -265,10 +295,10 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __rest
 constexpr int WBM = 32;          // m rows per reduction step
 constexpr int WLD_PAD = 32;      // row padding (elements): 320-byte rows -> conflict-free tr reads
 
-template <int BCO>
+template <int BCO, bool PRO = false>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                             float* __restrict__ dw, ConvDims d, int m_per_split,
-                                                            int mode) {
+                                                            int mode, const float* __restrict__ pro) {
     constexpr int TCO = BCO / 64;
     constexpr int LDY = BCO + WLD_PAD, LDX = 128 + WLD_PAD;
     constexpr int YCH = BCO / 8;        // 16-byte chunks per dY row
@@ -299,10 +329,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const bf16_t* __rest
         kr = rs / d.S;
         ks = rs - kr * d.S;
     }
+    float psc[8], psh[8];  // BN prologue of this thread's fixed 8 channels
+    if (PRO && kin) pro_load(pro, d.Cin, kc, psc, psh);
     // dY staging: thread -> (row yr + YROWS i, chunk yc)
     const int yr = tid / YCH, yc = tid - yr * YCH;
     uint4 yreg[WBM / YROWS], xreg[2];
+    uint32_t xok = 0;  // in-range X rows of the staged tile (BN prologue applied at LDS-write time)
     auto gload = [&](int mb) {
+        xok = 0;
 #pragma unroll
         for (int i = 0; i < WBM / YROWS; ++i) {
             const int m = mb + yr + YROWS * i;
@@ -316,8 +350,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const bf16_t* __rest
             if (kin && m < mend) {
                 const int n = m / PQ, pq = m - n * PQ, p = pq / d.Q, q = pq - p * d.Q;
                 const int y = p * d.stride - d.pad + kr, xx = q * d.stride - d.pad + ks;
-                if ((unsigned)y < (unsigned)d.Hin && (unsigned)xx < (unsigned)d.Win)
+                if ((unsigned)y < (unsigned)d.Hin && (unsigned)xx < (unsigned)d.Win) {
                     v = *(const uint4*)(x + (((size_t)n * d.Hin + y) * d.Win + xx) * d.Cin + kc);
+                    xok |= 1u << i;
+                }
             }
             xreg[i] = v;
         }
@@ -326,7 +362,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(const bf16_t* __rest
 #pragma unroll
         for (int i = 0; i < WBM / YROWS; ++i) *(uint4*)(Ys[buf] + (yr + YROWS * i) * LDY + 8 * yc) = yreg[i];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) *(uint4*)(Xs[buf] + (xr + 16 * i) * LDX + 8 * xc) = xreg[i];
+        for (int i = 0; i < 2; ++i) {
+            const uint4 v = (PRO && ((xok >> i) & 1u)) ? pro_apply(xreg[i], psc, psh) : xreg[i];
+            *(uint4*)(Xs[buf] + (xr + 16 * i) * LDX + 8 * xc) = v;
+        }
     };
 
     f32x16 acc[TCO][2];
@@ -419,11 +458,11 @@ bool dims_ok(const ConvDims& d) {
 // hold tdl_conv_stats_ws_floats(...) floats (one partial row per 128-pixel tile).
 TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) { return (int64_t)((M + BM - 1) / BM) * 2 * Cout; }
 
-TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
+static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
                         int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
-                        hipStream_t s) {
+                        const float* pro, hipStream_t s) {
     ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
-    if (!dims_ok(d)) return (int)hipErrorInvalidValue;
+    if (!dims_ok(d) || (pro != nullptr && transposed)) return (int)hipErrorInvalidValue;
     const int M = N * P * Q;
     const bool st = stats != nullptr;
     if (st && stats_ws == nullptr) return (int)hipErrorInvalidValue;
@@ -433,8 +472,12 @@ TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats
     auto A = (const bf16_t*)act;
     auto W = (const bf16_t*)wk;
     auto O = (bf16_t*)out;
-#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d)
-    if (big) {
+#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr)
+#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro)
+    if (pro != nullptr) {
+        if (big) { if (st) LAUNCHP(128, true); else LAUNCHP(128, false); }
+        else { if (st) LAUNCHP(64, true); else LAUNCHP(64, false); }
+    } else if (big) {
         if (transposed) { if (st) LAUNCH(128, true, true); else LAUNCH(128, true, false); }
         else { if (st) LAUNCH(128, false, true); else LAUNCH(128, false, false); }
     } else {
@@ -442,6 +485,7 @@ TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats
         else { if (st) LAUNCH(64, false, true); else LAUNCH(64, false, false); }
     }
 #undef LAUNCH
+#undef LAUNCHP
     if (st) {
         hipError_t e = hipMemsetAsync(stats, 0, sizeof(float) * 2 * Cout, s);
         if (e != hipSuccess) return (int)e;
@@ -454,8 +498,9 @@ TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats
 
 // dw (fp32 [Cout][Cin][R][S], accumulated) += sum_m dY[m][co] * im2col(X)[m][k].  For R*S > 1 the
 // kernel reduces into ws (fp32, Cout*R*S*Cin floats, [Cout][R][S][Cin]) and one pass adds it to dw.
-TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,
-                           int Q, int Cout, int R, int S, int stride, int pad, int num_cu, hipStream_t s) {
+static int conv_wgrad_impl(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,
+                           int Q, int Cout, int R, int S, int stride, int pad, int num_cu, const float* pro,
+                           hipStream_t s) {
     ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
     if (!dims_ok(d)) return (int)hipErrorInvalidValue;
     const int M = N * P * Q, K = R * S * Cin;
@@ -480,8 +525,14 @@ TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
         if (e != hipSuccess) return (int)e;
     }
     const dim3 grid(tiles, 1, split);
-    if (big) conv_wgrad_kernel<128><<<grid, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, target_buf, d, mps, mode);
-    else conv_wgrad_kernel<64><<<grid, 256, 0, s>>>((const bf16_t*)dy, (const bf16_t*)x, target_buf, d, mps, mode);
+    const bf16_t *Y = (const bf16_t*)dy, *X = (const bf16_t*)x;
+    if (pro != nullptr) {
+        if (big) conv_wgrad_kernel<128, true><<<grid, 256, 0, s>>>(Y, X, target_buf, d, mps, mode, pro);
+        else conv_wgrad_kernel<64, true><<<grid, 256, 0, s>>>(Y, X, target_buf, d, mps, mode, pro);
+    } else {
+        if (big) conv_wgrad_kernel<128><<<grid, 256, 0, s>>>(Y, X, target_buf, d, mps, mode, nullptr);
+        else conv_wgrad_kernel<64><<<grid, 256, 0, s>>>(Y, X, target_buf, d, mps, mode, nullptr);
+    }
     if (!direct) {
         const int64_t n = (int64_t)Cout * K;
         int g = (int)((n + 255) / 256);
@@ -489,4 +540,33 @@ TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, 
         krsc_to_kcrs_add_kernel<<<g, 256, 0, s>>>(ws, dw, Cout, R * S, Cin);
     }
     TDL_LAUNCH_CHECK();
+}
+
+TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
+                        int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
+                        hipStream_t s) {
+    return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, transposed,
+                        nullptr, s);
+}
+
+// Forward convolution of relu(BN(y)) without materialising it: act = the previous layer's pre-BN
+// output y, pro = [scale | shift] fp32 [2 Cin] from tdl_bn_finalize.
+TDL_API int tdl_conv_nt_pro(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
+                            int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad,
+                            const float* pro, hipStream_t s) {
+    if (pro == nullptr) return (int)hipErrorInvalidValue;
+    return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 0, pro, s);
+}
+
+TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,
+                           int Q, int Cout, int R, int S, int stride, int pad, int num_cu, hipStream_t s) {
+    return conv_wgrad_impl(dy, x, dw, ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, num_cu, nullptr, s);
+}
+
+// Weight gradient against relu(BN(y)) recomputed on load (pro as in tdl_conv_nt_pro).
+TDL_API int tdl_conv_wgrad_pro(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin,
+                               int P, int Q, int Cout, int R, int S, int stride, int pad, int num_cu, const float* pro,
+                               hipStream_t s) {
+    if (pro == nullptr) return (int)hipErrorInvalidValue;
+    return conv_wgrad_impl(dy, x, dw, ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, num_cu, pro, s);
 }

@@ -123,6 +123,79 @@ def test_conv_bn_act_train_matches_torch(relu, residual):
     assert _rel(bn.running_var, bn_r.running_var) < 2e-2
 
 
+def _chain_modules(cin, mid, cout, stride, seed):
+    torch.manual_seed(seed)
+    units = [(nn.Conv2d(cin, mid, 1, 1, 0, bias=False), nn.BatchNorm2d(mid)),
+             (nn.Conv2d(mid, mid, 3, stride, 1, bias=False), nn.BatchNorm2d(mid)),
+             (nn.Conv2d(mid, cout, 1, 1, 0, bias=False), nn.BatchNorm2d(cout))]
+    for _, bn in units:
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.3, 0.3)
+    return units
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bn_fold_chain_matches_unfolded_and_fp32(stride, monkeypatch):
+    """Bottleneck chain conv1-BN1-ReLU-conv2-BN2-ReLU-conv3-BN3(+res)-ReLU with BN1/BN2 + ReLU folded
+    into conv2 / conv3 (tdl_bn_finalize + tdl_conv_nt_pro / tdl_conv_wgrad_pro + tdl_bn_act_bwd_pro:
+    the BN outputs are never written) against the unfolded native path and an fp32 torch reference:
+    output, input / residual / weight / BN gradients and running statistics."""
+    from trustworthy_dl.ops import conv as conv_mod
+    from trustworthy_dl.ops.conv import conv_bn_chain
+    folded = []
+    orig = conv_mod._BNActConvNHWC.apply
+    monkeypatch.setattr(conv_mod._BNActConvNHWC, "apply", lambda *a: folded.append(1) or orig(*a))
+    cin, mid, cout = 64, 32, 64
+    x = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(4, cout, 16 // stride, 16 // stride, device="cuda").to(torch.bfloat16)
+    gy = torch.randn(4, cout, 16 // stride, 16 // stride, device="cuda").to(torch.bfloat16)
+    runs = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("TDL_BN_FOLD", fold)
+        units = _chain_modules(cin, mid, cout, stride, 0)
+        for conv, bn in units:
+            conv.cuda().to(torch.bfloat16)
+            bn.cuda()
+            bn.weight.data = bn.weight.data.to(torch.bfloat16)
+            bn.bias.data = bn.bias.data.to(torch.bfloat16)
+        xn, rn = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+        n0 = len(folded)
+        out = conv_bn_chain(xn, units, relu=True, residual=rn)
+        assert len(folded) - n0 == (2 if fold == "1" else 0)   # BN1 / BN2 folded only when enabled
+        out.backward(gy)
+        runs[fold] = (out.detach().float(), xn.grad.float(), rn.grad.float(),
+                      [c.weight.grad.float() for c, _ in units], [b.weight.grad.float() for _, b in units],
+                      [b.bias.grad.float() for _, b in units], [b.running_mean.clone() for _, b in units],
+                      [b.running_var.clone() for _, b in units])
+    # fp32 reference with the same (bf16-rounded) parameters
+    units_r = _chain_modules(cin, mid, cout, stride, 0)
+    for conv, bn in units_r:
+        conv.cuda()
+        bn.cuda()
+        conv.weight.data = conv.weight.data.to(torch.bfloat16).float()
+        bn.weight.data = bn.weight.data.to(torch.bfloat16).float()
+        bn.bias.data = bn.bias.data.to(torch.bfloat16).float()
+    xr, rr = x.float().requires_grad_(True), res.float().requires_grad_(True)
+    h = xr
+    for i, (conv, bn) in enumerate(units_r):
+        h = bn(conv(h))
+        h = F.relu(h + rr) if i == 2 else F.relu(h)
+    h.backward(gy.float())
+    # folded vs unfolded native: the same per-channel fold and bf16 rounding (bit-identical on
+    # MI355X); vs fp32 torch: bf16 error of a 3-conv / 3-BN chain incl. ReLU-mask flips at
+    # |pre| ~ 1 ulp (input gradient ~7 %, residual gradient ~5 %)
+    f, u = runs["1"], runs["0"]
+    assert _rel(f[0], u[0]) < 1e-2 and _rel(f[0], h.detach()) < 5e-2
+    assert _rel(f[1], u[1]) < 1e-2 and _rel(f[1], xr.grad) < 1e-1
+    assert _rel(f[2], u[2]) < 1e-2 and _rel(f[2], rr.grad) < 1e-1
+    for i in range(3):
+        assert _rel(f[3][i], u[3][i]) < 1e-2 and _rel(f[3][i], units_r[i][0].weight.grad) < 1e-1, i
+        assert _rel(f[4][i], u[4][i]) < 1e-2 and _rel(f[4][i], units_r[i][1].weight.grad) < 1e-1, i
+        assert _rel(f[5][i], u[5][i]) < 1e-2 and _rel(f[5][i], units_r[i][1].bias.grad) < 1e-1, i
+        assert _rel(f[6][i], units_r[i][1].running_mean) < 2e-2 and _rel(f[7][i], units_r[i][1].running_var) < 2e-2
+
+
 def test_resnet_engine_step_native():
     """A ResNet-32 pipeline step on the GPU goes through the native conv path (bf16) and matches
     the CPU fp32 engine's first loss."""

@@ -61,9 +61,8 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        out = ops.conv_bn_act(x, self.conv1, self.bn1, relu=True)
         sc = x if self.shortcut is None else ops.conv_bn_act(x, self.shortcut[0], self.shortcut[1], relu=False)
-        return ops.conv_bn_act(out, self.conv2, self.bn2, relu=True, residual=sc)
+        return ops.conv_bn_chain(x, [(self.conv1, self.bn1), (self.conv2, self.bn2)], relu=True, residual=sc)
 
 
 class Bottleneck(nn.Module):
@@ -83,10 +82,10 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        out = ops.conv_bn_act(x, self.conv1, self.bn1, relu=True)
-        out = ops.conv_bn_act(out, self.conv2, self.bn2, relu=True)
         sc = x if self.shortcut is None else ops.conv_bn_act(x, self.shortcut[0], self.shortcut[1], relu=False)
-        return ops.conv_bn_act(out, self.conv3, self.bn3, relu=True, residual=sc)
+        # BN1 + ReLU and BN2 + ReLU are folded into conv2 / conv3 on the native path (never written)
+        return ops.conv_bn_chain(x, [(self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3)],
+                                 relu=True, residual=sc)
 
 
 class Stem(nn.Module):

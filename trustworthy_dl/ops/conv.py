@@ -14,6 +14,7 @@ the kernels cannot serve raises.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -168,6 +169,123 @@ class _BatchNormActNHWC(torch.autograd.Function):
         gg = None if mg_g is not None else dg.to(gamma.dtype)
         gb = None if mg_b is not None else db.to(beta.dtype)
         return dx, None, gg, gb, dres, None, None, None, None, None, None
+
+
+class _BNActConvNHWC(torch.autograd.Function):
+    """y_next = conv(relu(BN(y)), w) with the BN output never materialised: the batch statistics
+    of y (from the producing conv's epilogue) are folded into a per-channel scale / shift
+    (tdl_bn_finalize, no pass over y), the forward conv applies relu(y * scale + shift) while it
+    stages its activation operand, the weight gradient re-applies it on its own load, and the BN
+    backward recomputes the ReLU mask from y (tdl_bn_act_bwd_pro).  Saves the BN-apply pass, the
+    write of its output and every later read of it (training mode only)."""
+
+    @staticmethod
+    def forward(ctx, y, stats, gamma, beta, running_mean, running_var, momentum: float, eps: float, weight,
+                stride: int, pad: int, want_stats: bool):
+        N, C, H, W = y.shape
+        Cout, Cw, R, S = weight.shape
+        if Cw != C or C % 8 or Cout % 8:
+            raise ValueError(f"folded BN conv: unsupported shapes y={tuple(y.shape)} w={tuple(weight.shape)}")
+        dev = y.device
+        ys = y.contiguous(memory_format=torch.channels_last)
+        M = N * H * W
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        pro = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        sums = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(C)), dtype=torch.float32, device=dev)
+        upd = running_mean is not None
+        _lib.call("tdl_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
+                  ptr(running_mean if upd else None), ptr(running_var if upd else None), ptr(pro), ptr(sums), M, C,
+                  float(eps), float(momentum), stream_ptr(dev))
+        wk = weight.permute(0, 2, 3, 1).contiguous()
+        P, Q = _out_hw(H, W, R, S, stride, pad)
+        out = torch.empty((N, Cout, P, Q), dtype=y.dtype, device=dev, memory_format=torch.channels_last)
+        st = ws = None
+        if want_stats:
+            st = torch.empty(2 * Cout, dtype=torch.float32, device=dev)
+            ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * P * Q, Cout)), dtype=torch.float32,
+                             device=dev)
+        _lib.call("tdl_conv_nt_pro", ptr(ys), ptr(wk), ptr(out), ptr(st), ptr(ws), N, H, W, C, P, Q, Cout, R, S,
+                  stride, pad, ptr(pro), stream_ptr(dev))
+        ctx.save_for_backward(ys, mean, rstd, gamma, pro, weight)
+        ctx.sums = sums
+        ctx.beta = beta  # a parameter (leaf): only its identity / main_grad is needed
+        ctx.geom = (N, C, H, W, Cout, R, S, P, Q, stride, pad)
+        if st is None:
+            st = torch.zeros(0, dtype=torch.float32, device=dev)
+        ctx.mark_non_differentiable(st)
+        return out, st
+
+    @staticmethod
+    def backward(ctx, dout, _dstats):
+        ys, mean, rstd, gamma, pro, weight = ctx.saved_tensors
+        N, C, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
+        dev = dout.device
+        dout = dout.contiguous(memory_format=torch.channels_last)
+        if dout.dtype != ys.dtype:
+            dout = dout.to(ys.dtype)
+        # data gradient of the conv = gradient w.r.t. the (never stored) BN output
+        wd = weight.permute(1, 2, 3, 0).contiguous()  # [C][R][S][Cout]
+        dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
+        _lib.call("tdl_conv_nt", ptr(dout), ptr(wd), ptr(dbn), None, None, N, P, Q, Cout, H, W, C, R, S, stride, pad, 1,
+                  stream_ptr(dev))
+        # weight gradient against relu(BN(y)) recomputed on load
+        gw = None
+        if ctx.needs_input_grad[8]:
+            mg = getattr(weight, "main_grad", None)
+            acc = mg if (mg is not None and mg.is_contiguous()) else torch.zeros((Cout, C, R, S), dtype=torch.float32,
+                                                                                 device=dev)
+            wsw = torch.empty(Cout * R * S * C, dtype=torch.float32, device=dev) if R * S > 1 else None
+            _lib.call("tdl_conv_wgrad_pro", ptr(dout), ptr(ys), ptr(acc), ptr(wsw), N, H, W, C, P, Q, Cout, R, S,
+                      stride, pad, _num_cu(dev), ptr(pro), stream_ptr(dev))
+            if acc is not mg:
+                if mg is not None:
+                    mg.add_(acc)
+                else:
+                    gw = acc.to(weight.dtype)
+        # BN (+ ReLU) backward with the mask recomputed from y
+        dy = torch.empty_like(ys, memory_format=torch.channels_last)
+        beta = ctx.beta
+        mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
+        dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+        db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+        _lib.call("tdl_bn_act_bwd_pro", ptr(dbn), ptr(ys), ptr(mean), ptr(rstd), ptr(gamma), ptr(pro), ptr(ctx.sums),
+                  ptr(dy), ptr(dg), ptr(db), N * H * W, C, 1, stream_ptr(dev))
+        gg = None if mg_g is not None else dg.to(gamma.dtype)
+        gb = None if mg_b is not None else db.to(beta.dtype)
+        return dy, None, gg, gb, None, None, None, None, gw, None, None, None
+
+
+def _bn_fold_enabled() -> bool:
+    return os.environ.get("TDL_BN_FOLD", "1") != "0"
+
+
+def conv_bn_chain(x: torch.Tensor, units, relu: bool = True, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``units`` = [(conv, bn), ...]: relu(bn(conv(...relu(bn(conv(x)))...)) (+ residual)) with ReLU after
+    every intermediate BN.  On the native training path each intermediate BN + ReLU is folded into
+    the next convolution (``_BNActConvNHWC``: its output is never written); otherwise the units run
+    one by one through ``conv_bn_act``."""
+    units = list(units)
+    if not (native_conv_ok(x) and _bn_fold_enabled() and all(bn.training for _, bn in units)) or len(units) == 1:
+        for i, (conv, bn) in enumerate(units):
+            last = i == len(units) - 1
+            x = conv_bn_act(x, conv, bn, relu=relu if last else True, residual=residual if last else None)
+        return x
+    conv0, _ = units[0]
+    if conv0.bias is not None:
+        raise NotImplementedError("native conv: bias")
+    y, stats = _Conv2dNHWC.apply(x, conv0.weight, _single(conv0.stride), _single(conv0.padding), True)
+    for (_, bn), (conv, _) in zip(units[:-1], units[1:]):
+        if conv.groups != 1 or _single(conv.dilation) != 1 or conv.bias is not None \
+                or conv.kernel_size[0] != conv.kernel_size[1]:
+            raise NotImplementedError(f"native conv: unsupported configuration {conv}")
+        momentum = bn.momentum if bn.momentum is not None else 0.1
+        y, stats = _BNActConvNHWC.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, momentum, bn.eps,
+                                        conv.weight, _single(conv.stride), _single(conv.padding), True)
+    bn = units[-1][1]
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    return _BatchNormActNHWC.apply(y, stats, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, True,
+                                   momentum, bn.eps, relu)
 
 
 def _single(v) -> int:

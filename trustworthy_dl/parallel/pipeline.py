@@ -68,7 +68,7 @@ class EngineConfig:
     output_check: str = "random"         # which micro-batch output is monitored each step: "random" (a
                                          # per-step choice from a private seeded RNG, so an attacker
                                          # cannot predict which output is inspected) | "first" | "none"
-    monitor_seed: Optional[int] = None   # seed of that RNG (None: from os.urandom; tests pin it)
+    monitor_seed: Optional[int] = None   # seed of that RNG (None: $TDL_MONITOR_SEED, else os.urandom)
     early_grad_stats: bool = True        # start each layer's gradient statistics on the side stream
                                          # as soon as its last-micro-batch backward is done
     compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
@@ -156,7 +156,11 @@ class PipelineEngine:
         self._comm_wait = 0.0
         self._step_time = 0.0
         # private per-process RNG for the monitored micro-batch (not derived from the data seed)
-        seed = cfg.monitor_seed if cfg.monitor_seed is not None else int.from_bytes(os.urandom(8), "little")
+        seed = cfg.monitor_seed
+        if seed is None and os.environ.get("TDL_MONITOR_SEED"):
+            seed = int(os.environ["TDL_MONITOR_SEED"])   # reproducible runs / tests
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), "little")
         self._mon_rng = __import__("random").Random(seed)
         self._mon_idx = 0
 
