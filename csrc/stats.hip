@@ -584,6 +584,9 @@ __device__ __forceinline__ float wave_median(const float* v, int n, int lane) {
                    : 0.5f * (wave_select(v, n, n / 2 - 1, lane) + wave_select(v, n, n / 2, lane));
 }
 
+constexpr int ZS_EARLY_MIN = 8;
+constexpr float ZS_EARLY_FACTOR = 2.f;
+
 __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, int* __restrict__ state,
                                                      const float* __restrict__ cur, int K, int H, int warmup,
                                                      float z_decision, int window, int exclude_current,
@@ -593,6 +596,11 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
     __shared__ float col[4][128];
     __shared__ int cnt_sh;
     const bool agg_max = (robust & 4) != 0;  // decision on the largest |z| instead of the mean
+    // early gate (bit 8): during warm-up, once ZS_EARLY_MIN entries exist, a gross outlier (largest
+    // |z| > ZS_EARLY_FACTOR x z_decision) is flagged and kept out of the baseline — otherwise an
+    // attack that is already running while a baseline (re)builds (a stage re-planned after a
+    // re-shard) is learnt as normal and masks its later injections
+    const bool early_gate = (robust & 8) != 0;
     robust &= 3;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int count = state[0], head = state[1];
@@ -604,6 +612,7 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
         count = count < H ? count + 1 : H;
     }
     const bool ready = count >= warmup;
+    const bool early = !ready && early_gate && robust && count >= ZS_EARLY_MIN;
     const int wn = robust ? (count < window ? count : window) : count;
     for (int k = wid; k < K; k += 4) {
         float center, scale;
@@ -653,7 +662,7 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
         }
         if (lane == 0) {
             float z = -1.f;
-            if (ready && scale > 0.f) {
+            if ((ready || early) && scale > 0.f) {
                 const float c = cur[k];
                 z = isfinite(c) ? fabsf((c - center) / scale) : 1e6f;
             }
@@ -667,7 +676,7 @@ __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, i
         for (int k = 0; k < K; ++k)
             if (zs[k] >= 0.f) { sum += zs[k]; mx = fmaxf(mx, zs[k]); ++nv; }
         const float mz = agg_max ? mx : (nv ? sum / nv : 0.f);
-        const bool flag = ready && mz > z_decision;
+        const bool flag = ready ? mz > z_decision : (early && mz > ZS_EARLY_FACTOR * z_decision);
         out[0] = flag ? 1.f : 0.f;
         out[1] = mz;
         out[2] = fminf(1.f, mz / 5.f);

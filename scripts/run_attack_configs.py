@@ -34,14 +34,18 @@ from trustworthy_dl.utils.metrics import MetricsCollector  # noqa: E402
 CONFIGS = {
     3: dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="scale",
                                              gradient_scale=10.0), targets=[3], lr=1e-4),
-    4: dict(model="resnet50", attack=dict(attack_types=["model_poisoning"], intensity=0.05), targets=[4], lr=3e-4),
+    # ImageNet-shape ResNet-50 at the bench's batch (64, micro-batch 8): BatchNorm over 2 images
+    # (the r2 first run: batch 8 / micro-batch 2) makes every stage's gradient norm heavy-tailed
+    4: dict(model="resnet50", attack=dict(attack_types=["model_poisoning"], intensity=0.05), targets=[4], lr=3e-4,
+            batch=64, mbs=8),
     5: dict(model="gpt2-medium", attack=dict(attack_types=["byzantine"], intensity=0.5), targets=[2, 5], lr=1e-4),
 }
 
 
 def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, seq_len: int, p_attack: float,
-        small: bool = False):
+        small: bool = False, warmup: int = 50):
     c = dict(CONFIGS[cfg_id])
+    batch, mbs = c.get("batch", batch), c.get("mbs", mbs)
     if small:   # CPU smoke: same flow on the tiny models
         c["model"] = {"gpt2-medium": "gpt2-tiny", "resnet50": "resnet32"}[c["model"]]
     att = AdversarialAttacker(AttackConfig(target_nodes=c["targets"], start_step=start, probability=p_attack, seed=3,
@@ -55,7 +59,12 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
     extra = {"seq_len": seq_len} if gpt else {}
     cfg = EngineConfig(num_nodes=8, micro_batches=max(1, batch // mbs), device=device,
                        adamw=AdamWConfig(lr=c["lr"], weight_decay=0.01, max_grad_norm=1.0, warmup_steps=20),
-                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=True, **extra)
+                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=True,
+                       # detector warm-up of 50 clean steps before the attacks start at step 100 (the
+                       # reference protocol warms up on 100 clean steps: BASELINE.md); at 20 the
+                       # baselines of GPT-2 hidden states caught early-training transients as z ~ 30
+                       # output anomalies; the monitored micro-batch RNG is pinned for reproducibility
+                       verifier={"warmup": warmup}, monitor_seed=0, **extra)
     eng = PipelineEngine(model, cfg, attacker=att, metrics=MetricsCollector())
     del model
     plan0 = eng.plan.describe()
@@ -77,7 +86,7 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
         "p_attack": p_attack, "attack_start_step": start, "first_attack_step": first_attack, "steps": steps,
         "batch": batch, "micro_batch": mbs, "seq_len": seq_len if gpt else None, "device": device,
         "data": "markov tokens (order 1, branching 4, 8192 ids)" if gpt else "class-conditional synthetic images",
-        "lr": c["lr"], "lr_warmup_steps": 20,
+        "lr": c["lr"], "lr_warmup_steps": 20, "detector_warmup": warmup,
         "detection": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in m.items()
                       if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
         "injections": len(att.injections),
@@ -90,6 +99,10 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
         "final_trust": [round(eng.trust.get_trust_score(n), 3) for n in range(8)],
         "final_status": [eng.trust.get_node_status(n).value for n in range(8)],
         "loss_curve": losses, "wall_s": round(wall, 1),
+        # every per-stage verdict: (step, node, kind, ground truth, output z, gradient z)
+        "events": [(r["step"], r["node_id"], r.get("attack_type"), bool(r.get("ground_truth")),
+                    round(float(r.get("output_stats", {}).get("z", 0.0)), 2),
+                    round(float(r.get("gradient_stats", {}).get("z", 0.0)), 2)) for r in eng.attack_history],
     }
     return rec
 
@@ -106,10 +119,11 @@ def main():
     ap.add_argument("--p-attack", type=float, default=0.3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--small", action="store_true", help="tiny models (CPU smoke of the same flow)")
+    ap.add_argument("--detector-warmup", type=int, default=50)
     args = ap.parse_args()
     for cid in [int(x) for x in args.configs.split(",")]:
         rec = run(cid, args.device, args.steps, args.start, args.batch, args.mbs, args.seq_len, args.p_attack,
-                  args.small)
+                  args.small, args.detector_warmup)
         line = json.dumps(rec)
         print(line, flush=True)
         if args.out:

@@ -267,7 +267,9 @@ def test_grad_stats_in_pieces_match_one_pass():
 
 @pytest.mark.parametrize("kw", [{}, {"robust": "detrend", "window": 32},
                                 {"robust": "detrend", "agg": "max", "abs_floor": 0.02, "rel_floor": 0.0,
-                                 "z_decision": 8.0, "max_quarantine": 5}])
+                                 "z_decision": 8.0, "max_quarantine": 5},
+                                {"robust": "detrend", "agg": "max", "abs_floor": 0.02, "rel_floor": 0.0,
+                                 "z_decision": 8.0, "max_quarantine": 5, "early_gate": True}])
 def test_zscore_matches_cpu(kw):
     from trustworthy_dl.ops.stats import DeviceZScore
     K = 17
@@ -277,11 +279,13 @@ def test_zscore_matches_cpu(kw):
     drift = torch.linspace(0, 3, K)
     for step in range(80):
         cur = torch.randn(K, generator=g) + drift * step / 20.0
-        if step in (30, 31, 60):
+        if step in (9, 30, 31, 60):   # step 9: inside the warm-up (10), after 8 entries: early gate
             cur = cur * 20
         a = dg.observe(cur.to(DEV)).cpu()
         b = dc.observe(cur.clone())
         assert float(a[0]) == float(b[0]), step
+        if kw.get("early_gate") and step == 9:
+            assert float(a[0]) == 1.0           # gross outlier flagged and kept out of the baseline
         assert abs(float(a[1]) - float(b[1])) < 1e-3 * max(1, float(b[1])), step
 
 

@@ -258,9 +258,11 @@ def _lower_upper_median(x: torch.Tensor) -> torch.Tensor:
 class DeviceZScore:
     """Device ring-buffer baseline + z-score decision for one monitored signal (K4)."""
 
+    EARLY_MIN, EARLY_FACTOR = 8, 2.0   # csrc/stats.hip ZS_EARLY_MIN / ZS_EARLY_FACTOR
+
     def __init__(self, k: int, device, history: int = 1000, warmup: int = 10, z_decision: float = 2.5,
                  exclude_current: bool = True, max_quarantine: int = 50, robust=True, window: int = 100,
-                 rel_floor: float = 0.02, agg: str = "mean", abs_floor: float = 0.0):
+                 rel_floor: float = 0.02, agg: str = "mean", abs_floor: float = 0.0, early_gate: bool = False):
         """``robust``: 1/True = median / 1.4826*MAD over the ``window`` most recent entries; 2 or
         "detrend" = the same about a robust linear trend of the window (the drift of learning:
         line through the medians of the window's recent and older halves), scale floored at
@@ -268,6 +270,9 @@ class DeviceZScore:
         ``history``.  ``agg``: "mean" (the reference's rule: mean |z| over the features) or "max"
         (largest |z|: for short, targeted feature vectors)."""
         self.k, self.history, self.warmup = k, history, warmup
+        # during warm-up, once EARLY_MIN entries exist, flag (and keep out of the baseline) gross
+        # outliers above EARLY_FACTOR x z_decision (robust baselines only)
+        self.early_gate = bool(early_gate)
         self.agg_max = agg == "max"
         self.robust = 2 if robust == "detrend" else int(robust)
         self.window = int(min(window, 128))
@@ -287,7 +292,8 @@ class DeviceZScore:
         if self.device.type == "cuda":
             _lib.call("tdl_zscore_detect", ptr(self.ring), ptr(self.state), ptr(cur), self.k, self.history,
                       self.warmup, self.z_decision, self.window, int(self.exclude_current), self.max_quarantine,
-                      self.robust | (4 if self.agg_max else 0), self.rel_floor, self.abs_floor, ptr(self.out),
+                      self.robust | (4 if self.agg_max else 0) | (8 if self.early_gate else 0), self.rel_floor,
+                      self.abs_floor, ptr(self.out),
                       stream_ptr(self.device))
         else:
             self._cpu(cur)
@@ -304,6 +310,7 @@ class DeviceZScore:
         if not self.exclude_current:
             count, head = append(count, head)
         ready = count >= self.warmup
+        early = (not ready) and self.early_gate and bool(self.robust) and count >= self.EARLY_MIN
         zs = torch.full((self.k,), -1.0)
         if count > 0:
             if self.robust:
@@ -329,7 +336,7 @@ class DeviceZScore:
                 mean = hist.mean(0)
                 sd = hist.std(0, unbiased=False)
             for j in range(self.k):
-                if ready and sd[j] > 0:
+                if (ready or early) and sd[j] > 0:
                     c = float(cur[j])
                     zs[j] = abs((c - float(mean[j])) / float(sd[j])) if math.isfinite(c) else 1e6
         valid = zs >= 0
@@ -337,7 +344,7 @@ class DeviceZScore:
             mz = float(zs[valid].max()) if valid.any() else 0.0
         else:
             mz = float(zs[valid].mean()) if valid.any() else 0.0
-        flag = ready and mz > self.z_decision
+        flag = (mz > self.z_decision) if ready else (early and mz > self.EARLY_FACTOR * self.z_decision)
         if self.exclude_current:
             if flag and qrun < self.max_quarantine:
                 qrun += 1

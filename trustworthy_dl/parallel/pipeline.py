@@ -83,6 +83,10 @@ class EngineConfig:
     shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
                                          # (0 = off); a compromised stage is restored from it, not from itself
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
+    soft_output_z: float = 5.0           # with an output flag in a replica, an EARLIER stage whose output z
+                                         # exceeds this (below its own decision threshold) is the source: a
+                                         # tampered output moves its own statistics at least as much as the
+                                         # downstream echoes (0 = off)
     global_event_fraction: float = 0.5   # gradient anomalies on >= this fraction of a replica's stages (>= 3
                                          # stages) in one step = a pipeline-wide event (a loss spike of real
                                          # training), not a Byzantine stage: the step's update is skipped, nobody
@@ -247,6 +251,11 @@ class PipelineEngine:
         vk.setdefault("output_detection", self.cfg.attack_detection)
         vk.setdefault("gradient_verification", self.cfg.gradient_verification)
         vk.setdefault("serialize_streams", self.cfg.serialize_streams)
+        # a verifier built by a re-plan (re-shard, resume) warms its baselines while attacks may be
+        # running: gross outliers are flagged and kept out of the baseline from its 8th entry on.
+        # The first build warms up on the start of training, which is assumed clean (as the
+        # reference's warm-up does) and whose early transients must not be flagged.
+        vk.setdefault("early_gate", getattr(self, "_built_once", False))
         return vk
 
     def _build(self, layer_modules: Optional[Dict[int, List[nn.Module]]] = None):
@@ -261,6 +270,7 @@ class PipelineEngine:
         self._set_clip_exclusions()
         self._set_early_stats()
         self._build_comm()
+        self._built_once = True
 
     def _set_early_stats(self):
         """Per-layer gradient-statistics triggers (verification overlapped with the backward).
@@ -921,6 +931,7 @@ class PipelineEngine:
         pipeline replica with an output anomaly, and (c) gradient anomalies only when the replica
         shows no output / integrity evidence (gradient poisoning does not propagate)."""
         of, gf, pf = D[:, SV.D_OUT_FLAG], D[:, SV.D_GRAD_FLAG], D[:, SV.D_PARAM_FLAG]
+        oz = D[:, SV.D_OUT_Z]
         blame = torch.zeros_like(of)
         evidence = torch.zeros_like(of)
         self.t_taint.copy_(torch.maximum(self.t_taint, (pf > 0).float()))
@@ -932,6 +943,10 @@ class PipelineEngine:
                 # earliest anomalous stage; a stage with tampered (integrity-failed, not yet
                 # restored) weights counts as anomalous, so the output echoes it causes downstream
                 # are neither blamed nor skip the step (its own flag already compromised it)
+                if self.cfg.soft_output_z > 0:
+                    # a replica with an output flag: softly anomalous earlier stages count too
+                    soft = (oz[idx] > self.cfg.soft_output_z).float() * o.max()
+                    o = torch.maximum(o, soft)
                 a = torch.maximum(o, taint)
                 head = (torch.cumsum(a, 0) == 1).float() * a
                 first = head * o * (1.0 - taint)

@@ -40,7 +40,8 @@ class StageVerifier:
                  output_detection: bool = True, gradient_verification: bool = True,
                  consistency_tolerance: float = 2.0, deviation_deadzone: float = 0.25,
                  robust_baseline="detrend", baseline_window: int = 64, serialize_streams: bool = False,
-                 features: str = "targeted", z_grad: float = 8.0, z_out: float = 8.0, sign_flip_cos: float = -0.4):
+                 features: str = "targeted", z_grad: float = 8.0, z_out: float = 8.0, sign_flip_cos: float = -0.7,
+                 early_gate: bool = False):
         """``consistency_tolerance`` / ``deviation_deadzone`` make the trust metrics tolerate the
         legitimate drift of training (gradient norms routinely move 2x within a few steps early in
         training): a norm ratio r scores min(1, tol * min(r, 1/r)), an output deviation d scores
@@ -68,10 +69,14 @@ class StageVerifier:
             # the largest |z|, scale floored at 5 % per step.  The cosine to the EMA reference
             # gradient is too autocorrelated for a z-score (it swings from -0.2 to 0.97 within a
             # few clean steps after a loss spike, MI355X trace r2): sign flips are caught by an
-            # absolute rule instead (mean cosine < sign_flip_cos once the baseline is warm).
+            # absolute rule instead (mean cosine < sign_flip_cos once the baseline is warm).  -0.7:
+            # clean ResNet-50 gradients at micro-batch 8 dip below -0.4 against their EMA (the r2
+            # attack-config trace: 13 false gradient flags at |z| < 3), a flipped gradient that
+            # follows a real descent direction lands near -1
+            # ``early_gate``: see ops.stats.DeviceZScore (set for verifiers built by a re-plan)
             kw = dict(history=history, warmup=warmup, exclude_current=exclude_current,
                       max_quarantine=max_quarantine, robust=robust_baseline, window=baseline_window,
-                      agg="max", rel_floor=0.0, abs_floor=0.05)
+                      agg="max", rel_floor=0.0, abs_floor=0.05, early_gate=early_gate)
             self.out_det = S.DeviceZScore(3, self.device, z_decision=z_out, **kw)
             self.grad_det = S.DeviceZScore(3, self.device, z_decision=z_grad, **kw)
         self.sign_flip_cos = float(sign_flip_cos)
