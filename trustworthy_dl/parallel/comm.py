@@ -128,7 +128,9 @@ class LinkMeter:
         if kind == "cuda":
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
+            self._harvest()          # bounded: finished intervals leave the pending list here
             self._pending.append((start, ev, float(link_bytes)))
+            del self._pending[:-4 * self.keep]
         else:
             self._add(float(link_bytes), time.perf_counter() - start)
 
