@@ -52,7 +52,9 @@ ensure_hw_queues()
 # timings on MI355X (scripts/time_units.py at micro-batch 4/8/16/32: 24 blocks + LM head +
 # embedding per sequence; profiles/r1_gpt2m_unit_times.jsonl): larger micro-batches feed the GEMMs
 # and the attention kernels larger tiles.  Used only to choose the micro-batch size.
-_MBS_EFF = {4: 220.9, 8: 269.8, 16: 329.3, 32: 354.8}
+# 64 (one micro-batch: N=1 only in practice): +2.1 % over 32 in an interleaved A/B with the LM head
+# unchunked (profiles/r2_mbs64_ab.txt)
+_MBS_EFF = {4: 220.9, 8: 269.8, 16: 329.3, 32: 354.8, 64: 362.3}
 # fill/drain slot cost relative to a steady-state slot: with the B/W split the drain advances one
 # stage per (F + B_input) ~ 2/3 of a full (F + B_input + W) slot
 _BUBBLE_WEIGHT = 2.0 / 3.0

@@ -552,9 +552,9 @@ def linear_t(x, weight):
 # ============================================================== tied LM head + cross-entropy, one node
 def lmhead_chunk_rows(vocab_padded: int) -> int:
     """Rows per logits chunk: the whole micro-batch unless its bf16 logits exceed
-    TDL_LMHEAD_CHUNK_MB (default 4096 MB) — then the [rows, vocab] logits are never materialised
+    TDL_LMHEAD_CHUNK_MB (default 8192 MB) — then the [rows, vocab] logits are never materialised
     at once."""
-    budget = int(os.environ.get("TDL_LMHEAD_CHUNK_MB", "4096")) << 20
+    budget = int(os.environ.get("TDL_LMHEAD_CHUNK_MB", "8192")) << 20
     return max(256, budget // (2 * vocab_padded) // 256 * 256)
 
 
