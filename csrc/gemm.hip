@@ -945,20 +945,57 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
 //   RAW: each wave keeps the copies of its last 4 phases in flight (s_waitcnt vmcnt(2 x issued
 //        copies in phases g-3..g) before phase g's first barrier), so a unit issued in phase g is
 //        readable from phase g+5 on — every unit is read >= 5 phases after its issue.
-template <bool TA, bool TB, int EPI, int ABL = 0>
+// Vector-memory operations one wave's epilogue_store<EPI, 4> issues, counted LOW (stores and
+// operand loads only): the persistent form lets that many more ops stay in flight at the waits of
+// the first K step after an epilogue (vmcnt retires in issue order: MI355X_MICROARCH.md, vmcnt),
+// so the next tile's MFMAs start while the stores drain.  Under-counting only waits longer.
+template <int EPI>
+constexpr int pp_epi_vmem() {
+    return EPI == EPI_BF16 || EPI == EPI_F32 ? 32 : EPI == EPI_F32ATOM ? 128 : 64;
+}
+// copies allowed in flight at phase q's wait: 2 per issuing phase among q-3..q (PM / MK: issue
+// masks of the previous / this K step), plus EX, capped at the 6-bit vmcnt field
+constexpr int pp_vm_allow(int PM, int MK, int q, int EX) {
+    int n = 0;
+    for (int d = 0; d < 4; ++d) {
+        const int x = q - d;  // <= 0: phase x + 4 of the previous step
+        n += (x >= 1 ? (MK >> (x - 1)) & 1 : (PM >> (x + 3)) & 1) ? 2 : 0;
+    }
+    n += EX;
+    return n > 63 ? 63 : n;
+}
+template <int N>
+__device__ __forceinline__ void wait_vmc() {
+    asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(N) : "memory");
+}
+
+// PERS: persistent form (NT only): gridDim.x (a multiple of 8) workgroups walk the tiles
+// blockIdx.x, + gridDim.x, ...; the copies of the next tile's first two K steps are issued during
+// the current tile's last two (the K-step sequence runs on across tiles, nk even keeps the LDS
+// buffer parity), so neither the pipeline fill nor the store drain of a tile is exposed.
+template <bool TA, bool TB, int EPI, int ABL = 0, bool PERS = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     // ABL (timing-only ablations, wrong results): 1 = no copies in the K loop, 2 = no fragment
     // reads in the K loop, 4 = no waits / barriers in the K loop, 8 = no epilogue stores
+    static_assert(!PERS || (!TA && !TB), "persistent ping-pong: k-contiguous operands only");
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // [buf 2][UA0 UA1 UB0 UB1][16 KiB]
     constexpr int UNIT = 16384, BUF = 4 * UNIT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
-    const int wg = xcd_remap(blockIdx.x, p.tiles);
-    const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    auto coords = [&](int item, int& mm, int& nn) {
+        const int wg = xcd_remap(item, p.tiles);
+        const int tm = wg / p.tiles_n;
+        mm = tm * BM;
+        nn = (wg - tm * p.tiles_n) * BN;
+    };
+    int item = blockIdx.x;
+    int m0, n0, m1 = 0, n1 = 0;
+    coords(item, m0, n0);
+    bool has_next = PERS && item + (int)gridDim.x < p.tiles;
+    if (has_next) coords(item + gridDim.x, m1, n1);
     const int kbeg = blockIdx.y * p.k_per_split;
-    const int nk = p.k_per_split / BK;  // >= 2 (host)
+    const int nk = p.k_per_split / BK;  // >= 2 (host); PERS: even and >= 4
 
     // Per-lane byte offsets of piece 0 of each unit (piece 1 adds the uniform di_a / di_b).
     //  k-contiguous operand: unit image [128 unit-rows][64 k], 128-B rows, 16-B chunk c of row r at
@@ -1001,16 +1038,20 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         return make_rsrc(G + (size_t)r0 * ld + k0, rem);
     };
     // unit u (0 UA0, 1 UA1, 2 UB0, 3 UB1) of K step t -> LDS buffer t & 1
-    auto issue = [&](int u, int t) {
+    auto issue_at = [&](int u, int t, int mm, int nn) {
         const int k0 = kbeg + t * BK;
         char* dst = smem + (t & 1) * BUF + u * UNIT + w * 1024;
         const bool isA = u < 2;
-        const __amdgpu_buffer_rsrc_t r = isA ? rsrc(p.A, p.lda, m0, p.M, k0, TA) : rsrc(p.B, p.ldb, n0, p.N, k0, TB);
+        const __amdgpu_buffer_rsrc_t r = isA ? rsrc(p.A, p.lda, mm, p.M, k0, TA) : rsrc(p.B, p.ldb, nn, p.N, k0, TB);
         uint32_t o = uoff[u];
         const uint32_t di = isA ? di_a : di_b;
         asm volatile("" : "+v"(o));
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, o, 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(dst + 8 * 1024), 16, o + di, 0, 0, 0);
+    };
+    auto issue = [&](int u, int t) {  // K step t of this tile, or t - nk of the next one
+        if (!PERS || t < nk) issue_at(u, t, m0, n0);
+        else issue_at(u, t - nk, m1, n1);
     };
     // MFMA operand fragment (16 unit-rows from rb x 32 k) of a unit: lane l gets unit-row
     // rb + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7
@@ -1061,20 +1102,13 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
                     acc[4 * mh + i][2 * nh + j] =
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[j][ks], FA[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
     };
-    auto wait_vm = [&](int n) {
-        switch (n) {  // wave-uniform compile-time in practice (unrolled phases)
-            case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-            case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-            case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-            case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-            default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        }
-    };
     // one phase: [reads] [copies] vmcnt(n) barrier lgkmcnt(0) | MFMA cluster | barrier
-    auto phase_sync = [&](int n) {
+    // ex (persistent form, first step after an epilogue): the epilogue's ops may stay in flight
+    auto phase_sync = [&](auto nc, auto nxc, bool ex) {
         __builtin_amdgcn_sched_barrier(0);
         if (!(ABL & 4)) {
-            wait_vm(n);
+            if (PERS && ex) wait_vmc<decltype(nxc)::value>();
+            else wait_vmc<decltype(nc)::value>();
             __builtin_amdgcn_s_barrier();
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1088,40 +1122,42 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         __builtin_amdgcn_sched_barrier(0);
     };
     // K step t with this step's / the previous step's issue masks (bit q-1: phase q issues)
-    auto step = [&](int t, auto pmc, auto mc) {
+    // ex: the first K step after a persistent epilogue (EX more ops allowed in flight)
+    constexpr int EX = pp_epi_vmem<EPI>();
+    auto step = [&](int t, auto pmc, auto mc, bool ex) {
         constexpr int PM = decltype(pmc)::value, MK = decltype(mc)::value;
-        auto vm = [](int q) {  // copies allowed in flight before phase q's barrier: phases q-3..q
-            int n = 0;
-            for (int d = 0; d < 4; ++d) {
-                const int x = q - d;  // <= 0: phase x + 4 of the previous step
-                n += (x >= 1 ? (MK >> (x - 1)) & 1 : (PM >> (x + 3)) & 1) ? 2 : 0;
-            }
-            return n;
-        };
+        using V1 = std::integral_constant<int, pp_vm_allow(PM, MK, 1, 0)>;
+        using V2 = std::integral_constant<int, pp_vm_allow(PM, MK, 2, 0)>;
+        using V3 = std::integral_constant<int, pp_vm_allow(PM, MK, 3, 0)>;
+        using V4 = std::integral_constant<int, pp_vm_allow(PM, MK, 4, 0)>;
+        using X1 = std::integral_constant<int, pp_vm_allow(PM, MK, 1, EX)>;
+        using X2 = std::integral_constant<int, pp_vm_allow(PM, MK, 2, EX)>;
+        using X3 = std::integral_constant<int, pp_vm_allow(PM, MK, 3, EX)>;
+        using X4 = std::integral_constant<int, pp_vm_allow(PM, MK, 4, EX)>;
         const int cur = t & 1;
         constexpr bool RD = !(ABL & 2), CP = !(ABL & 1);
         // P1
         if (RD) readA(cur, 0);
         if (RD) readB(FB0, cur, 0);
         if (CP && (MK & 1)) issue(3, t + 1);
-        phase_sync(vm(1));
+        phase_sync(V1{}, X1{}, ex);
         quad(FB0, 0, 0);
         phase_end();
         // P2
         if (RD) readB(FB1, cur, 1);
         if (CP && (MK & 2)) issue(1, t + 1);
-        phase_sync(vm(2));
+        phase_sync(V2{}, X2{}, ex);
         quad(FB1, 0, 1);
         phase_end();
         // P3
         if (RD) readA(cur, 1);
         if (CP && (MK & 4)) issue(0, t + 2);
-        phase_sync(vm(3));
+        phase_sync(V3{}, X3{}, ex);
         quad(FB1, 1, 1);
         phase_end();
         // P4
         if (CP && (MK & 8)) issue(2, t + 2);
-        phase_sync(vm(4));
+        phase_sync(V4{}, X4{}, ex);
         quad(FB0, 1, 0);
         phase_end();
     };
@@ -1144,22 +1180,55 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     using I15 = std::integral_constant<int, 15>;
     using I3 = std::integral_constant<int, 3>;
     using I0 = std::integral_constant<int, 0>;
-    int t = 0;
+    auto epilogue = [&]() {
+        if (ABL & 8) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+        } else {
+            auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
+            GemmParams q = p;
+            if (ABL & 16) q.M = 0;  // ablation: every store falls outside the buffer (issued, dropped)
+            epilogue_store<EPI, 4>(q, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
+        }
+    };
+    if constexpr (!PERS) {
+        int t = 0;
 #pragma clang loop unroll(disable)
-    for (; t < nk - 2; ++t) step(t, I15{}, I15{});
-    step(t, I15{}, I3{});      // t = nk-2: P3 / P4 have no step t+2
-    step(t + 1, I3{}, I0{});   // t = nk-1: nothing left to stage
-
-    if (ABL & 8) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+        for (; t < nk - 2; ++t) step(t, I15{}, I15{}, false);
+        step(t, I15{}, I3{}, false);      // t = nk-2: P3 / P4 have no step t+2
+        step(t + 1, I3{}, I0{}, false);   // t = nk-1: nothing left to stage
+        epilogue();
     } else {
-        auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
-        GemmParams q = p;
-        if (ABL & 16) q.M = 0;  // ablation: every store falls outside the buffer (issued, dropped)
-        epilogue_store<EPI, 4>(q, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
+        // ONE step instantiation (a loop of several spilled the accumulators): every step stages
+        // (the last tile's last two re-stage its own first steps, never read), and step 0 may leave
+        // the previous epilogue's ops in flight — for the first tile the prologue wait below already
+        // retired everything step 0 reads.
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // UB1(0), UA1(0) landed too
+        if (!has_next) {
+            m1 = m0;
+            n1 = n0;
+        }
+        int t = 0;
+#pragma clang loop unroll(disable)
+        while (true) {
+            step(t, I15{}, I15{}, t == 0);
+            if (++t < nk) continue;
+            epilogue();
+            if (!has_next) break;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            item += gridDim.x;
+            m0 = m1;
+            n0 = n1;
+            has_next = item + (int)gridDim.x < p.tiles;
+            if (has_next) coords(item + gridDim.x, m1, n1);
+            t = 0;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unread re-staged copies
     }
     if (!wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
 }
@@ -1231,6 +1300,20 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
             case 26: gemm_pp<false, false, 0, 15><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only, no epilogue
             case 28: gemm_pp<false, false, 0, 16><<<grid, NTHR, 0, s>>>(p); break;  // stores dropped
             default: gemm_pp<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;   // no sync
+        }
+        TDL_LAUNCH_CHECK();
+    }
+    if (variant == 35 && !ta && !tb && kps / BK >= 4 && (kps / BK) % 2 == 0) {  // persistent ping-pong
+        const int g8 = num_cus() & ~7;
+        const dim3 pgrid(p.tiles < g8 ? p.tiles : g8, split);
+        switch (epi) {
+            case 0: gemm_pp<false, false, 0, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            case 1: gemm_pp<false, false, 1, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            case 2: gemm_pp<false, false, 2, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            case 3: gemm_pp<false, false, 3, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            case 4: gemm_pp<false, false, 4, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            case 5: gemm_pp<false, false, 5, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, 6, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
         }
         TDL_LAUNCH_CHECK();
     }

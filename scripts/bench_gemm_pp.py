@@ -32,7 +32,8 @@ def relerr(x, ref):
 def check(dev, variants):
     torch.manual_seed(0)
     out = []
-    for (M, K, N) in [(1000, 128, 200), (256, 192, 256), (4104, 1024, 1032), (32768, 1024, 1024)]:
+    for (M, K, N) in [(1000, 128, 200), (256, 192, 256), (4104, 1024, 1032), (32768, 1024, 1024),
+                      (8200, 512, 8200)]:  # last: > 1 tile per workgroup of the persistent form, ragged
         a = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
         bt = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).bfloat16()
         bias = (torch.rand(N, device=dev) - 0.5).bfloat16()

@@ -146,3 +146,41 @@ def test_production_shape_fwd_dgrad():
     assert _rel(gemm.matmul(x, w), x.float() @ w.float()) < 1e-2
     dy = _rand(M, N)
     assert _rel(gemm.matmul(dy, w.t()), dy.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(8200, 8200, 256), (33000, 1032, 512), (4096, 2048, 1024)])
+def test_persistent_pingpong_epilogues(M, N, K):
+    """tdl_gemm variant 35 (persistent ping-pong: > 1 tile per workgroup, the next tile's first K
+    steps staged during the current tile's last, stores drained behind the next tile's MFMAs)
+    against fp32 torch on ragged M / N, every epilogue the GPT-2 block uses (bias, bias+GELU with the
+    pre-activation, residual add, dGELU with bias-gradient column sums, fp32 accumulate)."""
+    from trustworthy_dl.ops import gemm
+    x = _rand(M, K)
+    wt = _rand(N, K, scale=0.1)
+    bias = _rand(N, scale=0.5)
+    ref = x.float() @ wt.float().t()
+    old = gemm.VARIANT
+    gemm.VARIANT = 35
+    try:
+        y = gemm.matmul(x, wt.t(), bias=bias)
+        assert _rel(y, ref + bias.float()) < 1e-2
+        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        f = gemm.matmul(x, wt.t(), bias=bias, epi="gelu", aux=pre)
+        assert _rel(pre, ref + bias.float()) < 1e-2
+        assert _rel(f, F.gelu(ref + bias.float(), approximate="tanh")) < 1e-2
+        res = _rand(M, N)
+        out = res.clone()
+        gemm.matmul(x, wt.t(), out=out, epi="resadd")
+        assert _rel(out, res.float() + ref) < 1e-2
+        colsum = torch.zeros(N, device=DEV)
+        dy = _rand(M, K)
+        d = gemm.matmul(dy, wt.t(), epi="dgelu", aux=pre, colsum=colsum)
+        u = pre.float().requires_grad_(True)
+        (gr,) = torch.autograd.grad(F.gelu(u, approximate="tanh"), u, dy.float() @ wt.float().t())
+        assert _rel(d, gr) < 2e-2
+        assert _rel(colsum, gr.sum(0)) < 2e-2
+        acc = torch.ones(M, N, device=DEV)
+        gemm._launch(x, wt.t(), acc, N, "f32acc")
+        assert _rel(acc, ref + 1.0) < 1e-4
+    finally:
+        gemm.VARIANT = old
