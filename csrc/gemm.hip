@@ -973,8 +973,14 @@ __device__ __forceinline__ void wait_vmc() {
 // blockIdx.x, + gridDim.x, ...; the copies of the next tile's first two K steps are issued during
 // the current tile's last two (the K-step sequence runs on across tiles, nk even keeps the LDS
 // buffer parity), so neither the pipeline fill nor the store drain of a tile is exposed.
-template <bool TA, bool TB, int EPI, int ABL = 0, bool PERS = false>
+// LEPI (EPI_BF16 / EPI_GELU, one tile per workgroup): LDS-staged epilogue — after the K loop each
+// wave writes its 128 x 64 bf16 block into its own 16 KiB of the (then idle) operand LDS (16-B chunks
+// XOR-swizzled by row) and reads it back row-contiguous, so every store instruction writes 8 whole
+// 128-B row segments (1 KiB) instead of 16 rows x 32 B: a quarter of the store instructions and
+// L2 requests of the direct MFMA-layout store.
+template <bool TA, bool TB, int EPI, int ABL = 0, bool PERS = false, bool LEPI = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
+    static_assert(!LEPI || (!PERS && EPI <= EPI_DGELU), "LDS epilogue: bf16 outputs, one tile");
     // ABL (timing-only ablations, wrong results): 1 = no copies in the K loop, 2 = no fragment
     // reads in the K loop, 4 = no waits / barriers in the K loop, 8 = no epilogue stores
     static_assert(!PERS || (!TA && !TB), "persistent ping-pong: k-contiguous operands only");
@@ -1193,7 +1199,131 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
             epilogue_store<EPI, 4>(q, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
         }
     };
-    if constexpr (!PERS) {
+    if constexpr (LEPI) {
+        int t = 0;
+#pragma clang loop unroll(disable)
+        for (; t < nk - 2; ++t) step(t, I15{}, I15{}, false);
+        step(t, I15{}, I3{}, false);
+        step(t + 1, I3{}, I0{}, false);
+        // group 0's extra barrier first: past it every wave has retired its last fragment reads and
+        // waited its last copies (vmcnt(0) in the final phase), so the operand LDS is free
+        if (!wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");  // no LDS access of the epilogue moves above that barrier
+        __builtin_amdgcn_sched_barrier(0);
+        char* ws = smem + w * 16384;
+        const int g = lane >> 4, rl = lane & 15;
+        const int mw = m0 + wr * 128, nw = n0 + wc * 64;
+        const long long rem = (long long)(p.M - mw) * p.ldc * 2;
+        const __amdgpu_buffer_rsrc_t rc = make_rsrc((const bf16_t*)p.C + (size_t)mw * p.ldc, rem);
+        const __amdgpu_buffer_rsrc_t rx =
+            EPI == EPI_GELU || EPI == EPI_DGELU ? make_rsrc(p.aux + (size_t)mw * p.ldc, rem) : rc;
+        const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
+        float bv[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = nw + 16 * j + 4 * g;
+            const u32x2_t b = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
+            unpack4(make_uint2(b.x, b.y), bv[j]);
+        }
+        // read-back: lane -> row 8 q + (lane >> 3), 16-B chunk lane & 7 (columns nw + 8 c ..+7)
+        const int cb = lane & 7;
+        const uint32_t coff = nw + 8 * cb < p.N ? (uint32_t)(nw + 8 * cb) * 2u : 0x80000000u;
+        auto pass = [&](bool post, __amdgpu_buffer_rsrc_t dst) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = acc[i][j][r] + bv[j][r];
+                        if (post) v[r] = gelu_tanh(v[r]);
+                    }
+                    const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
+                    *(uint2*)(ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3)) = pack4(v);
+                }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + (lane >> 3);
+                const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
+                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, dst, off, 0, 0);
+            }
+        };
+        if constexpr (EPI == EPI_RESADD || EPI == EPI_DGELU) {
+            // the operand tile (residual C / pre-activation aux) comes in the same way reversed:
+            // row-contiguous 16-B loads -> swizzled LDS -> each lane's MFMA-layout 4-vectors, which
+            // the lane combines with its accumulators in fp32 and writes back to the same 8 bytes
+            const __amdgpu_buffer_rsrc_t rs = EPI == EPI_RESADD ? rc : rx;
+            uint4 ld[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + (lane >> 3);
+                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+                const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+                ld[q] = make_uint4(v[0], v[1], v[2], v[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + (lane >> 3);
+                *(uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4)) = ld[q];
+            }
+            float csum[4][4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
+                    char* a8 = ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3);
+                    float o[4], v[4];
+                    unpack4(*(const uint2*)a8, o);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if constexpr (EPI == EPI_RESADD) {
+                            v[r] = acc[i][j][r] + bv[j][r] + o[r];
+                        } else {
+                            v[r] = acc[i][j][r] * gelu_tanh_grad(o[r]);
+                            csum[j][r] = (i == 0 ? 0.f : csum[j][r]) + v[r];
+                        }
+                    }
+                    *(uint2*)a8 = pack4(v);
+                }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 8 * q + (lane >> 3);
+                const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
+                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, rc, off, 0, 0);
+            }
+            if constexpr (EPI == EPI_DGELU) {
+                if (p.colsum != nullptr) {  // rows past M / columns past N had zero operands
+                    const __amdgpu_buffer_rsrc_t rsum = make_rsrc(p.colsum, (long long)p.N * 4);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            float t = csum[j][r];
+                            t += __shfl_xor(t, 1, 64);
+                            t += __shfl_xor(t, 2, 64);
+                            t += __shfl_xor(t, 4, 64);
+                            t += __shfl_xor(t, 8, 64);
+                            csum[j][r] = t;
+                        }
+                        const int n = nw + 16 * j + 4 * g, r = lane & 3;
+                        const float t = r == 0 ? csum[j][0] : r == 1 ? csum[j][1] : r == 2 ? csum[j][2] : csum[j][3];
+                        const bool writer = (lane & 15) < 4 && n + r < p.N;
+                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(t, rsum, writer ? (uint32_t)(n + r) * 4u : 0x80000000u, 0, 0);
+                    }
+                }
+            }
+        } else if constexpr (EPI == EPI_GELU) {
+            pass(false, rx);  // the pre-activation
+            pass(true, rc);
+        } else {
+            pass(false, rc);
+        }
+        return;
+    } else if constexpr (!PERS) {
         int t = 0;
 #pragma clang loop unroll(disable)
         for (; t < nk - 2; ++t) step(t, I15{}, I15{}, false);
@@ -1303,6 +1433,16 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         }
         TDL_LAUNCH_CHECK();
     }
+    if (variant == 36 && !ta && !tb && epi <= EPI_DGELU && split == 1 && kps / BK >= 2 && p.ldc % 8 == 0) {
+        switch (epi) {
+            case EPI_BF16: gemm_pp<false, false, EPI_BF16, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_GELU: gemm_pp<false, false, EPI_GELU, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_RESADD: gemm_pp<false, false, EPI_RESADD, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, EPI_DGELU, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
+        }
+        TDL_LAUNCH_CHECK();
+    }
+    if (variant == 36) variant = 20;  // other epilogues / layouts: the direct-store ping-pong
     if (variant == 35 && !ta && !tb && kps / BK >= 4 && (kps / BK) % 2 == 0) {  // persistent ping-pong
         const int g8 = num_cus() & ~7;
         const dim3 pgrid(p.tiles < g8 ? p.tiles : g8, split);

@@ -148,19 +148,21 @@ def test_production_shape_fwd_dgrad():
     assert _rel(gemm.matmul(dy, w.t()), dy.float() @ w.float().t()) < 1e-2
 
 
+@pytest.mark.parametrize("variant", [35, 36])
 @pytest.mark.parametrize("M,N,K", [(8200, 8200, 256), (33000, 1032, 512), (4096, 2048, 1024)])
-def test_persistent_pingpong_epilogues(M, N, K):
+def test_persistent_pingpong_epilogues(M, N, K, variant):
     """tdl_gemm variant 35 (persistent ping-pong: > 1 tile per workgroup, the next tile's first K
-    steps staged during the current tile's last, stores drained behind the next tile's MFMAs)
-    against fp32 torch on ragged M / N, every epilogue the GPT-2 block uses (bias, bias+GELU with the
-    pre-activation, residual add, dGELU with bias-gradient column sums, fp32 accumulate)."""
+    steps staged during the current tile's last, stores drained behind the next tile's MFMAs) and
+    36 (LDS-staged row-contiguous epilogues: stores, and the residual / pre-activation loads) against fp32 torch on ragged M / N,
+    every epilogue the GPT-2 block uses (bias, bias+GELU with the pre-activation, residual add,
+    dGELU with bias-gradient column sums, fp32 accumulate)."""
     from trustworthy_dl.ops import gemm
     x = _rand(M, K)
     wt = _rand(N, K, scale=0.1)
     bias = _rand(N, scale=0.5)
     ref = x.float() @ wt.float().t()
     old = gemm.VARIANT
-    gemm.VARIANT = 35
+    gemm.VARIANT = variant
     try:
         y = gemm.matmul(x, wt.t(), bias=bias)
         assert _rel(y, ref + bias.float()) < 1e-2
