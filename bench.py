@@ -277,6 +277,7 @@ def run(args):
                        "detections": len(engine.attack_history),
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
+                       "native_gemm": os.environ.get("TDL_NATIVE_GEMM", "mlp"),
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        "reassignments": [{"step": r["step"], "from_nodes": r["from_nodes"],
                                           "migration_ms": round(1000 * r["migration_time"], 2),

@@ -15,13 +15,13 @@ is one ``torch.autograd.Function`` whose forward/backward call the gfx950 kernel
 * the bias gradients of the two residual-stream projections (``bp`` = colsum(dy), ``bo`` =
   colsum(dy1)) are column partials of that same LayerNorm-backward pass, not separate reductions;
 * weight gradients accumulate in fp32 straight into ``param.main_grad`` (GEMM beta=1 epilogue);
-* optionally the MLP's elementwise work rides in the native MFMA GEMM's epilogue (csrc/gemm.hip):
-  forward ``f = gelu(h2 @ Wfc + bfc)`` stores the pre-activation and the activation from one
-  kernel, backward ``dpre = (dy @ Wp^T) * gelu'(pre)`` accumulates the ``bfc`` gradient as column
-  sums in the same kernel (TDL_NATIVE_GEMM=mlp; ``all`` also routes the plain projections to it).
-  The default is ``off`` (hipBLASLt + the separate bias/GELU kernels) because that measures
-  faster on MI355X today: profiles/r2_gemm_native_vs_hipblaslt.jsonl (native 0.69-0.86x of
-  hipBLASLt per product) and profiles/r2_gemm_fused_epilogue_vs_lib.jsonl (fused 0.65-0.77x);
+* the MLP's elementwise work rides in the native MFMA GEMM's epilogue (csrc/gemm.hip, ping-pong
+  kernel with LDS-staged row-contiguous epilogues): forward ``f = gelu(h2 @ Wfc + bfc)`` stores the
+  pre-activation and the activation from one kernel, backward ``dpre = (dy @ Wp^T) * gelu'(pre)``
+  accumulates the ``bfc`` gradient as column sums in the same kernel (TDL_NATIVE_GEMM=mlp, the
+  default: 1.005x / 1.20x of hipBLASLt + the separate pass, profiles/r2_gemm_fused_lds_epilogue.jsonl;
+  +1.5 % per step, profiles/r2_native_mlp_ab.txt).  ``all`` also routes the plain projections to
+  it (0.81-0.88x of hipBLASLt per product: slower), ``off`` keeps hipBLASLt + the bias/GELU kernels;
 * autograd bookkeeping is one node per block instead of ~12 (host time matters at 8 stages x
   64 micro-batches per step).
 
@@ -144,7 +144,11 @@ def _colsum_into(acc, d):
 
 
 def _native_gemm_mode() -> str:
-    return os.environ.get("TDL_NATIVE_GEMM", "off")
+    # default "mlp": the MLP's fc forward (bias + GELU epilogue, pre-activation stored) and its
+    # proj dgrad (dGELU epilogue + bias-gradient column sums) run on the native MFMA GEMM — +1.5 %
+    # per step over hipBLASLt + separate passes (profiles/r2_native_mlp_ab.txt); "all" also routes
+    # the plain projections (slower: 0.81-0.88x of hipBLASLt), "off" keeps every product on the library
+    return os.environ.get("TDL_NATIVE_GEMM", "mlp")
 
 
 def _native_mlp(h2, wfc, bfc) -> bool:

@@ -25,11 +25,12 @@ from ._lib import ptr, stream_ptr
 
 EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f32atomic": 6}
 BK = 64
-# A/B switch for benchmarks: 0 = shipped kernel (8-wave, pipelined), 1 = plain (unpipelined)
-# schedule, >= 2 = schedule variants / persistent kernels of tdl_gemm (NT, bf16 out only; some are
-# timing-only ablations), 20 = the staggered ping-pong kernel (NT, every epilogue), 21..28 its
-# timing-only ablations (csrc/gemm.hip tdl_gemm; profiles/r2_gemm_pingpong_ablation.jsonl)
-VARIANT = 0
+# Kernel selection (TDL_GEMM_VARIANT): 36 (default) = the staggered ping-pong kernel with the
+# LDS-staged row-contiguous epilogues on NT operands (bias / GELU / residual add / dGELU; the other
+# layouts and fp32 outputs take the ping-pong kernel's direct stores, 20), 0 = the 8-wave pipelined
+# kernel, 1 = its plain schedule, 2..19 / 21..35 = schedule variants, persistent forms and
+# timing-only ablations (csrc/gemm.hip tdl_gemm; profiles/r2_gemm_*.jsonl)
+VARIANT = int(os.environ.get("TDL_GEMM_VARIANT", "36"))
 
 
 def _operand_a(a: torch.Tensor):
