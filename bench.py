@@ -119,7 +119,16 @@ def main():
 
 
 _WATCHDOG = None
-METRIC = "tokens/sec GPT-2-medium MP=N with grad-verify on"
+METRIC = "tokens/sec GPT-2-medium MP=N with grad-verify on"   # the BASELINE.json headline (defaults)
+
+
+def _metric(args) -> str:
+    """The headline name for the default run; other models / --no-verify say what they measured."""
+    if args.model == "gpt2-medium" and not args.no_verify:
+        return METRIC
+    name = {"gpt2-small": "GPT-2-small", "gpt2-medium": "GPT-2-medium", "gpt2-large": "GPT-2-large",
+            "gpt2-xl": "GPT-2-xl"}.get(args.model, args.model)
+    return f"tokens/sec {name} MP=N with grad-verify {'off' if args.no_verify else 'on'}"
 
 
 def _failure_line(args, kind: str, marks, errors) -> str:
@@ -134,7 +143,7 @@ def _failure_line(args, kind: str, marks, errors) -> str:
     else:
         msg = kind
     return json.dumps({
-        "metric": METRIC, "value": None, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "metric": _metric(args), "value": None, "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens, random-init weights",
         "error": msg, "failure_kind": kind,
@@ -264,7 +273,7 @@ def run(args):
     tps = tokens / elapsed
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": _metric(args),
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
