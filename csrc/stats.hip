@@ -366,7 +366,32 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
         const float nr = proc(g[i], ref ? ref[i] : 0.f);
         if (ref) ref[i] = nr;
     }
-    for (int64_t i = vbeg + 4 * (int64_t)threadIdx.x; i < vend; i += 4 * (int64_t)blockDim.x) {
+    // main body: 4 float4 per lane per trip, every load issued before any math (a layer's chunks
+    // are ~1.5 blocks per CU, so latency is hidden by loads in flight, not by occupancy)
+    int64_t i = vbeg + 4 * (int64_t)threadIdx.x;
+    const int64_t step = 4 * (int64_t)blockDim.x;
+    for (; i + 3 * step < vend; i += 4 * step) {
+        float4 v[4], r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(g + i + u * step);
+        if (ref) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = *(const float4*)(ref + i + u * step);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float4 nr;
+            nr.x = proc(v[u].x, r[u].x);
+            nr.y = proc(v[u].y, r[u].y);
+            nr.z = proc(v[u].z, r[u].z);
+            nr.w = proc(v[u].w, r[u].w);
+            if (ref) *(float4*)(ref + i + u * step) = nr;
+        }
+    }
+    for (; i < vend; i += step) {
         const float4 v = *(const float4*)(g + i);
         const float4 r = ref ? *(const float4*)(ref + i) : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 nr;

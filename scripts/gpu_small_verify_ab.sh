@@ -5,8 +5,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
 out=gpurun_out/small_verify_ab.txt
 : > $out
-for round in 1 2; do
-  for model in gpt2-small gpt2-medium; do
+for round in $(seq 1 ${ROUNDS:-2}); do
+  for model in ${MODELS:-gpt2-small gpt2-medium}; do
     for v in on off; do
       flag=""; [ $v = off ] && flag="--no-verify"
       timeout -k 10 200 python -u bench.py --model $model --steps 10 --warmup 3 $flag > gpurun_out/sv.json 2> gpurun_out/sv.err || { echo "$model $v failed"; tail -5 gpurun_out/sv.err; exit 1; }
