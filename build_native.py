@@ -87,8 +87,7 @@ def build(arch: str = "gfx950", jobs: int = 8, debug: bool = False, verbose: boo
     if kobjs:
         lib = os.path.join(OUT_DIR, "libtdl_kernels.so")
         if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in kobjs):
-            rc, cmd, out = _run([cc, f"--offload-arch={arch}", "-shared", "-fPIC", *kobjs, "-L/opt/rocm/lib",
-                                  "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib", "-o", lib + ".tmp"])
+            rc, cmd, out = _run([cc, f"--offload-arch={arch}", "-shared", "-fPIC", *kobjs, "-o", lib + ".tmp"])
             if rc != 0:
                 print(cmd)
                 print(out)

@@ -12,23 +12,21 @@
 //   dgrad    dx = dy W^T   : A = dy [M][out] (TA=0), B = W [in][out]  (TB=0: rows = in, k = out)
 //   wgrad    dW = x^T dy   : A = x  [M][in]  (TA=1: rows = in, k = M), B = dy [M][out] (TB=1)
 //
-// Geometry: workgroup tile 256 x 256, K step 64, 512 threads = 8 waves as 2 (m) x 4 (n); each wave
-// owns a 128 x 64 output block = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 (the 16x16 shape holds a
-// higher clock than 32x32x16 on random data, cdna_hip_programming.md rule 28).  The MFMA "A"
-// operand is the B tile and the MFMA "B" operand the A tile, so the accumulator of a tile holds
-// D[n][m]: lane l owns output row m = l & 15 and FOUR CONSECUTIVE columns n = 4 (l >> 4) + 0..3 —
-// one 8-byte bf16 / 16-byte fp32 vector store per (tile, lane), no shuffles.
+// Two kernels, both on a 256 x 256 x 64 workgroup tile of v_mfma_f32_16x16x32_bf16 (the 16x16
+// shape holds a higher clock than 32x32x16 on random data, cdna_hip_programming.md rule 28):
+//   gemm_p4  persistent grid (one workgroup per CU walks its tiles), 4 waves of 128 x 128 with the
+//            256 accumulators per lane in AGPRs, operands register-staged two K steps ahead;
+//   gemm_pp  one tile per workgroup, 8 waves of 128 x 64 in two groups staggered by one barrier,
+//            operands staged by LDS-DMA (buffer_load ... lds), optional LDS-staged epilogue.
+// In both, the MFMA "A" operand is the B tile and the MFMA "B" operand the A tile, so the
+// accumulator of a tile holds D[n][m]: lane l owns output row m = l & 15 and FOUR CONSECUTIVE
+// columns n = 4 (l >> 4) + 0..3 — one 8-byte bf16 / 16-byte fp32 vector store per (tile, lane).
 //
-// Staging: both operands go global -> LDS with global_load_lds_dwordx4 (1 KiB per wave
-// instruction, lane-linear LDS image), two LDS stages of 64 KiB (one K step of A and B each).
-//   k-contiguous tile [256 rows][64 k] : 128-B rows, 16-B chunk c of row r stored at c ^ (r & 7)
-//       (source-address permutation, cdna_hip_programming.md rule 21); fragments read with
-//       ds_read_b128 — every 16-lane group of a read hits 16 distinct bank slots.
-//   row-contiguous tile [64 k][256 rows] : 512-B k-rows, 32-B block b of k-row k stored at
-//       b ^ f(k), f(k) = (k & 3) | ((k >> 1) & 4); fragments read with ds_read_b64_tr_b16 (T10):
-//       the 8 k-rows a 32-lane half touches map to 8 distinct 32-B bank blocks (conflict-free).
-// The tile for K step t+1 is issued at the top of step t and waited for (vmcnt(0) + barrier) at
-// its end, so each DMA has a whole step of MFMA work (~2k cycles per SIMD) to land.
+// LDS images (16-byte chunks, conflict-free fragment reads):
+//   k-contiguous tile [rows][64 k] : 128-B rows, 16-B chunk c of row r stored at c ^ (r & 7)
+//       (source-address permutation, cdna_hip_programming.md rule 21); fragments via ds_read_b128.
+//   row-contiguous tile [64 k][rows] : 32-B block b of k-row k stored at b ^ f(k),
+//       f(k) = (k & 3) | ((k >> 1) & 4); fragments via ds_read_b64_tr_b16 (T10).
 //
 // Epilogues (EPI):
 //   0 BF16      C = bf16(acc (+ bias[n]))
@@ -72,7 +70,6 @@ struct GemmParams {
     long long split_stride;  // EPI_F32: elements between split slabs
     int tiles_n, tiles;
     int splits;
-    int rotate;  // persistent kernels: rotate the K order per XCD group
 };
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
@@ -185,285 +182,17 @@ __device__ __forceinline__ bf16x8_t frag(const char* tile, int rb, int ks, int l
     }
 }
 
-template <bool TA, bool TB, int EPI, int SCHED>
-__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w >> 2, wn = w & 3;
-    const int wg = xcd_remap(blockIdx.x, p.tiles);
-    const int tm = wg / p.tiles_n, tn = wg - tm * p.tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = blockIdx.y * p.k_per_split;
-    const int kend = min(p.K, kbeg + p.k_per_split);
-    const int nk = (kend - kbeg) / BK;
-
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    Stager<TA> sa;
-    Stager<TB> sb;
-    sa.init(p.lda, m0, p.M, w, lane);
-    sb.init(p.ldb, n0, p.N, w, lane);
-    auto stage_a = [&](int t, int buf) { sa.issue(p.A, p.lda, m0, p.M, kbeg + t * BK, smem + buf * STAGE_BYTES, w); };
-    auto stage_b = [&](int t, int buf) {
-        sb.issue(p.B, p.ldb, n0, p.N, kbeg + t * BK, smem + buf * STAGE_BYTES + TILE_BYTES, w);
-    };
-    // fragments: B tiles j = 0..3 (MFMA A operand) of one 32-deep sub-step; A tiles in two halves
-    auto load_b = [&](bf16x8_t (&f)[4], int buf, int ks) {
-        const char* Bt = smem + buf * STAGE_BYTES + TILE_BYTES;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = frag<TB>(Bt, wn * 64 + 16 * j, ks, lane);
-    };
-    auto load_a = [&](bf16x8_t (&f)[4], int buf, int ks, int half) {
-        const char* At = smem + buf * STAGE_BYTES;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = frag<TA>(At, wm * 128 + 64 * half + 16 * i, ks, lane);
-    };
-    auto mma = [&](const bf16x8_t (&fb)[4], const bf16x8_t (&fa)[4], int half) {
-        if (SCHED & 16) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[4 * half + i][j] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * half + i][j], 0, 0, 0);
-        if (SCHED & 16) __builtin_amdgcn_s_setprio(0);
-    };
-    // Quarter-step scheduling region: with SCHED bit 5 the reads / DMAs issued in the region are
-    // spread between its 16 MFMAs (one after each of the first ones) instead of issued up front.
-    constexpr int RD = TA ? 2 : 1, RDB = TB ? 2 : 1;  // LDS read instructions per fragment
-    auto region_end = [&](int n_ds, int n_vm) {
-        if (SCHED & 32) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // 1 MFMA
-                if (k < n_vm) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 DMA (VMEM read)
-                if (2 * k < n_ds) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 LDS reads
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto vm_wait = [&](int n) {  // s_waitcnt vmcnt(n) lgkmcnt(0), n in {0, 4, 8}
-        if (SCHED & 4) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        } else if (n >= 8) {
-            asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-        } else if (n >= 4) {
-            asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        }
-    };
-    auto barrier = [&]() {
-        if (!(SCHED & 8)) __builtin_amdgcn_s_barrier();
-    };
-
-    if (SCHED == 0) {
-        if (nk > 0) {
-            stage_a(0, 0);
-            stage_b(0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        for (int t = 0; t < nk; ++t) {
-            const int cur = t & 1;
-            if (t + 1 < nk) {
-                stage_a(t + 1, cur ^ 1);
-                stage_b(t + 1, cur ^ 1);
-            }
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks) {
-                bf16x8_t fb[4], fa0[4], fa1[4];
-                load_b(fb, cur, ks);
-                load_a(fa0, cur, ks, 0);
-                load_a(fa1, cur, ks, 1);
-                mma(fb, fa0, 0);
-                mma(fb, fa1, 1);
-            }
-            // tile t+1 landed (own DMAs) and this wave's reads of stage `cur` retired, then the
-            // barrier publishes both to the other waves (stage `cur` is restaged at step t+1)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-    } else {
-        // Software pipeline in quarter steps (16 MFMAs per wave each):
-        //   Q1 (t,ks0): MFMA B0 x Alo   | read Ahi(t,0)            [| DMA B of tile t+1 (default)]
-        //   Q2 (t,ks0): MFMA B0 x Ahi   | read B1(t,1), Alo(t,1)
-        //   Q3 (t,ks1): MFMA B1 x Alo   | read Ahi(t,1)            [| bit 1: barrier, DMA B of t+2]
-        //   Q4 (t,ks1): [own DMAs of tile t+1 done, own reads of stage t&1 done] barrier |
-        //               DMA A of tile t+2 into stage t&1; read B0(t+1,0), Alo(t+1,0);  MFMA B1 x Ahi
-        // Every fragment read has a quarter step (16 MFMAs per wave) to land, every DMA 3-5 quarters.
-        constexpr bool B_EARLY = (SCHED & 2) != 0;
-        bf16x8_t B0[4], B1[4], Alo[4], Ahi[4];
-        if (nk > 0) {
-            stage_a(0, 0);
-            stage_b(0, 0);
-            if (nk > 1) {
-                if (B_EARLY) stage_b(1, 1);
-                stage_a(1, 1);
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed
-                if (!B_EARLY) {
-                    __builtin_amdgcn_s_barrier();
-                } else {
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                    __builtin_amdgcn_s_barrier();
-                }
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-            load_b(B0, 0, 0);
-            load_a(Alo, 0, 0, 0);
-        }
-        for (int t = 0; t < nk; ++t) {
-            const int cur = t & 1;
-            // Q1
-            const bool b_now = !B_EARLY && t + 1 < nk;
-            if (b_now) stage_b(t + 1, cur ^ 1);
-            load_a(Ahi, cur, 0, 1);
-            mma(B0, Alo, 0);
-            region_end(4 * RD, b_now ? 4 : 0);
-            // Q2
-            load_b(B1, cur, 1);
-            load_a(Alo, cur, 1, 0);
-            mma(B0, Ahi, 1);
-            region_end(4 * RD + 4 * RDB, 0);
-            // Q3
-            bool b3 = false;
-            if (B_EARLY) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                barrier();
-                if (t + 2 < nk) {
-                    stage_b(t + 2, cur);
-                    b3 = true;
-                }
-            }
-            load_a(Ahi, cur, 1, 1);
-            mma(B1, Alo, 0);
-            region_end(4 * RD, b3 ? 4 : 0);
-            // Q4: default order of DMA groups: A(t+1)@Q4(t-1), B(t+1)@Q1(t) -> wait all (vmcnt 0);
-            //     B_EARLY: B(t+1)@Q3(t-1), A(t+1)@Q4(t-1), B(t+2)@Q3(t) -> vmcnt(4)
-            vm_wait(B_EARLY && b3 ? 4 : 0);
-            barrier();
-            const bool a4 = t + 2 < nk;
-            if (a4) stage_a(t + 2, cur);
-            if (t + 1 < nk) {
-                load_b(B0, cur ^ 1, 0);
-                load_a(Alo, cur ^ 1, 0, 0);
-            }
-            mma(B1, Ahi, 1);
-            region_end(t + 1 < nk ? 4 * RD + 4 * RDB : 0, a4 ? 4 : 0);
-        }
-    }
-
-    // ---------------------------------------------------------------- epilogue
-    const int g = lane >> 4;
-    float csum[4][4];
-    if (EPI == EPI_DGELU) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn * 64 + 16 * j + 4 * g;
-        const bool nok = n < p.N;
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if ((EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_RESADD) && p.bias != nullptr && nok)
-            unpack4(*(const uint2*)(p.bias + n), bv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = m0 + wm * 128 + 16 * i + (lane & 15);
-            if (!(nok && m < p.M)) continue;
-            float v[4] = {acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]};
-            const size_t off = (size_t)m * p.ldc + n;
-            if (EPI == EPI_BF16) {
-                *(uint2*)((bf16_t*)p.C + off) = pack4(v);
-            } else if (EPI == EPI_GELU) {
-                *(uint2*)(p.aux + off) = pack4(v);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-                *(uint2*)((bf16_t*)p.C + off) = pack4(v);
-            } else if (EPI == EPI_RESADD) {
-                float o[4];
-                unpack4(*(const uint2*)((const bf16_t*)p.C + off), o);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] += o[r];
-                *(uint2*)((bf16_t*)p.C + off) = pack4(v);
-            } else if (EPI == EPI_DGELU) {
-                float u[4];
-                unpack4(*(const uint2*)(p.aux + off), u);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    v[r] = acc[i][j][r] * gelu_tanh_grad(u[r]);
-                    csum[j][r] += v[r];
-                }
-                *(uint2*)((bf16_t*)p.C + off) = pack4(v);
-            } else if (EPI == EPI_F32) {
-                float* c = (float*)p.C + (size_t)blockIdx.y * p.split_stride + off;
-                *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-            } else if (EPI == EPI_F32ACC) {
-                float4* c = (float4*)((float*)p.C + off);
-                float4 o = *c;
-                *c = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-            } else {  // EPI_F32ATOM
-                float* c = (float*)p.C + off;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) atomicAdd(c + r, v[r]);
-            }
-        }
-    }
-    if (EPI == EPI_DGELU && p.colsum != nullptr) {
-        // sum over the 16 lanes of a group (rows), then one atomic per column per wave
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = csum[j][r];
-                s += __shfl_xor(s, 1, 64);
-                s += __shfl_xor(s, 2, 64);
-                s += __shfl_xor(s, 4, 64);
-                s += __shfl_xor(s, 8, 64);
-                csum[j][r] = s;
-            }
-        if ((lane & 15) < 4) {
-            const int r = lane & 3;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int n = n0 + wn * 64 + 16 * j + 4 * g + r;
-                const float s = r == 0 ? csum[j][0] : r == 1 ? csum[j][1] : r == 2 ? csum[j][2] : csum[j][3];
-                if (n < p.N) atomicAdd(p.colsum + n, s);
-            }
-        }
-    }
-}
-
-
-// ============================================================================ persistent kernel
-// One workgroup per CU walks its share of the output tiles (and split-K slices): 256 threads =
-// 4 waves as 2 (m) x 2 (n), one wave per SIMD, each wave a 128 x 128 block = 8 x 8 MFMA tiles, so
-// the 256 accumulator registers live in AGPRs and the 512-entry register file is one wave's.
-// Versus 8 waves of 128 x 64 this reads a third less LDS per MFMA (hipBLASLt's fastest gfx950
-// kernels for these shapes use the same geometry and a persistent grid: rocprofv3 SQ_WAVES).
-//
-// The DMA pipeline runs across tile boundaries: step s = (item, k step) is staged into LDS stage
-// s & 1 two steps ahead, so the next tile's first K steps land while the current tile finishes and
-// only the epilogue itself (accumulator read-out + stores) interrupts the MFMA stream.
-// Per step, two phases of 64 MFMAs:
-//   A (k-half 0): MFMAs on F0                      | read F1 = frags(s, k-half 1)
-//   B (k-half 1): [DMA(s+1) landed, own reads of stage s&1 retired] barrier |
-//                 DMA step s+2 -> stage s&1; read F0 = frags(s+1, k-half 0) | MFMAs on F1
-// The DMA copies and fragment reads are spread between the MFMAs (sched_group_barrier), so the
-// single wave of a SIMD keeps its matrix pipe fed while it issues them.
+// ============================================================================ 4-wave helpers
+// Shared by the 4-wave persistent kernel (gemm_p4) and the ping-pong kernel's epilogue: 256-thread
+// workgroups, one wave per SIMD, each wave a 128 x 128 block = 8 x 8 MFMA tiles whose 256
+// accumulator registers live in AGPRs.
 constexpr int PNTHR = 256;
 
+// Fragments of the 4-wave kernel: the B fragments of both k-halves (the next half's are read while
+// the current half's MFMAs use all eight), and ONE set of A fragments — row i of the next half is
+// read into a[i] as soon as the current half's MFMAs of row i are done.
 struct PFrags {
-    bf16x8_t b[8], a[8];
+    bf16x8_t b[2][8], a[8];
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
@@ -589,337 +318,39 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, Get& get, in
     for_tiles<0>(tile);
 }
 
-// ---- asm-owned accumulators: tile T = 8 i + j (i: A tile, j: B tile) lives in a[4T : 4T+3].
-// hipcc cannot keep 256 loop-carried MFMA accumulators in place (it shuffled them through VGPRs
-// inside the K loop, with spills); the MFMAs are therefore inline asm on fixed AGPRs, and one
-// empty asm statement clobbering a0..a255 makes the kernel descriptor allocate them.
+// ---- AGPR accumulators: tile T = 8 i + j (i: A tile, j: B tile) is acc[T].  The MFMAs are inline
+// asm with "+a" operands: the 256 accumulator registers stay in AGPRs for the whole K loop and the
+// register allocator knows they are live (with builtins hipcc shuffled 256 loop-carried accumulators
+// through VGPRs; with a bare AGPR clobber it reused "free" AGPRs for its own values).
+typedef f32x4 Acc[64];
 template <int T>
-__device__ __forceinline__ void amfma(const bf16x8_t& b, const bf16x8_t& a) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(b), "v"(a), "i"(4 * T), "i"(4 * T + 3));
+__device__ __forceinline__ void amfma(Acc& acc, const bf16x8_t& b, const bf16x8_t& a) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[T]) : "v"(b), "v"(a));
 }
 template <int T>
-__device__ __forceinline__ void amfma0(const bf16x8_t& b, const bf16x8_t& a) {  // C = 0: first K step
-    asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, 0" ::"v"(b), "v"(a), "i"(4 * T), "i"(4 * T + 3));
+__device__ __forceinline__ void amfma0(Acc& acc, const bf16x8_t& b, const bf16x8_t& a) {  // C = 0: first K step
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[T]) : "v"(b), "v"(a));
 }
-template <int T>
-__device__ __forceinline__ f32x4 aread() {
-    float x, y, z, w;
-    asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\tv_accvgpr_read_b32 %2, a%c6\n\t"
-                 "v_accvgpr_read_b32 %3, a%c7"
-                 : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
-                 : "i"(4 * T), "i"(4 * T + 1), "i"(4 * T + 2), "i"(4 * T + 3));
-    return f32x4{x, y, z, w};
+// an empty asm that reads and "writes" accumulators B..B+15 (ordering fence for their readers)
+template <int B>
+__device__ __forceinline__ void acc_fence(Acc& acc) {
+    asm volatile("" : "+a"(acc[B + 0]), "+a"(acc[B + 1]), "+a"(acc[B + 2]), "+a"(acc[B + 3]), "+a"(acc[B + 4]),
+                 "+a"(acc[B + 5]), "+a"(acc[B + 6]), "+a"(acc[B + 7]), "+a"(acc[B + 8]), "+a"(acc[B + 9]),
+                 "+a"(acc[B + 10]), "+a"(acc[B + 11]), "+a"(acc[B + 12]), "+a"(acc[B + 13]), "+a"(acc[B + 14]),
+                 "+a"(acc[B + 15]));
 }
 // 64 MFMAs of one 32-deep k-half in tile order T = 0..63; after MFMA T the hook issues that
-// slot's companion instructions (DMA copies / fragment reads), pinned by a scheduling fence
-template <int T, bool ZERO, class Hook>
-__device__ __forceinline__ void mfma_run(const PFrags& f, Hook& hook) {
+// slot's companion instructions (global loads / LDS reads and writes), pinned by a scheduling fence
+template <int H, int T, bool ZERO, class Hook>
+__device__ __forceinline__ void mfma_run(Acc& acc, PFrags& f, Hook& hook) {
     if constexpr (T < 64) {
-        if constexpr (ZERO) amfma0<T>(f.b[T % 8], f.a[T / 8]);
-        else amfma<T>(f.b[T % 8], f.a[T / 8]);
+        if constexpr (ZERO) amfma0<T>(acc, f.b[H][T % 8], f.a[T / 8]);
+        else amfma<T>(acc, f.b[H][T % 8], f.a[T / 8]);
         hook(std::integral_constant<int, T>{});
         __builtin_amdgcn_sched_barrier(0);
-        mfma_run<T + 1, ZERO>(f, hook);
+        mfma_run<H, T + 1, ZERO>(acc, f, hook);
     }
 }
-template <bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(PNTHR, 1) void gemm_persistent(GemmParams p) {
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    asm volatile("" ::: "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255");
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w >> 1, wn = w & 1;
-    const int G = gridDim.x;
-    const int lb = xcd_remap(blockIdx.x, G);
-    const int nk = p.k_per_split / BK;
-    const int n_items = p.tiles * p.splits;
-    const int n_mine = lb < n_items ? (n_items - 1 - lb) / G + 1 : 0;
-    const int total = n_mine * nk;
-    if (total == 0) return;
-
-    // item i of this workgroup -> tile origin and split slice (split-major: the items running at
-    // the same time are consecutive tiles of one slice, which share operand panels in L2)
-    auto coords = [&](int i, int& m0, int& n0, int& sp) {
-        const int item = lb + i * G;
-        sp = item / p.tiles;
-        const int tile = item - sp * p.tiles;
-        const int tm = tile / p.tiles_n;
-        m0 = tm * BM;
-        n0 = (tile - tm * p.tiles_n) * BN;
-    };
-
-    Stager<TA, 4> sa;
-    Stager<TB, 4> sb;
-    // ---- producer (DMA) state: the step it stages next; after the last step it repeats it into
-    // the free stage (harmless, keeps the copy count per K step constant)
-    int pi = 0, pt = 0, pm0, pn0, psp;
-    coords(0, pm0, pn0, psp);
-    sa.init(p.lda, pm0, p.M, w, lane);
-    sb.init(p.ldb, pn0, p.N, w, lane);
-    int prod_left = total;
-    auto produce_rsrc = [&](__amdgpu_buffer_rsrc_t& ra, __amdgpu_buffer_rsrc_t& rb) {
-        const int k0 = psp * p.k_per_split + pt * BK;
-        ra = sa.rsrc(p.A, p.lda, pm0, p.M, k0);
-        rb = sb.rsrc(p.B, p.ldb, pn0, p.N, k0);
-    };
-    auto produce_advance = [&]() {
-        if (--prod_left > 0) {
-            if (++pt == nk) {
-                pt = 0;
-                ++pi;
-                coords(pi, pm0, pn0, psp);
-                sa.init(p.lda, pm0, p.M, w, lane);
-                sb.init(p.ldb, pn0, p.N, w, lane);
-            }
-        } else {
-            prod_left = 0;
-        }
-    };
-    auto frag_b = [&](int buf, int j, int ks) {
-        return frag<TB>(smem + buf * STAGE_BYTES + TILE_BYTES, wn * 128 + 16 * j, ks, lane);
-    };
-    auto frag_a = [&](int buf, int i, int ks) { return frag<TA>(smem + buf * STAGE_BYTES, wm * 128 + 16 * i, ks, lane); };
-
-    PFrags F0, F1;
-    {   // prologue: steps 0 and 1 in flight, step 0's first k-half in registers
-        __amdgpu_buffer_rsrc_t ra, rb;
-        for (int st = 0; st < 2; ++st) {
-            produce_rsrc(ra, rb);
-            char* base = smem + st * STAGE_BYTES;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                sa.piece(ra, base, w, i);
-                sb.piece(rb, base + TILE_BYTES, w, i);
-            }
-            produce_advance();
-        }
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 landed, step 1 in flight
-        __builtin_amdgcn_s_barrier();
-#pragma unroll
-        for (int j = 0; j < 8; ++j) F0.b[j] = frag_b(0, j, 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) F0.a[i] = frag_a(0, i, 0);
-    }
-
-    int s = 0;
-    bool prev_epi = false;
-    for (int ci = 0; ci < n_mine; ++ci) {
-        int cm0, cn0, csp;
-        coords(ci, cm0, cn0, csp);
-        int ct = 0;
-#pragma clang loop unroll(disable)
-        do {
-            const int cur = s & 1;
-            // ---- phase A: MFMAs on F0 (k-half 0 of step s); F1 = k-half 1 of step s, one
-            // fragment read after every 4th MFMA
-            {
-                auto hook = [&](auto tc) {
-                    constexpr int T = decltype(tc)::value;
-                    if constexpr (T % 4 == 0) {
-                        constexpr int q = T / 4;
-                        if constexpr (q < 8) F1.b[q] = frag_b(cur, q, 1);
-                        else F1.a[q - 8] = frag_a(cur, q - 8, 1);
-                    }
-                };
-                if (ct == 0) mfma_run<0, true>(F0, hook);
-                else mfma_run<0, false>(F0, hook);
-            }
-            // ---- phase B: step s+1 must have landed (staged two phases ago, before any epilogue
-            // stores: vmcnt(63) then covers it), every wave's reads of stage `cur` retired
-            if (prev_epi) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            prev_epi = false;
-            {
-                __amdgpu_buffer_rsrc_t ra, rb;
-                produce_rsrc(ra, rb);
-                char* base = smem + cur * STAGE_BYTES;
-                const int nxt = cur ^ 1;
-                // slots 0..15: the 16 DMA copies of step s+2 into stage `cur`; slots 16..61: the
-                // 16 fragment reads of step s+1's k-half 0, one every 3 MFMAs
-                auto hook = [&](auto tc) {
-                    constexpr int T = decltype(tc)::value;
-                    if constexpr (T < 16) {
-                        if constexpr (T % 2 == 0) sa.piece(ra, base, w, T / 2);
-                        else sb.piece(rb, base + TILE_BYTES, w, T / 2);
-                    } else if constexpr ((T - 16) % 3 == 0 && (T - 16) / 3 < 16) {
-                        constexpr int q = (T - 16) / 3;
-                        if constexpr (q < 8) F0.b[q] = frag_b(nxt, q, 0);
-                        else F0.a[q - 8] = frag_a(nxt, q - 8, 0);
-                    }
-                };
-                mfma_run<0, false>(F1, hook);
-            }
-            produce_advance();
-            ++s;
-        } while (++ct < nk);
-        // ---- epilogue: the last MFMAs' results must be written before the accumulator reads
-        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
-        auto get = [&](auto ic, auto jc) { return aread<8 * decltype(ic)::value + decltype(jc)::value>(); };
-        epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
-        prev_epi = true;
-    }
-    // no LDS-DMA may still be landing when the workgroup's LDS is handed to the next one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-
-// ============================================================================ persistent, 8 waves
-// The 8-wave geometry of gemm_kernel (2 waves per SIMD, 128 x 64 per wave, accumulators in
-// VGPRs) on a persistent grid.  Two waves per SIMD are what hides the LDS-DMA issue cost (60-185
-// cycles per 1-KiB copy): the partner wave's MFMAs keep the matrix pipe busy meanwhile.  With one
-// wave per SIMD (gemm_persistent) the 16 copies per K step stall the pipe and it ran 10-20 % slower.
-// Quarter-step schedule as gemm_kernel's pipeline; the DMA producers run ahead ACROSS items (A two
-// steps ahead, B one), so a tile's first K steps land while the previous tile finishes.
-template <bool TA, bool TB, int EPI, int ABL = 0>
-__global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
-    // ABL (benchmark ablations, wrong results): 1 = no operand staging in the K loop, 2 = no
-    // fragment reads in the K loop, 4 = no waits / barriers in the K loop
-    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w >> 2, wn = w & 3;
-    const int G = gridDim.x;
-    const int lb = xcd_remap(blockIdx.x, G);
-    const int nk = p.k_per_split / BK;
-    const int n_items = p.tiles * p.splits;
-    const int n_mine = lb < n_items ? (n_items - 1 - lb) / G + 1 : 0;
-    const int total = n_mine * nk;
-    if (total == 0) return;
-    auto coords = [&](int i, int& m0, int& n0, int& sp) {
-        const int item = lb + i * G;
-        sp = item / p.tiles;
-        const int tile = item - sp * p.tiles;
-        const int tm = tile / p.tiles_n;
-        m0 = tm * BM;
-        n0 = (tile - tm * p.tiles_n) * BN;
-    };
-    // K-order rotation per XCD group (blockIdx % 8; speed only)
-    const int rot = p.rotate ? ((int)(blockIdx.x & 7) * nk) >> 3 : 0;
-    auto kstep = [&](int t) { return t + rot < nk ? t + rot : t + rot - nk; };
-
-    // ---- producer: the (item, k step) whose operands it loads next (after the last step it repeats
-    // that step; its copies then go to a stage nobody reads any more)
-    int pi = 0, pt = 0, pm0, pn0, psp, pleft = total;
-    coords(0, pm0, pn0, psp);
-    Stager<TA, 8> sa;
-    Stager<TB, 8> sb;
-    sa.init(p.lda, pm0, p.M, w, lane);
-    sb.init(p.ldb, pn0, p.N, w, lane);
-    u32x4_t ra[4], rb[4];  // one K step of this wave's share of the operand tiles, in flight
-    auto produce_load = [&]() {
-        const int k0 = psp * p.k_per_split + kstep(pt) * BK;
-        sa.load_regs(p.A, p.lda, pm0, p.M, k0, ra);
-        sb.load_regs(p.B, p.ldb, pn0, p.N, k0, rb);
-        if (--pleft > 0) {
-            if (++pt == nk) {
-                pt = 0;
-                ++pi;
-                coords(pi, pm0, pn0, psp);
-                sa.init(p.lda, pm0, p.M, w, lane);
-                sb.init(p.ldb, pn0, p.N, w, lane);
-            }
-        } else {
-            pleft = 0;
-        }
-    };
-    auto produce_write = [&](int buf) {
-        char* base = smem + buf * STAGE_BYTES;
-        sa.write_regs(base, w, lane, ra);
-        sb.write_regs(base + TILE_BYTES, w, lane, rb);
-    };
-    auto load_b = [&](bf16x8_t (&f)[4], int buf, int ks) {
-        const char* Bt = smem + buf * STAGE_BYTES + TILE_BYTES;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[j] = frag<TB>(Bt, wn * 64 + 16 * j, ks, lane);
-    };
-    auto load_a = [&](bf16x8_t (&f)[4], int buf, int ks, int half) {
-        const char* At = smem + buf * STAGE_BYTES;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) f[i] = frag<TA>(At, wm * 128 + 64 * half + 16 * i, ks, lane);
-    };
-    f32x4 acc[8][4];
-    auto mma = [&](const bf16x8_t (&fb)[4], const bf16x8_t (&fa)[4], int half) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[4 * half + i][j] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * half + i][j], 0, 0, 0);
-    };
-
-    // prologue: steps 0 and 1 into stages 0 and 1, step 2's operands in flight into registers
-    produce_load();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    produce_write(0);
-    produce_load();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    produce_write(1);
-    produce_load();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    bf16x8_t B0[4], B1[4], Alo[4], Ahi[4];
-    load_b(B0, 0, 0);
-    load_a(Alo, 0, 0, 0);
-    if (ABL & 2) {  // ablation: fragments read once
-        load_b(B1, 0, 1);
-        load_a(Ahi, 0, 1, 1);
-    }
-
-    int s = 0;
-    for (int ci = 0; ci < n_mine; ++ci) {
-        int cm0, cn0, csp;
-        coords(ci, cm0, cn0, csp);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        int ct = 0;
-#pragma clang loop unroll(disable)
-        do {
-            const int cur = s & 1;
-            // Q1
-            if (!(ABL & 2)) load_a(Ahi, cur, 0, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(B0, Alo, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            // Q2
-            if (!(ABL & 2)) {
-                load_b(B1, cur, 1);
-                load_a(Alo, cur, 1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            mma(B0, Ahi, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            // Q3
-            if (!(ABL & 2)) load_a(Ahi, cur, 1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(B1, Alo, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            // Q4: step s+2's operands arrived in registers; this wave's LDS writes (step s+1) and
-            // reads of stage `cur` retired; after the barrier stage `cur` is free and step s+1 visible
-            if (!(ABL & 4)) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();
-            }
-            if (!(ABL & 1)) {
-                produce_write(cur);  // step s+2 -> stage `cur`
-                produce_load();      // step s+3 -> registers (one K step to arrive)
-            }
-            if (!(ABL & 2)) {
-                load_b(B0, cur ^ 1, 0);
-                load_a(Alo, cur ^ 1, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            mma(B1, Ahi, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            ++s;
-        } while (++ct < nk);
-        auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
-        epilogue_store<EPI, 4>(p, get, cm0 + wm * 128, cn0 + wn * 64, csp, lane);
-    }
-}
-
 
 // ============================================================================ ping-pong kernel
 // 256 x 256 x 64 tile, 8 waves as 2 (m) x 4 (n), 128 x 64 per wave (as gemm_kernel), but the two
@@ -945,45 +376,29 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persistent8(GemmParams p) {
 //   RAW: each wave keeps the copies of its last 4 phases in flight (s_waitcnt vmcnt(2 x issued
 //        copies in phases g-3..g) before phase g's first barrier), so a unit issued in phase g is
 //        readable from phase g+5 on — every unit is read >= 5 phases after its issue.
-// Vector-memory operations one wave's epilogue_store<EPI, 4> issues, counted LOW (stores and
-// operand loads only): the persistent form lets that many more ops stay in flight at the waits of
-// the first K step after an epilogue (vmcnt retires in issue order: MI355X_MICROARCH.md, vmcnt),
-// so the next tile's MFMAs start while the stores drain.  Under-counting only waits longer.
-template <int EPI>
-constexpr int pp_epi_vmem() {
-    return EPI == EPI_BF16 || EPI == EPI_F32 ? 32 : EPI == EPI_F32ATOM ? 128 : 64;
-}
 // copies allowed in flight at phase q's wait: 2 per issuing phase among q-3..q (PM / MK: issue
-// masks of the previous / this K step), plus EX, capped at the 6-bit vmcnt field
-constexpr int pp_vm_allow(int PM, int MK, int q, int EX) {
+// masks of the previous / this K step)
+constexpr int pp_vm_allow(int PM, int MK, int q) {
     int n = 0;
     for (int d = 0; d < 4; ++d) {
         const int x = q - d;  // <= 0: phase x + 4 of the previous step
         n += (x >= 1 ? (MK >> (x - 1)) & 1 : (PM >> (x + 3)) & 1) ? 2 : 0;
     }
-    n += EX;
-    return n > 63 ? 63 : n;
+    return n;
 }
 template <int N>
 __device__ __forceinline__ void wait_vmc() {
     asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(N) : "memory");
 }
 
-// PERS: persistent form (NT only): gridDim.x (a multiple of 8) workgroups walk the tiles
-// blockIdx.x, + gridDim.x, ...; the copies of the next tile's first two K steps are issued during
-// the current tile's last two (the K-step sequence runs on across tiles, nk even keeps the LDS
-// buffer parity), so neither the pipeline fill nor the store drain of a tile is exposed.
 // LEPI (EPI_BF16 / EPI_GELU, one tile per workgroup): LDS-staged epilogue — after the K loop each
 // wave writes its 128 x 64 bf16 block into its own 16 KiB of the (then idle) operand LDS (16-B chunks
 // XOR-swizzled by row) and reads it back row-contiguous, so every store instruction writes 8 whole
 // 128-B row segments (1 KiB) instead of 16 rows x 32 B: a quarter of the store instructions and
 // L2 requests of the direct MFMA-layout store.
-template <bool TA, bool TB, int EPI, int ABL = 0, bool PERS = false, bool LEPI = false>
+template <bool TA, bool TB, int EPI, bool LEPI = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
-    static_assert(!LEPI || (!PERS && EPI <= EPI_DGELU), "LDS epilogue: bf16 outputs, one tile");
-    // ABL (timing-only ablations, wrong results): 1 = no copies in the K loop, 2 = no fragment
-    // reads in the K loop, 4 = no waits / barriers in the K loop, 8 = no epilogue stores
-    static_assert(!PERS || (!TA && !TB), "persistent ping-pong: k-contiguous operands only");
+    static_assert(!LEPI || EPI <= EPI_DGELU, "LDS epilogue: bf16 outputs");
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];  // [buf 2][UA0 UA1 UB0 UB1][16 KiB]
     constexpr int UNIT = 16384, BUF = 4 * UNIT;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -995,13 +410,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         mm = tm * BM;
         nn = (wg - tm * p.tiles_n) * BN;
     };
-    int item = blockIdx.x;
-    int m0, n0, m1 = 0, n1 = 0;
-    coords(item, m0, n0);
-    bool has_next = PERS && item + (int)gridDim.x < p.tiles;
-    if (has_next) coords(item + gridDim.x, m1, n1);
+    int m0, n0;
+    coords(blockIdx.x, m0, n0);
     const int kbeg = blockIdx.y * p.k_per_split;
-    const int nk = p.k_per_split / BK;  // >= 2 (host); PERS: even and >= 4
+    const int nk = p.k_per_split / BK;  // >= 2 (host)
 
     // Per-lane byte offsets of piece 0 of each unit (piece 1 adds the uniform di_a / di_b).
     //  k-contiguous operand: unit image [128 unit-rows][64 k], 128-B rows, 16-B chunk c of row r at
@@ -1044,7 +456,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         return make_rsrc(G + (size_t)r0 * ld + k0, rem);
     };
     // unit u (0 UA0, 1 UA1, 2 UB0, 3 UB1) of K step t -> LDS buffer t & 1
-    auto issue_at = [&](int u, int t, int mm, int nn) {
+    auto issue = [&](int u, int t) {
+        const int mm = m0, nn = n0;
         const int k0 = kbeg + t * BK;
         char* dst = smem + (t & 1) * BUF + u * UNIT + w * 1024;
         const bool isA = u < 2;
@@ -1054,10 +467,6 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         asm volatile("" : "+v"(o));
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)dst, 16, o, 0, 0, 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)(dst + 8 * 1024), 16, o + di, 0, 0, 0);
-    };
-    auto issue = [&](int u, int t) {  // K step t of this tile, or t - nk of the next one
-        if (!PERS || t < nk) issue_at(u, t, m0, n0);
-        else issue_at(u, t - nk, m1, n1);
     };
     // MFMA operand fragment (16 unit-rows from rb x 32 k) of a unit: lane l gets unit-row
     // rb + (l & 15), k = 32 ks + 8 (l >> 4) + 0..7
@@ -1109,14 +518,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
                         __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[j][ks], FA[i][ks], acc[4 * mh + i][2 * nh + j], 0, 0, 0);
     };
     // one phase: [reads] [copies] vmcnt(n) barrier lgkmcnt(0) | MFMA cluster | barrier
-    // ex (persistent form, first step after an epilogue): the epilogue's ops may stay in flight
-    auto phase_sync = [&](auto nc, auto nxc, bool ex) {
+    auto phase_sync = [&](auto nc) {
         __builtin_amdgcn_sched_barrier(0);
-        if (!(ABL & 4)) {
-            if (PERS && ex) wait_vmc<decltype(nxc)::value>();
-            else wait_vmc<decltype(nc)::value>();
-            __builtin_amdgcn_s_barrier();
-        }
+        wait_vmc<decltype(nc)::value>();
+        __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
@@ -1124,46 +529,39 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     auto phase_end = [&]() {
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
-        if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     };
     // K step t with this step's / the previous step's issue masks (bit q-1: phase q issues)
-    // ex: the first K step after a persistent epilogue (EX more ops allowed in flight)
-    constexpr int EX = pp_epi_vmem<EPI>();
-    auto step = [&](int t, auto pmc, auto mc, bool ex) {
+    auto step = [&](int t, auto pmc, auto mc) {
         constexpr int PM = decltype(pmc)::value, MK = decltype(mc)::value;
-        using V1 = std::integral_constant<int, pp_vm_allow(PM, MK, 1, 0)>;
-        using V2 = std::integral_constant<int, pp_vm_allow(PM, MK, 2, 0)>;
-        using V3 = std::integral_constant<int, pp_vm_allow(PM, MK, 3, 0)>;
-        using V4 = std::integral_constant<int, pp_vm_allow(PM, MK, 4, 0)>;
-        using X1 = std::integral_constant<int, pp_vm_allow(PM, MK, 1, EX)>;
-        using X2 = std::integral_constant<int, pp_vm_allow(PM, MK, 2, EX)>;
-        using X3 = std::integral_constant<int, pp_vm_allow(PM, MK, 3, EX)>;
-        using X4 = std::integral_constant<int, pp_vm_allow(PM, MK, 4, EX)>;
+        using V1 = std::integral_constant<int, pp_vm_allow(PM, MK, 1)>;
+        using V2 = std::integral_constant<int, pp_vm_allow(PM, MK, 2)>;
+        using V3 = std::integral_constant<int, pp_vm_allow(PM, MK, 3)>;
+        using V4 = std::integral_constant<int, pp_vm_allow(PM, MK, 4)>;
         const int cur = t & 1;
-        constexpr bool RD = !(ABL & 2), CP = !(ABL & 1);
         // P1
-        if (RD) readA(cur, 0);
-        if (RD) readB(FB0, cur, 0);
-        if (CP && (MK & 1)) issue(3, t + 1);
-        phase_sync(V1{}, X1{}, ex);
+        readA(cur, 0);
+        readB(FB0, cur, 0);
+        if (MK & 1) issue(3, t + 1);
+        phase_sync(V1{});
         quad(FB0, 0, 0);
         phase_end();
         // P2
-        if (RD) readB(FB1, cur, 1);
-        if (CP && (MK & 2)) issue(1, t + 1);
-        phase_sync(V2{}, X2{}, ex);
+        readB(FB1, cur, 1);
+        if (MK & 2) issue(1, t + 1);
+        phase_sync(V2{});
         quad(FB1, 0, 1);
         phase_end();
         // P3
-        if (RD) readA(cur, 1);
-        if (CP && (MK & 4)) issue(0, t + 2);
-        phase_sync(V3{}, X3{}, ex);
+        readA(cur, 1);
+        if (MK & 4) issue(0, t + 2);
+        phase_sync(V3{});
         quad(FB1, 1, 1);
         phase_end();
         // P4
-        if (CP && (MK & 8)) issue(2, t + 2);
-        phase_sync(V4{}, X4{}, ex);
+        if (MK & 8) issue(2, t + 2);
+        phase_sync(V4{});
         quad(FB0, 1, 0);
         phase_end();
     };
@@ -1177,37 +575,23 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     issue(2, 1);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // UA0(0), UB0(0) landed
     __builtin_amdgcn_s_barrier();
-    if (wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
-    if (ABL & 2) {
-        readA(0, 0);
-        readB(FB0, 0, 0);
-        readB(FB1, 0, 1);
-    }
+    if (wr) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
     using I15 = std::integral_constant<int, 15>;
     using I3 = std::integral_constant<int, 3>;
     using I0 = std::integral_constant<int, 0>;
     auto epilogue = [&]() {
-        if (ABL & 8) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-        } else {
-            auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
-            GemmParams q = p;
-            if (ABL & 16) q.M = 0;  // ablation: every store falls outside the buffer (issued, dropped)
-            epilogue_store<EPI, 4>(q, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
-        }
+        auto get = [&](auto ic, auto jc) { return acc[decltype(ic)::value][decltype(jc)::value]; };
+        epilogue_store<EPI, 4>(p, get, m0 + wr * 128, n0 + wc * 64, blockIdx.y, lane);
     };
     if constexpr (LEPI) {
         int t = 0;
 #pragma clang loop unroll(disable)
-        for (; t < nk - 2; ++t) step(t, I15{}, I15{}, false);
-        step(t, I15{}, I3{}, false);
-        step(t + 1, I3{}, I0{}, false);
+        for (; t < nk - 2; ++t) step(t, I15{}, I15{});
+        step(t, I15{}, I3{});
+        step(t + 1, I3{}, I0{});
         // group 0's extra barrier first: past it every wave has retired its last fragment reads and
         // waited its last copies (vmcnt(0) in the final phase), so the operand LDS is free
-        if (!wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();
+        if (!wr) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");  // no LDS access of the epilogue moves above that barrier
         __builtin_amdgcn_sched_barrier(0);
         char* ws = smem + w * 16384;
@@ -1323,44 +707,347 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
             pass(false, rc);
         }
         return;
-    } else if constexpr (!PERS) {
-        int t = 0;
-#pragma clang loop unroll(disable)
-        for (; t < nk - 2; ++t) step(t, I15{}, I15{}, false);
-        step(t, I15{}, I3{}, false);      // t = nk-2: P3 / P4 have no step t+2
-        step(t + 1, I3{}, I0{}, false);   // t = nk-1: nothing left to stage
-        epilogue();
     } else {
-        // ONE step instantiation (a loop of several spilled the accumulators): every step stages
-        // (the last tile's last two re-stage its own first steps, never read), and step 0 may leave
-        // the previous epilogue's ops in flight — for the first tile the prologue wait below already
-        // retired everything step 0 reads.
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // UB1(0), UA1(0) landed too
-        if (!has_next) {
-            m1 = m0;
-            n1 = n0;
-        }
         int t = 0;
 #pragma clang loop unroll(disable)
-        while (true) {
-            step(t, I15{}, I15{}, t == 0);
-            if (++t < nk) continue;
-            epilogue();
-            if (!has_next) break;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            item += gridDim.x;
-            m0 = m1;
-            n0 = n1;
-            has_next = item + (int)gridDim.x < p.tiles;
-            if (has_next) coords(item + gridDim.x, m1, n1);
-            t = 0;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unread re-staged copies
+        for (; t < nk - 2; ++t) step(t, I15{}, I15{});
+        step(t, I15{}, I3{});      // t = nk-2: P3 / P4 have no step t+2
+        step(t + 1, I3{}, I0{});   // t = nk-1: nothing left to stage
+        epilogue();
     }
-    if (!wr && !(ABL & 4)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
+    if (!wr) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
+}
+
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+
+// LDS-staged epilogue of one wave's 128 x 128 block with bf16 outputs (EPI_BF16 / GELU / RESADD /
+// DGELU), in two passes of 64 rows through the wave's own 16 KiB of an idle LDS stage: the MFMA-layout
+// accumulators (lane: row l & 15, 4 consecutive columns) go to LDS as 8-byte pieces and come back
+// row-contiguous, so each store instruction writes 4 whole 256-B row segments instead of 16 rows x
+// 32 B (a quarter of the store instructions, full-line writes).  Staging rows are 272 B apart (the
+// 16 rows one 8-byte store instruction touches hit distinct banks) and every address is a per-lane
+// base plus an immediate.
+// Operand tiles of RESADD (C) / DGELU (aux) come in the same way reversed.
+constexpr int P4_EPI_PITCH = 272, P4_EPI_WAVE = 64 * P4_EPI_PITCH;
+template <int EPI>
+__device__ __forceinline__ void p4_lds_epilogue(const GemmParams& p, Acc& acc, char* ws, int mw, int nw, int lane) {
+    const int g = lane >> 4, rl = lane & 15;
+    const long long rem = (long long)(p.M - mw) * p.ldc * 2;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const bf16_t*)p.C + (size_t)mw * p.ldc, rem);
+    const __amdgpu_buffer_rsrc_t rx =
+        EPI == EPI_GELU || EPI == EPI_DGELU ? make_rsrc(p.aux + (size_t)mw * p.ldc, rem) : rc;
+    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
+    // row-contiguous side: lane -> row 4 q + (lane >> 4) of the pass, 16-B chunk lane & 15
+    const int cb = lane & 15;
+    const uint32_t coff = nw + 8 * cb < p.N ? (uint32_t)(nw + 8 * cb) * 2u : 0x80000000u;
+    auto goff = [&](int row) { return coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff; };
+    auto lrow = [&](int row, int ch) { return ws + row * P4_EPI_PITCH + ch * 16; };
+    const __amdgpu_buffer_rsrc_t rsum = make_rsrc(p.colsum, p.colsum != nullptr ? (long long)p.N * 4 : 0);
+#pragma unroll
+    for (int hr = 0; hr < 2; ++hr) {
+        if constexpr (EPI == EPI_RESADD || EPI == EPI_DGELU) {
+            // operand tile rows -> LDS (row-contiguous), then each lane picks its MFMA-layout 8 bytes
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // 8 rows of 16 B per lane in flight at a time
+                uint4 ld[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(EPI == EPI_RESADD ? rc : rx,
+                                                                          goff(64 * hr + 4 * (8 * h + q) + g), 0, 0);
+                    ld[q] = make_uint4(v[0], v[1], v[2], v[3]);
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) *(uint4*)lrow(4 * (8 * h + q) + g, cb) = ld[q];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float bv[4] = {0.f, 0.f, 0.f, 0.f}, csum[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI != EPI_DGELU) {
+                const int n = nw + 16 * j + 4 * g;
+                const u32x2_t b = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
+                unpack4(make_uint2(b.x, b.y), bv);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f32x4 a = acc[8 * (4 * hr + i) + j];
+                const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
+                char* a8 = lrow(row, ch) + ((g & 1) << 3);
+                float v[4];
+                if constexpr (EPI == EPI_RESADD) {
+                    float o[4];
+                    unpack4(*(const uint2*)a8, o);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = a[r] + bv[r] + o[r];
+                } else if constexpr (EPI == EPI_DGELU) {
+                    float u[4];
+                    unpack4(*(const uint2*)a8, u);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        v[r] = a[r] * gelu_tanh_grad(u[r]);
+                        csum[r] += v[r];
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = a[r] + bv[r];
+                }
+                *(uint2*)a8 = pack4(v);
+                __builtin_amdgcn_sched_barrier(0);  // one tile at a time (no hoisted accumulator reads)
+            }
+            if constexpr (EPI == EPI_DGELU) {
+                // this pass's 64-row column sums of column block j: over the 16 lanes of a group,
+                // one atomic per column (rows past M read aux as zero and had zero accumulators)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float t = csum[r];
+                    t += __shfl_xor(t, 1, 64);
+                    t += __shfl_xor(t, 2, 64);
+                    t += __shfl_xor(t, 4, 64);
+                    t += __shfl_xor(t, 8, 64);
+                    csum[r] = t;
+                }
+                const int n = nw + 16 * j + 4 * g, r = lane & 3;
+                const float t = r == 0 ? csum[0] : r == 1 ? csum[1] : r == 2 ? csum[2] : csum[3];
+                const bool writer = p.colsum != nullptr && (lane & 15) < 4 && n + r < p.N;
+                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(t, rsum, writer ? (uint32_t)(n + r) * 4u : 0x80000000u, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint4 v = *(const uint4*)lrow(4 * q + g, cb);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, EPI == EPI_GELU ? rx : rc,
+                                                   goff(64 * hr + 4 * q + g), 0, 0);
+            if (q % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 rows in registers
+        }
+        if constexpr (EPI == EPI_GELU) {  // the stored pre-activation -> gelu -> C
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                uint4 v = *(const uint4*)lrow(4 * q + g, cb);
+                float f[8];
+                unpack8(v, f);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) f[r] = gelu_tanh(f[r]);
+                v = pack8(f);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, rc, goff(64 * hr + 4 * q + g), 0, 0);
+                if (q % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pass hr's reads before pass hr+1 rewrites
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// ============================================================================ persistent 4-wave, register staged
+// hipBLASLt's fastest gfx950 kernels for these products (MT256x256x64, MIWT8_8, WG 256, stream-K
+// persistent grid, register-staged global reads two K steps ahead: their kernel names in
+// profiles/r3_baseline_rocprof_summary.txt) use ONE wave per SIMD owning a 128 x 128 block.  That
+// reads a third less LDS per MFMA than 8 waves of 128 x 64, and the 128 MFMAs of a K step leave
+// 128 issue gaps for the step's 32 fragment reads + 16 global loads + 16 LDS writes.
+// Versus gemm_persistent (same geometry, LDS-DMA staging: 60-185 issue cycles per 1-KiB copy with
+// no partner wave to hide them) the operands come through VGPRs (global_load_dwordx4 -> ds_write_b128).
+//
+// Per K step s (LDS buffer cur = s & 1 holds step s, F0 = its k-half 0 fragments, R = the global
+// data of step s + 1, loaded during step s - 1):
+//   half 0: 64 MFMAs on F0 | read F1 (k-half 1 of cur) ; write R -> buffer cur ^ 1 ; load R <- step s + 2
+//   half 1: [own LDS reads / writes retired] barrier | 64 MFMAs on F1 | read F0 (k-half 0 of cur ^ 1)
+// One barrier per step covers both hazards: after it every wave's writes of step s + 1 are visible,
+// and every wave has finished reading buffer cur ^ 1's previous contents (step s - 1) long before
+// (its last reads were in half 0 of step s - 1, before the previous barrier).
+// The K-step sequence runs on across the tiles of the persistent walk, so the next tile's first
+// steps are loaded while the current tile finishes; only the epilogue stalls the matrix pipe.
+template <bool TA, bool TB, int EPI, bool LEPI = false>
+__global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
+    static_assert(!LEPI || EPI <= EPI_DGELU, "LDS epilogue: bf16 outputs");
+    __shared__ __attribute__((aligned(16))) char smem[LEPI ? LDS_BYTES + 32768 : LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 1, wn = w & 1;
+    const int G = gridDim.x;
+    const int lb = xcd_remap(blockIdx.x, G);
+    const int nk = p.k_per_split / BK;
+    const int n_items = p.tiles * p.splits;
+    const int n_mine = lb < n_items ? (n_items - 1 - lb) / G + 1 : 0;
+    const int total = n_mine * nk;
+    if (total == 0) return;
+    auto coords = [&](int i, int& m0, int& n0, int& sp) {
+        const int item = lb + i * G;
+        sp = item / p.tiles;
+        const int tile = item - sp * p.tiles;
+        const int tm = tile / p.tiles_n;
+        m0 = tm * BM;
+        n0 = (tile - tm * p.tiles_n) * BN;
+    };
+
+    // ---- producer: the (item, k step) it loads next; after the last step it repeats that step
+    // (its data then goes to a buffer nobody reads)
+    int pi = 0, pt = 0, pm0, pn0, psp, pleft = total;
+    coords(0, pm0, pn0, psp);
+    Stager<TA, 4> sa;
+    Stager<TB, 4> sb;
+    sa.init(p.lda, pm0, p.M, w, lane);
+    sb.init(p.ldb, pn0, p.N, w, lane);
+    u32x4_t R[16];  // one K step of this wave's share: pieces 0-7 of A, 8-15 of B
+    __amdgpu_buffer_rsrc_t qa, qb;
+    auto produce_rsrc = [&]() {
+        const int k0 = psp * p.k_per_split + pt * BK;
+        qa = sa.rsrc(p.A, p.lda, pm0, p.M, k0);
+        qb = sb.rsrc(p.B, p.ldb, pn0, p.N, k0);
+    };
+    auto produce_advance = [&]() {
+        if (--pleft > 0) {
+            if (++pt == nk) {
+                pt = 0;
+                ++pi;
+                coords(pi, pm0, pn0, psp);
+                sa.init(p.lda, pm0, p.M, w, lane);
+                sb.init(p.ldb, pn0, p.N, w, lane);
+            }
+        } else {
+            pleft = 0;
+        }
+    };
+    auto load_piece = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        // per-lane base in the VGPR offset, the piece's uniform offset in the SGPR offset: no VALU
+        if constexpr (i < 8) {
+            R[i] = __builtin_amdgcn_raw_buffer_load_b128(qa, sa.base[TA ? (i & 1) : 0], (uint32_t)i * sa.delta, 0);
+        } else {
+            R[i] = __builtin_amdgcn_raw_buffer_load_b128(qb, sb.base[TB ? (i & 1) : 0], (uint32_t)(i - 8) * sb.delta, 0);
+        }
+    };
+    auto write_piece = [&](char* buf, auto ic) {
+        constexpr int i = decltype(ic)::value;
+        char* t = buf + (i < 8 ? 0 : TILE_BYTES);
+        *(u32x4_t*)(t + (w + 4 * (i & 7)) * 1024 + lane * 16) = R[i];
+    };
+    // fragment reads: a per-lane base (lane part + buffer + wave block, one VGPR per operand and
+    // k-half, recomputed per half step) plus the tile's constant offset as the ds_read immediate
+    auto frag_base = [&](bool isB, int buf, int ks) -> uint32_t {
+        uint32_t v;
+        if constexpr (true) {
+            const bool tr = isB ? TB : TA;
+            const int wb = isB ? wn : wm;
+            if (!tr) {
+                v = (uint32_t)((lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ (lane & 7)) << 4) + wb * 128 * 128);
+            } else {
+                v = 0;  // transposed images: frag<> computes the full address
+            }
+            v += (uint32_t)(buf * STAGE_BYTES + (isB ? TILE_BYTES : 0));
+        }
+        asm volatile("" : "+v"(v));
+        return v;
+    };
+    auto frag_at = [&](uint32_t base, bool isB, int t, int buf, int ks) -> bf16x8_t {
+        const bool tr = isB ? TB : TA;
+        if (!tr) return *(const bf16x8_t*)(smem + base + t * 16 * 128);
+        return isB ? frag<TB>(smem + buf * STAGE_BYTES + TILE_BYTES, wn * 128 + 16 * t, ks, lane)
+                   : frag<TA>(smem + buf * STAGE_BYTES, wm * 128 + 16 * t, ks, lane);
+    };
+
+    PFrags F;
+    Acc acc;
+    {   // prologue: step 0 -> LDS buffer 0, step 1 -> R, F = step 0's k-half 0
+        produce_rsrc();
+        static_for<16>(load_piece);
+        produce_advance();
+        static_for<16>([&](auto ic) { write_piece(smem, ic); });
+        produce_rsrc();
+        static_for<16>(load_piece);
+        produce_advance();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t bb = frag_base(true, 0, 0), ba = frag_base(false, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) F.b[0][j] = frag_at(bb, true, j, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) F.a[i] = frag_at(ba, false, i, 0, 0);
+    }
+
+    int s = 0;
+    // one K step; ZERO: the tile's first (accumulators start from C = 0); LAST: the tile's last (the
+    // next step's k-half 0 fragments are read after the epilogue, so they are not live across it)
+    auto read_half0 = [&](int buf) {
+        const uint32_t bb = frag_base(true, buf, 0), ba = frag_base(false, buf, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) F.b[0][j] = frag_at(bb, true, j, buf, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) F.a[i] = frag_at(ba, false, i, buf, 0);
+    };
+    auto kstep = [&](auto zc, auto lc) {
+        constexpr bool ZERO = decltype(zc)::value, LAST = decltype(lc)::value;
+        const int cur = s & 1, nxt = cur ^ 1;
+        char* wbuf = smem + nxt * STAGE_BYTES;
+        produce_rsrc();
+        // ---- half 0 (MFMAs on b[0], a = k-half 0 of step s):
+        //   b[1][j] <- k-half 1 of cur after MFMAs 1, 3, .., 15;  a[i] <- k-half 1 after row i (MFMA 8i + 7);
+        //   R piece i -> LDS buffer nxt after MFMA 17 + 3i, then the next load into R[i] after 18 + 3i
+        {
+            const uint32_t bb = frag_base(true, cur, 1), ba = frag_base(false, cur, 1);
+            auto hook = [&](auto tc) {
+                constexpr int T = decltype(tc)::value;
+                if constexpr (T < 16 && T % 2 == 1) F.b[1][T / 2] = frag_at(bb, true, T / 2, cur, 1);
+                if constexpr (T % 8 == 7) F.a[T / 8] = frag_at(ba, false, T / 8, cur, 1);
+                if constexpr (T >= 17 && (T - 17) % 3 == 0) write_piece(wbuf, std::integral_constant<int, (T - 17) / 3>{});
+                if constexpr (T >= 18 && (T - 18) % 3 == 0) load_piece(std::integral_constant<int, (T - 18) / 3>{});
+            };
+            mfma_run<0, 0, ZERO>(acc, F, hook);
+        }
+        produce_advance();
+        // ---- half 1: every wave's writes of step s + 1 and reads of step s landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            const uint32_t bb = frag_base(true, nxt, 0), ba = frag_base(false, nxt, 0);
+            auto hook = [&](auto tc) {
+                constexpr int T = decltype(tc)::value;
+                if constexpr (!LAST && T < 16 && T % 2 == 1) F.b[0][T / 2] = frag_at(bb, true, T / 2, nxt, 0);
+                if constexpr (!LAST && T % 8 == 7) F.a[T / 8] = frag_at(ba, false, T / 8, nxt, 0);
+            };
+            mfma_run<1, 0, false>(acc, F, hook);
+        }
+        ++s;
+    };
+    for (int ci = 0; ci < n_mine; ++ci) {
+        int cm0, cn0, csp;
+        coords(ci, cm0, cn0, csp);
+        kstep(std::true_type{}, std::false_type{});
+#pragma clang loop unroll(disable)
+        for (int ct = 1; ct < nk - 1; ++ct) kstep(std::false_type{}, std::false_type{});
+        kstep(std::false_type{}, std::true_type{});  // nk >= 2 (host)
+        // ---- epilogue: the last MFMAs' results must be written before the accumulator reads.
+        // Inline-asm MFMAs are opaque to the hazard recognizer, and hipcc copied finished
+        // accumulators to VGPRs right behind their last MFMA (stale values): after the nop sled,
+        // empty asm statements "redefine" every accumulator, so no read can move above them.
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+        acc_fence<0>(acc);
+        acc_fence<16>(acc);
+        acc_fence<32>(acc);
+        acc_fence<48>(acc);
+        __builtin_amdgcn_sched_barrier(0);
+        auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
+        if constexpr (LEPI) {
+            // the stage the last step read is idle until the next step's writes: waves 0-2 stage
+            // through 17 KiB each of it, wave 3 through the spare 32 KiB past the two stages; a
+            // barrier keeps the next step's writes behind every wave's epilogue reads
+            char* ws = w < 3 ? smem + (s & 1 ? 0 : STAGE_BYTES) + w * P4_EPI_WAVE : smem + LDS_BYTES;
+            p4_lds_epilogue<EPI>(p, acc, ws, cm0 + wm * 128, cn0 + wn * 128, lane);
+            __builtin_amdgcn_s_barrier();
+        } else {
+            epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        read_half0(s & 1);  // the next tile's first k-half (step s, staged in buffer s & 1)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace
@@ -1369,12 +1056,8 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
 // Requirements: K % 64 == 0, N % 4 == 0; TA needs M % 8 == 0, TB N % 8 == 0; 16-byte aligned rows
 // (lda/ldb % 8 == 0), ldc % 4 == 0.  split > 1 only with EPI 4 (slab i at C + i * split_stride) or
 // 6 (atomics); the split is reduced until it divides K / 64 (every slice the same depth).
-// epi bits 8..15 select a benchmark variant: 0 (and 10) = the 8-wave kernel with its pipelined
-// schedule (default: the fastest of these on MI355X, profiles/r2_gemm_variants.jsonl), 1 = its plain
-// schedule, 2..9 = its NT bf16 schedule variants, 11 = the persistent 4-wave kernel, 12 = the
-// persistent 8-wave kernel (register-staged producer), 13..18 its timing-only ablations, 19 = 12
-// without the per-XCD K rotation (11..19: NT bf16 only), 20 = the ping-pong kernel (NT, every
-// epilogue), 21..28 its timing-only ablations (NT bf16).
+// `kernel` (epi bits 8..15): 0 = the persistent 4-wave kernel (gemm_p4), 1 = the staggered
+// ping-pong kernel (gemm_pp; LDS-staged row-contiguous epilogue on NT operands with bf16 outputs).
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -1390,74 +1073,75 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
                      hipStream_t s) {
     if (M <= 0 || N <= 0 || K <= 0 || K % BK || N % 4 || lda % 8 || ldb % 8 || ldc % 4) return (int)hipErrorInvalidValue;
     if ((ta && M % 8) || (tb && N % 8)) return (int)hipErrorInvalidValue;
-    int variant = (epi >> 8) & 0xff;
+    int kernel = (epi >> 8) & 0xff;
     epi &= 0xff;
-    if (epi < 0 || epi > 6) return (int)hipErrorInvalidValue;
+    if (epi < 0 || epi > 6 || kernel > 2) return (int)hipErrorInvalidValue;
+    const bool lds_epi = kernel == 2;  // p4 with the LDS-staged epilogue (NT, bf16 outputs)
+    if (kernel == 2) kernel = 0;
+    // the dGELU column sums assume rows past M read as zero, which a transposed A cannot give
+    if (epi == EPI_DGELU && ta) return (int)hipErrorInvalidValue;
     if (split < 1) split = 1;
+    if (split > (K / BK) / 2) split = (K / BK) / 2 > 1 ? (K / BK) / 2 : 1;
     while (split > 1 && (K / BK) % split) --split;
     if (split > 1 && epi != EPI_F32 && epi != EPI_F32ATOM) return (int)hipErrorInvalidValue;
     const int kps = K / split;
     GemmParams p{(const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (bf16_t*)aux, colsum, M, N, K,
-                 lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split, 1};
+                 lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split};
     p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
-    if (variant >= 11 && variant <= 19) {  // benchmark-only persistent kernels (NT, bf16 out)
-        if (ta || tb || epi != 0) return (int)hipErrorInvalidValue;
+#ifdef TDL_GEMM_ISA_ONLY  // inspection builds: one instantiation (scripts/isa_p4.sh)
+#ifndef P4_TA
+#define P4_TA false
+#define P4_TB false
+#define P4_EPI 0
+#endif
+#ifndef P4_LEPI
+#define P4_LEPI false
+#endif
+    gemm_p4<P4_TA, P4_TB, P4_EPI, P4_LEPI><<<256, PNTHR, 0, s>>>(p);
+    TDL_LAUNCH_CHECK();
+#else
+    if (kernel == 0) {
+        if (kps / BK < 2) return (int)hipErrorInvalidValue;  // a tile's first and last K step differ
         const int items = p.tiles * split;
         const int grid = items < num_cus() ? items : num_cus();
-        if (variant == 11) {
-            gemm_persistent<false, false, 0><<<grid, PNTHR, 0, s>>>(p);
-        } else {
-            p.rotate = variant != 19;
-            switch (variant - 12) {
-                case 1: gemm_persistent8<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;  // no staging
-                case 2: gemm_persistent8<false, false, 0, 2><<<grid, NTHR, 0, s>>>(p); break;  // no LDS reads
-                case 4: gemm_persistent8<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;  // no waits
-                case 5: gemm_persistent8<false, false, 0, 5><<<grid, NTHR, 0, s>>>(p); break;
-                case 6: gemm_persistent8<false, false, 0, 7><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only
-                default: gemm_persistent8<false, false, 0, 0><<<grid, NTHR, 0, s>>>(p); break;
+#define P4_EPI(TA_, TB_)                                                 \
+    switch (epi) {                                                       \
+        case 0: gemm_p4<TA_, TB_, 0><<<grid, PNTHR, 0, s>>>(p); break;  \
+        case 1: gemm_p4<TA_, TB_, 1><<<grid, PNTHR, 0, s>>>(p); break;  \
+        case 2: gemm_p4<TA_, TB_, 2><<<grid, PNTHR, 0, s>>>(p); break;  \
+        case 3: gemm_p4<TA_, TB_, 3><<<grid, PNTHR, 0, s>>>(p); break;  \
+        case 4: gemm_p4<TA_, TB_, 4><<<grid, PNTHR, 0, s>>>(p); break;  \
+        case 5: gemm_p4<TA_, TB_, 5><<<grid, PNTHR, 0, s>>>(p); break;  \
+        default: gemm_p4<TA_, TB_, 6><<<grid, PNTHR, 0, s>>>(p); break; \
+    }
+        // the LDS-staged epilogue (NT, bf16 outputs; dGELU keeps the direct stores: its column sums
+        // and pre-activation tile pushed the staged form past the register file)
+        if (lds_epi && !ta && !tb && epi <= EPI_RESADD && p.ldc % 8 == 0) {
+            switch (epi) {
+                case EPI_BF16: gemm_p4<false, false, EPI_BF16, true><<<grid, PNTHR, 0, s>>>(p); break;
+                case EPI_GELU: gemm_p4<false, false, EPI_GELU, true><<<grid, PNTHR, 0, s>>>(p); break;
+                default: gemm_p4<false, false, EPI_RESADD, true><<<grid, PNTHR, 0, s>>>(p); break;
             }
+            TDL_LAUNCH_CHECK();
         }
+        if (!ta && !tb) { P4_EPI(false, false) }
+        else if (!ta && tb) { P4_EPI(false, true) }
+        else if (ta && !tb) { P4_EPI(true, false) }
+        else { P4_EPI(true, true) }
+#undef P4_EPI
         TDL_LAUNCH_CHECK();
     }
+    if (kps / BK < 2) return (int)hipErrorInvalidValue;  // the ping-pong schedule needs two K steps
     const dim3 grid(p.tiles, split);
-    if (variant >= 21 && variant <= 28 && !ta && !tb && epi == 0 && kps / BK >= 2) {  // pp ablations
-        switch (variant) {
-            case 21: gemm_pp<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;   // no copies
-            case 22: gemm_pp<false, false, 0, 2><<<grid, NTHR, 0, s>>>(p); break;   // no frag reads
-            case 23: gemm_pp<false, false, 0, 3><<<grid, NTHR, 0, s>>>(p); break;   // MFMA + sync
-            case 24: gemm_pp<false, false, 0, 7><<<grid, NTHR, 0, s>>>(p); break;   // MFMA only
-            case 25: gemm_pp<false, false, 0, 8><<<grid, NTHR, 0, s>>>(p); break;   // no epilogue
-            case 26: gemm_pp<false, false, 0, 15><<<grid, NTHR, 0, s>>>(p); break;  // MFMA only, no epilogue
-            case 28: gemm_pp<false, false, 0, 16><<<grid, NTHR, 0, s>>>(p); break;  // stores dropped
-            default: gemm_pp<false, false, 0, 4><<<grid, NTHR, 0, s>>>(p); break;   // no sync
-        }
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant == 36 && !ta && !tb && epi <= EPI_DGELU && split == 1 && kps / BK >= 2 && p.ldc % 8 == 0) {
+    if (!ta && !tb && epi <= EPI_DGELU && split == 1 && p.ldc % 8 == 0) {
         switch (epi) {
-            case EPI_BF16: gemm_pp<false, false, EPI_BF16, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
-            case EPI_GELU: gemm_pp<false, false, EPI_GELU, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
-            case EPI_RESADD: gemm_pp<false, false, EPI_RESADD, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
-            default: gemm_pp<false, false, EPI_DGELU, 0, false, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_BF16: gemm_pp<false, false, EPI_BF16, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_GELU: gemm_pp<false, false, EPI_GELU, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_RESADD: gemm_pp<false, false, EPI_RESADD, true><<<grid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, EPI_DGELU, true><<<grid, NTHR, 0, s>>>(p); break;
         }
         TDL_LAUNCH_CHECK();
     }
-    if (variant == 36) variant = 20;  // other epilogues / layouts: the direct-store ping-pong
-    if (variant == 35 && !ta && !tb && kps / BK >= 4 && (kps / BK) % 2 == 0) {  // persistent ping-pong
-        const int g8 = num_cus() & ~7;
-        const dim3 pgrid(p.tiles < g8 ? p.tiles : g8, split);
-        switch (epi) {
-            case 0: gemm_pp<false, false, 0, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            case 1: gemm_pp<false, false, 1, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            case 2: gemm_pp<false, false, 2, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            case 3: gemm_pp<false, false, 3, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            case 4: gemm_pp<false, false, 4, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            case 5: gemm_pp<false, false, 5, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-            default: gemm_pp<false, false, 6, 0, true><<<pgrid, NTHR, 0, s>>>(p); break;
-        }
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant == 20 && kps / BK >= 2) {  // ping-pong kernel
 #define PP_LAUNCH(TA_, TB_, E_) gemm_pp<TA_, TB_, E_><<<grid, NTHR, 0, s>>>(p)
 #define PP_EPI(TA_, TB_)                       \
     switch (epi) {                             \
@@ -1469,52 +1153,12 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         case 5: PP_LAUNCH(TA_, TB_, 5); break; \
         default: PP_LAUNCH(TA_, TB_, 6); break; \
     }
-        if (!ta && !tb) { PP_EPI(false, false) }
-        else if (!ta && tb) { PP_EPI(false, true) }
-        else if (ta && !tb) { PP_EPI(true, false) }
-        else { PP_EPI(true, true) }
+    if (!ta && !tb) { PP_EPI(false, false) }
+    else if (!ta && tb) { PP_EPI(false, true) }
+    else if (ta && !tb) { PP_EPI(true, false) }
+    else { PP_EPI(true, true) }
 #undef PP_EPI
 #undef PP_LAUNCH
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant >= 2 && variant <= 9) {  // schedule variants of the 8-wave kernel (NT, bf16 out only)
-        if (ta || tb || epi != 0) return (int)hipErrorInvalidValue;
-        switch (variant) {
-            case 2: gemm_kernel<false, false, 0, 1><<<grid, NTHR, 0, s>>>(p); break;            // base pipeline
-            case 3: gemm_kernel<false, false, 0, 1 | 32><<<grid, NTHR, 0, s>>>(p); break;       // interleave
-            case 4: gemm_kernel<false, false, 0, 1 | 2><<<grid, NTHR, 0, s>>>(p); break;        // B early
-            case 5: gemm_kernel<false, false, 0, 1 | 2 | 32><<<grid, NTHR, 0, s>>>(p); break;
-            case 6: gemm_kernel<false, false, 0, 1 | 4><<<grid, NTHR, 0, s>>>(p); break;        // ablation: no vmcnt
-            case 7: gemm_kernel<false, false, 0, 1 | 4 | 8><<<grid, NTHR, 0, s>>>(p); break;    // ablation: no vm/barrier
-            case 8: gemm_kernel<false, false, 0, 1 | 16><<<grid, NTHR, 0, s>>>(p); break;       // setprio
-            default: gemm_kernel<false, false, 0, 1 | 16 | 32><<<grid, NTHR, 0, s>>>(p); break;
-        }
-        TDL_LAUNCH_CHECK();
-    }
-    if (variant == 1) {  // plain (unpipelined) schedule, benchmark reference
-        if (epi != 0) return (int)hipErrorInvalidValue;
-        if (!ta && !tb) gemm_kernel<false, false, 0, 0><<<grid, NTHR, 0, s>>>(p);
-        else if (!ta && tb) gemm_kernel<false, true, 0, 0><<<grid, NTHR, 0, s>>>(p);
-        else if (ta && !tb) gemm_kernel<true, false, 0, 0><<<grid, NTHR, 0, s>>>(p);
-        else gemm_kernel<true, true, 0, 0><<<grid, NTHR, 0, s>>>(p);
-        TDL_LAUNCH_CHECK();
-    }
-#define G_LAUNCH(TA_, TB_, E_) gemm_kernel<TA_, TB_, E_, 1><<<grid, NTHR, 0, s>>>(p)
-#define G_EPI(TA_, TB_)                                  \
-    switch (epi) {                                       \
-        case 0: G_LAUNCH(TA_, TB_, 0); break;            \
-        case 1: G_LAUNCH(TA_, TB_, 1); break;            \
-        case 2: G_LAUNCH(TA_, TB_, 2); break;            \
-        case 3: G_LAUNCH(TA_, TB_, 3); break;            \
-        case 4: G_LAUNCH(TA_, TB_, 4); break;            \
-        case 5: G_LAUNCH(TA_, TB_, 5); break;            \
-        default: G_LAUNCH(TA_, TB_, 6); break;           \
-    }
-    if (!ta && !tb) { G_EPI(false, false) }
-    else if (!ta && tb) { G_EPI(false, true) }
-    else if (ta && !tb) { G_EPI(true, false) }
-    else { G_EPI(true, true) }
-#undef G_EPI
-#undef G_LAUNCH
     TDL_LAUNCH_CHECK();
+#endif
 }

@@ -1,13 +1,18 @@
-"""Native MFMA GEMM (csrc/gemm.hip) vs a plain PyTorch fp32 reference of the same op (GPU only).
+"""Native MFMA GEMMs (csrc/gemm.hip: p4 = persistent 4-wave kernel, p4l = the same with the
+LDS-staged epilogue, pp = staggered 8-wave ping-pong kernel) vs a plain PyTorch fp32 reference of
+the same op (GPU only).
 
 Covers the four operand storage forms (k-contiguous / row-contiguous for A and B), every fused
-epilogue, ragged M and N (tile clamping + store masks), split-K slabs and atomics."""
+epilogue, ragged M and N (tile clamping + store masks), split-K slabs and atomics, and every
+product the engine routes to a native kernel at its production GPT-2-medium shape (64k tokens,
+K up to 4096)."""
 import pytest
 import torch
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+KERNELS = ["p4", "p4l", "pp"]
 
 
 def _rel(a, b):
@@ -31,98 +36,71 @@ def _view(t_logical, transposed):
     return t_logical.t().contiguous().t() if transposed else t_logical.contiguous()
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (768, 1024, 320), (520, 264, 64)])
-def test_layouts(ta, tb, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (776, 1032, 320), (8200, 520, 512)])
+def test_layouts(kernel, ta, tb, M, N, K):
+    """all four storage forms, ragged M / N, > 1 tile per persistent workgroup (8200 rows), plus an
+    fp32 split-K accumulation through slabs"""
     from trustworthy_dl.ops import gemm
     a = _view(_rand(M, K), ta)
     b = _view(_rand(K, N, scale=0.1), tb)
-    out = gemm.matmul(a, b)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    gemm._launch(a, b, out, N, "none", kernel=kernel)
     ref = a.float() @ b.float()
-    assert _rel(out, ref) < 1e-2, (ta, tb, M, N, K)
+    assert _rel(out, ref) < 1e-2, (kernel, ta, tb, M, N, K)
+    acc = torch.ones(M, N, device=DEV)
+    gemm.matmul_f32_acc(acc, a, b, split=2, mode="slab", kernel=kernel)
+    assert _rel(acc, ref + 1.0) < 1e-4
 
 
-def test_bias_gelu_resadd_dgelu():
-    from trustworthy_dl.ops import gemm
-    M, N, K = 1000, 512, 256          # ragged M (1000 = 3 x 256 + 232)
-    x = _rand(M, K)
-    w = _rand(K, N, scale=0.1)
-    bias = _rand(N, scale=0.5)
-    ref_pre = x.float() @ w.float() + bias.float()
-    # bias only
-    y = gemm.matmul(x, w, bias=bias)
-    assert _rel(y, ref_pre) < 1e-2
-    # bias + gelu (pre-activation stored too)
-    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    f = gemm.matmul(x, w, bias=bias, epi="gelu", aux=pre)
-    assert _rel(pre, ref_pre) < 1e-2
-    assert _rel(f, F.gelu(ref_pre, approximate="tanh")) < 1e-2
-    # residual accumulate: out += x @ w
-    res = _rand(M, N)
-    out = res.clone()
-    gemm.matmul(x, w, out=out, epi="resadd")
-    assert _rel(out, res.float() + x.float() @ w.float()) < 1e-2
-    # dgelu + bias-gradient column sums: d = (dy @ w2^T) * gelu'(pre)
-    dy = _rand(M, K)
-    w2 = _rand(N, K, scale=0.1)        # logical b = w2^T [K, N] from a [N, K] tensor
-    colsum = torch.zeros(N, device=DEV)
-    d = gemm.matmul(dy, w2.t(), epi="dgelu", aux=pre, colsum=colsum)
-    u = pre.float().requires_grad_(True)
-    (gr,) = torch.autograd.grad(F.gelu(u, approximate="tanh"), u, dy.float() @ w2.float().t())
-    assert _rel(d, gr) < 2e-2
-    assert _rel(colsum, gr.sum(0)) < 2e-2
-
-
-@pytest.mark.parametrize("ta", [False, True])
-@pytest.mark.parametrize("tb", [False, True])
-@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (776, 1032, 320)])
-def test_pingpong_variant_layouts(ta, tb, M, N, K):
-    """variant 20 on all four operand storage forms (transposed units read with ds_read_b64_tr_b16),
-    ragged M / N, plus an fp32 split-K weight-gradient accumulation (TA = TB = 1, slabs)."""
-    from trustworthy_dl.ops import gemm
-    a = _view(_rand(M, K), ta)
-    b = _view(_rand(K, N, scale=0.1), tb)
-    old = gemm.VARIANT
-    gemm.VARIANT = 20
-    try:
-        out = gemm.matmul(a, b)
-        assert _rel(out, a.float() @ b.float()) < 1e-2, (ta, tb, M, N, K)
-        if ta and tb:
-            acc = torch.ones(M, N, device=DEV)
-            gemm.matmul_f32_acc(acc, a, b, split=2, mode="slab")
-            assert _rel(acc, a.float() @ b.float() + 1.0) < 1e-4
-    finally:
-        gemm.VARIANT = old
-
-
-@pytest.mark.parametrize("M,N,K", [(1000, 200, 128), (520, 1032, 1024), (4096, 512, 192)])
-def test_pingpong_variant_epilogues(M, N, K):
-    """tdl_gemm variant 20 (staggered two-group ping-pong schedule, NT operands) against fp32 torch,
-    ragged M / N, the shortest K it takes (two K steps) and every epilogue it shares."""
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("M,N,K", [(1000, 200, 128), (8200, 1032, 256), (4096, 2048, 1024)])
+def test_epilogues(kernel, M, N, K):
+    """every epilogue the GPT-2 block uses (bias, bias+GELU with the pre-activation, residual add,
+    dGELU with bias-gradient column sums, fp32 accumulate / slabs / atomics), NT operands, ragged"""
     from trustworthy_dl.ops import gemm
     x = _rand(M, K)
     wt = _rand(N, K, scale=0.1)        # [N, K] storage: NT (forward with the W^T copy / dgrad)
     bias = _rand(N, scale=0.5)
     ref = x.float() @ wt.float().t()
-    old = gemm.VARIANT
-    gemm.VARIANT = 20
-    try:
-        y = gemm.matmul(x, wt.t(), bias=bias)
-        assert _rel(y, ref + bias.float()) < 1e-2
-        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        f = gemm.matmul(x, wt.t(), bias=bias, epi="gelu", aux=pre)
-        assert _rel(pre, ref + bias.float()) < 1e-2
-        assert _rel(f, F.gelu(ref + bias.float(), approximate="tanh")) < 1e-2
-        res = _rand(M, N)
-        out = res.clone()
-        gemm.matmul(x, wt.t(), out=out, epi="resadd")
-        assert _rel(out, res.float() + ref) < 1e-2
+
+    def mm(out, epi, **kw):
+        gemm._launch(x, wt.t(), out, N, epi, kernel=kernel, **kw)
+        return out
+    y = mm(torch.empty(M, N, dtype=torch.bfloat16, device=DEV), "none", bias=bias)
+    assert _rel(y, ref + bias.float()) < 1e-2
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    f = mm(torch.empty(M, N, dtype=torch.bfloat16, device=DEV), "gelu", bias=bias, aux=pre)
+    assert _rel(pre, ref + bias.float()) < 1e-2
+    assert _rel(f, F.gelu(ref + bias.float(), approximate="tanh")) < 1e-2
+    res = _rand(M, N)
+    out = mm(res.clone(), "resadd")
+    assert _rel(out, res.float() + ref) < 1e-2
+    colsum = torch.zeros(N, device=DEV)
+    dy = _rand(M, K)
+    d = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    gemm._launch(dy, wt.t(), d, N, "dgelu", aux=pre, colsum=colsum, kernel=kernel)
+    u = pre.float().requires_grad_(True)
+    (gr,) = torch.autograd.grad(F.gelu(u, approximate="tanh"), u, dy.float() @ wt.float().t())
+    assert _rel(d, gr) < 2e-2
+    assert _rel(colsum, gr.sum(0)) < 2e-2
+    acc = mm(torch.ones(M, N, device=DEV), "f32acc")
+    assert _rel(acc, ref + 1.0) < 1e-4
+    for mode in ("slab", "atomic"):
         acc = torch.ones(M, N, device=DEV)
-        gemm._launch(x, wt.t(), acc, N, "f32acc")
-        assert _rel(acc, ref + 1.0) < 1e-4
-    finally:
-        gemm.VARIANT = old
+        gemm.matmul_f32_acc(acc, x, wt.t(), split=2, mode=mode, kernel=kernel)
+        assert _rel(acc, ref + 1.0) < 1e-4, mode
+
+
+def test_dgelu_rejects_transposed_a():
+    """the dGELU column sums need rows past M to read as zero, which a transposed A cannot give"""
+    from trustworthy_dl.ops import gemm
+    a = _view(_rand(264, 128), True)
+    with pytest.raises(ValueError):
+        gemm.matmul(a, _rand(128, 256), epi="dgelu", aux=torch.empty(264, 256, dtype=torch.bfloat16, device=DEV),
+                    colsum=torch.zeros(256, device=DEV))
 
 
 @pytest.mark.parametrize("mode,split", [("slab", None), ("atomic", 4), ("slab", 1), ("slab", 3)])
@@ -138,51 +116,56 @@ def test_wgrad_f32(mode, split):
     assert _rel(acc - base, ref - base) < 2e-3
 
 
-def test_production_shape_fwd_dgrad():
-    from trustworthy_dl.ops import gemm
-    M, K, N = 8192, 1024, 3072
-    x = _rand(M, K)
-    w = _rand(K, N, scale=0.05)
-    assert _rel(gemm.matmul(x, w), x.float() @ w.float()) < 1e-2
-    dy = _rand(M, N)
-    assert _rel(gemm.matmul(dy, w.t()), dy.float() @ w.float().t()) < 1e-2
+# every product the engine routes to a native kernel, at the production shape (64k tokens)
+@pytest.mark.parametrize("name,tokens,cin,cout", [("qkv", 65536, 1024, 3072), ("o", 65536, 1024, 1024),
+                                                  ("fc", 65536, 1024, 4096), ("proj", 65536, 4096, 1024)])
+def test_production_wgrad(name, tokens, cin, cout):
+    """dW += x^T dy (fp32 main_grad) for the four projections of a GPT-2-medium block"""
+    from trustworthy_dl.ops.layers import wgrad_acc
+    x = _rand(tokens, cin)
+    dy = _rand(tokens, cout, scale=0.1)
+    acc = torch.randn(cin, cout, device=DEV)
+    ref = acc + x.float().t() @ dy.float()
+    wgrad_acc(acc, x.t(), dy)
+    assert float((acc - ref).norm() / ref.norm()) < 1e-4, name
 
 
-@pytest.mark.parametrize("variant", [35, 36])
-@pytest.mark.parametrize("M,N,K", [(8200, 8200, 256), (33000, 1032, 512), (4096, 2048, 1024)])
-def test_persistent_pingpong_epilogues(M, N, K, variant):
-    """tdl_gemm variant 35 (persistent ping-pong: > 1 tile per workgroup, the next tile's first K
-    steps staged during the current tile's last, stores drained behind the next tile's MFMAs) and
-    36 (LDS-staged row-contiguous epilogues: stores, and the residual / pre-activation loads) against fp32 torch on ragged M / N,
-    every epilogue the GPT-2 block uses (bias, bias+GELU with the pre-activation, residual add,
-    dGELU with bias-gradient column sums, fp32 accumulate)."""
+def test_production_lm_head_wgrad():
+    """tied LM head dW += dlogits^T x at V = 50304 (padded), 16k tokens, K = tokens"""
+    from trustworthy_dl.ops.layers import wgrad_acc
+    dl = _rand(16384, 50304, scale=0.01)
+    x = _rand(16384, 1024)
+    acc = torch.zeros(50304, 1024, device=DEV)
+    wgrad_acc(acc, dl.t(), x)
+    ref = dl.float().t() @ x.float()
+    assert float((acc - ref).norm() / ref.norm()) < 1e-4
+
+
+def test_production_fused_mlp():
+    """the MLP GEMMs the block fuses on the ping-pong kernel: fc forward (bias + GELU, pre-activation
+    stored, K = 1024) and proj dgrad (dGELU + bias-gradient column sums, K = 1024), and the
+    K = 4096 proj forward with the residual-add epilogue, at 64k tokens"""
     from trustworthy_dl.ops import gemm
-    x = _rand(M, K)
-    wt = _rand(N, K, scale=0.1)
-    bias = _rand(N, scale=0.5)
-    ref = x.float() @ wt.float().t()
-    old = gemm.VARIANT
-    gemm.VARIANT = variant
-    try:
-        y = gemm.matmul(x, wt.t(), bias=bias)
-        assert _rel(y, ref + bias.float()) < 1e-2
-        pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        f = gemm.matmul(x, wt.t(), bias=bias, epi="gelu", aux=pre)
-        assert _rel(pre, ref + bias.float()) < 1e-2
-        assert _rel(f, F.gelu(ref + bias.float(), approximate="tanh")) < 1e-2
-        res = _rand(M, N)
-        out = res.clone()
-        gemm.matmul(x, wt.t(), out=out, epi="resadd")
-        assert _rel(out, res.float() + ref) < 1e-2
-        colsum = torch.zeros(N, device=DEV)
-        dy = _rand(M, K)
-        d = gemm.matmul(dy, wt.t(), epi="dgelu", aux=pre, colsum=colsum)
-        u = pre.float().requires_grad_(True)
-        (gr,) = torch.autograd.grad(F.gelu(u, approximate="tanh"), u, dy.float() @ wt.float().t())
-        assert _rel(d, gr) < 2e-2
-        assert _rel(colsum, gr.sum(0)) < 2e-2
-        acc = torch.ones(M, N, device=DEV)
-        gemm._launch(x, wt.t(), acc, N, "f32acc")
-        assert _rel(acc, ref + 1.0) < 1e-4
-    finally:
-        gemm.VARIANT = old
+    M = 65536
+    h = _rand(M, 1024)
+    wfc_t = _rand(4096, 1024, scale=0.05)
+    bfc = _rand(4096, scale=0.5)
+    pre = torch.empty(M, 4096, dtype=torch.bfloat16, device=DEV)
+    f = gemm.matmul(h, wfc_t.t(), bias=bfc, epi="gelu", aux=pre)
+    ref = h.float() @ wfc_t.float().t() + bfc.float()
+    assert _rel(pre, ref) < 1e-2
+    assert _rel(f, F.gelu(ref, approximate="tanh")) < 1e-2
+    del ref
+    dy = _rand(M, 1024)
+    wp = _rand(4096, 1024, scale=0.05)                 # W_proj [in 4096, out 1024]
+    colsum = torch.zeros(4096, device=DEV)
+    d = gemm.matmul(dy, wp.t(), epi="dgelu", aux=pre, colsum=colsum)
+    u = pre.float().requires_grad_(True)
+    (gr,) = torch.autograd.grad(F.gelu(u, approximate="tanh"), u, dy.float() @ wp.float().t())
+    assert _rel(d, gr) < 2e-2
+    assert _rel(colsum, gr.sum(0)) < 2e-2
+    del u, gr
+    y = _rand(M, 1024)
+    y0 = y.float()
+    gemm.matmul(f, wp, out=y, epi="resadd")
+    assert _rel(y, y0 + f.float() @ wp.float()) < 1e-2

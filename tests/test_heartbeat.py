@@ -80,3 +80,30 @@ def test_offline_agreed_by_all_ranks_and_recovers():
     assert res[0]["status"][-1] in ("recovering", "trusted", "suspicious")
     kinds = [e["event"] for e in res[0]["events"] if e["node_id"] == 0]
     assert kinds[:2] == ["offline", "online"]
+
+
+class _DeadStore:
+    def add(self, key, v):
+        raise RuntimeError("Connection reset by peer (store host gone)")
+
+
+def test_store_host_loss_marks_rank0_offline():
+    """rank 0 hosts the TCPStore: when it dies every survivor's beat/poll fails.  Consecutive store
+    failures for longer than the timeout declare the store host OFFLINE (survivors used to
+    swallow the errors and never report anyone)."""
+    from trustworthy_dl.runtime.heartbeat import HeartbeatMonitor
+    m = HeartbeatMonitor(_DeadStore(), rank=2, world=3, interval=0.01, timeout=0.5)
+    seen = []
+    m.on_offline = seen.append
+    m.store_failed(RuntimeError("x"), now=10.0)   # starts the clock
+    m.store_failed(RuntimeError("x"), now=10.3)
+    assert m.offline() == set()
+    m.store_failed(RuntimeError("x"), now=10.6)
+    assert m.offline() == {0} and seen == [0]
+    m.store_failed(RuntimeError("x"), now=11.0)   # reported once
+    assert seen == [0]
+    # the store host itself never declares itself offline
+    h = HeartbeatMonitor(_DeadStore(), rank=0, world=3, timeout=0.1)
+    h.store_failed(RuntimeError("x"), now=0.0)
+    h.store_failed(RuntimeError("x"), now=5.0)
+    assert h.offline() == set()

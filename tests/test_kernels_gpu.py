@@ -463,15 +463,23 @@ def test_fused_gpt2_block_matches_fp32(native_gemm, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,K,N", [(32768, 1024, 1024), (16384, 1024, 3072), (8192, 1024, 1024)])
-def test_wgrad_splitk_accumulates(M, K, N):
-    from trustworthy_dl.ops.layers import wgrad_acc, wgrad_split
+@pytest.mark.parametrize("M,K,N", [(65536, 1024, 3072), (65536, 1024, 1024), (65536, 1024, 4096),
+                                   (65536, 4096, 1024), (8192, 1024, 1024), (4096, 1000, 264)])
+def test_wgrad_native_accumulates(M, K, N):
+    """Weight-gradient products (x^T dy into an fp32 main_grad) on the native persistent kernel at
+    the GPT-2-medium production shapes (64k tokens: qkv / out-proj / fc / proj), a short token count
+    and a ragged width, against fp32 torch."""
+    from trustworthy_dl.ops import gemm
+    from trustworthy_dl.ops.layers import wgrad_acc
     torch.manual_seed(0)
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     acc = torch.randn(K, N, device="cuda")
     ref = acc + x.float().t() @ dy.float()
-    assert wgrad_split(M, K, N) > 1
+    if K % 8 == 0 and N % 8 == 0:
+        assert gemm.supported(x.t(), dy)
+    if M == 65536:
+        assert gemm.wgrad_split(M, K, N) > 1
     wgrad_acc(acc, x.t(), dy)
     assert float((acc - ref).norm() / ref.norm()) < 1e-3
 

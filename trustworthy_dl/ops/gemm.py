@@ -25,12 +25,12 @@ from ._lib import ptr, stream_ptr
 
 EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f32atomic": 6}
 BK = 64
-# Kernel selection (TDL_GEMM_VARIANT): 36 (default) = the staggered ping-pong kernel with the
-# LDS-staged row-contiguous epilogues on NT operands (bias / GELU / residual add / dGELU; the other
-# layouts and fp32 outputs take the ping-pong kernel's direct stores, 20), 0 = the 8-wave pipelined
-# kernel, 1 = its plain schedule, 2..19 / 21..35 = schedule variants, persistent forms and
-# timing-only ablations (csrc/gemm.hip tdl_gemm; profiles/r2_gemm_*.jsonl)
-VARIANT = int(os.environ.get("TDL_GEMM_VARIANT", "36"))
+# Kernel (csrc/gemm.hip): "p4" = the persistent 4-wave kernel (one wave per SIMD owning 128 x 128,
+# register-staged operands), "pp" = the staggered 8-wave ping-pong kernel (LDS-DMA staging,
+# LDS-staged row-contiguous epilogue on NT operands).
+KERNELS = {"p4": 0, "pp": 1, "p4l": 2}
+KERNEL = os.environ.get("TDL_GEMM_KERNEL", "pp")        # bf16-output products (matmul)
+WGRAD_KERNEL = os.environ.get("TDL_WGRAD_KERNEL", "p4")  # fp32 weight-gradient products
 
 
 def _operand_a(a: torch.Tensor):
@@ -57,7 +57,7 @@ def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
         return False
     M, K = a.shape
     N = b.shape[1]
-    if K % BK or N % 8 or M % 8 or b.shape[0] != K:
+    if K % BK or K < 2 * BK or N % 8 or M % 8 or b.shape[0] != K:
         return False
     try:
         ta, lda = _operand_a(a)
@@ -67,13 +67,14 @@ def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
     return lda % 8 == 0 and ldb % 8 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
 
 
-def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_stride=0):
+def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_stride=0, kernel=None):
     M, K = a.shape
     N = b.shape[1]
     ta, lda = _operand_a(a)
     tb, ldb = _operand_b(b)
+    kid = KERNELS[kernel or KERNEL]
     _lib.call("tdl_gemm", ptr(a), ptr(b), ptr(c), ptr(bias), ptr(aux), ptr(colsum), M, N, K, lda, ldb, ldc,
-              ta, tb, EPI[epi] | (VARIANT << 8), int(split), int(split_stride), stream_ptr(a.device))
+              ta, tb, EPI[epi] | (kid << 8), int(split), int(split_stride), stream_ptr(a.device))
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
@@ -91,53 +92,71 @@ def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None
         raise ValueError("out must be row-major")
     if epi in ("gelu", "dgelu") and (aux is None or aux.stride() != out.stride()):
         raise ValueError(f"{epi} needs aux with the output's layout")
+    if epi == "dgelu" and _operand_a(a)[0]:
+        raise ValueError("dgelu needs a row-major A (rows past M must read as zero for the column sums)")
     _launch(a, b, out, out.stride(0), epi, bias=bias, aux=aux, colsum=colsum)
     return out
 
 
-def wgrad_split(M: int, K: int, N: int, num_cu: int = 256) -> int:
-    """Split of the token reduction for an fp32 weight-gradient product [K, M] @ [M, N]: enough
-    256x256 tiles x splits to fill the CUs once, each split at least 16 K steps deep."""
+def num_cus(device=None) -> int:
+    try:
+        return torch.cuda.get_device_properties(device or torch.cuda.current_device()).multi_processor_count
+    except (RuntimeError, AssertionError):
+        return 256
+
+
+def wgrad_split(K: int, M: int, N: int, num_cu: Optional[int] = None) -> int:
+    """Split of the reduction depth K of an fp32 product [M, K] @ [K, N] (a weight gradient: K =
+    tokens) for the persistent kernel: the (tiles x slices) work items should fill the CUs in whole
+    rounds (the slices of a round finish together), each slice at least 16 K steps deep; among
+    equally full choices the smallest split (least slab traffic).  At 64k tokens on 256 CUs:
+    qkv 16, out-proj 16, fc / proj 4, tied LM head 8 (profiles/r3_gemm_lab.jsonl)."""
     if os.environ.get("TDL_WGRAD_SPLITK", "1") == "0":
         return 1
-    tiles = ((K + 255) // 256) * ((N + 255) // 256)
-    s = max(1, num_cu // tiles)
-    s = min(s, max(1, M // (16 * BK)))
-    return s
+    cu = num_cu or num_cus()
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    best, best_eff = 1, -1.0
+    for s in (1, 2, 4, 8, 16):
+        if s > 1 and (K // s < 16 * BK or effective_split(K, s) != s):
+            continue
+        items = tiles * s
+        eff = items / (-(-items // cu) * cu)
+        if eff > best_eff + 1e-3:
+            best, best_eff = s, eff
+    return best
 
 
 def matmul_f32_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, split: Optional[int] = None,
-                   mode: Optional[str] = None) -> torch.Tensor:
+                   mode: Optional[str] = None, kernel: Optional[str] = None) -> torch.Tensor:
     """``acc (fp32) += a @ b``.  With a split reduction the partial products go to fp32 slabs
-    reduced by one native pass (``mode='slab'``) or straight into ``acc`` with fp32 atomics
-    (``mode='atomic'``)."""
+    reduced by one native pass (``mode='slab'``, default) or straight into ``acc`` with fp32
+    atomics (``mode='atomic'``)."""
     M, K = a.shape
     N = b.shape[1]
     if acc.dtype != torch.float32 or tuple(acc.shape) != (M, N) or not acc.is_contiguous():
         raise ValueError("acc must be a contiguous fp32 [M, N] buffer")
+    kernel = kernel or WGRAD_KERNEL
     S = wgrad_split(K, M, N) if split is None else max(1, int(split))
-    if S <= 1:
-        _launch(a, b, acc, N, "f32acc")
-        return acc
-    mode = mode or os.environ.get("TDL_WGRAD_REDUCE", "slab")
     S = effective_split(K, S)
+    mode = mode or os.environ.get("TDL_WGRAD_REDUCE", "slab")
     if S <= 1:
-        _launch(a, b, acc, N, "f32acc")
+        _launch(a, b, acc, N, "f32acc", kernel=kernel)
         return acc
     if mode == "atomic":
-        _launch(a, b, acc, N, "f32atomic", split=S)
+        _launch(a, b, acc, N, "f32atomic", split=S, kernel=kernel)
         return acc
     slabs = torch.empty(S, M, N, dtype=torch.float32, device=acc.device)
-    _launch(a, b, slabs, N, "f32", split=S, split_stride=M * N)
+    _launch(a, b, slabs, N, "f32", split=S, split_stride=M * N, kernel=kernel)
     _lib.call("tdl_splitk_reduce_add", ptr(acc), ptr(slabs), S, acc.numel(), stream_ptr(acc.device))
     return acc
 
 
 def effective_split(K: int, split: int) -> int:
-    """The split the kernel runs: the largest value <= ``split`` dividing the K / 64 steps (every
-    slice the same depth; mirrors tdl_gemm)."""
+    """The split the kernel runs: the largest value <= ``split`` dividing the K / 64 steps with at
+    least two steps per slice (every slice the same depth; both kernels need a distinct first and
+    last K step; mirrors tdl_gemm)."""
     steps = K // BK
-    s = max(1, min(int(split), steps))
+    s = max(1, min(int(split), steps // 2))
     while s > 1 and steps % s:
         s -= 1
     return s

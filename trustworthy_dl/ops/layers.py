@@ -1,8 +1,9 @@
 """Autograd ops for the model compute path.
 
-GPU tensors run the native gfx950 kernels (csrc/norm_act.hip, xent.hip, attention.hip) and
-hipBLASLt GEMMs (csrc/blaslt.cpp); CPU tensors run an equivalent PyTorch reference, which is
-what the CPU/gloo tests exercise.
+GPU tensors run the native gfx950 kernels (csrc/norm_act.hip, xent.hip, attention.hip, gemm.hip:
+the weight-gradient products, the fused MLP GEMMs) and, for the plain bf16 projections where the
+native GEMM is still slower, torch's hipBLASLt GEMM; CPU tensors run an equivalent PyTorch
+reference, which is what the CPU/gloo tests exercise.
 
 Gradient accumulation fusion: a parameter may carry ``.main_grad`` — an fp32 view into its
 stage's flat gradient buffer (parallel/flat.py).  Ops then accumulate that parameter's
@@ -184,16 +185,7 @@ def fwd_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def _gemm_backend(t: torch.Tensor) -> str:
-    """GEMM route for GPU tensors: ``torch`` (default: torch.mm on the hipBLASLt build torch ships
-    with) or ``blaslt`` (direct binding, csrc/blaslt.hip; opt-in via TDL_GEMM=blaslt — it links the
-    system ROCm 7.2 hipBLASLt while torch loads its own copy under the same SONAME)."""
-    if not t.is_cuda:
-        return "cpu"
-    return os.environ.get("TDL_GEMM", "torch")
-
-
-_MM_F32_OK = None
-_ADDMM_F32_OK = None
+    return "gpu" if t.is_cuda else "cpu"
 
 
 def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
@@ -207,62 +199,23 @@ def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
     return _accumulate(bias, dy2.float().sum(0))
 
 
-def wgrad_split(M: int, K: int, N: int) -> int:
-    """Split-K factor for a weight-gradient GEMM [K, M] @ [M, N] (reduction over M tokens).
-    A GPT-2 projection's gradient has only (K/256)(N/256) = 16..64 output tiles of hipBLASLt's
-    256x256 macro tile — a quarter of the 256 CUs or fewer — while M is 8k-32k deep; splitting M
-    into S batched products fills the chip (measured, scripts/bench_gemm.py on MI355X: o-proj
-    350 -> 813 TFLOP/s at M=32768 with S=8, qkv 660 -> 1027 with S=4)."""
-    tiles = max(1, (K // 256) * (N // 256))
-    if os.environ.get("TDL_WGRAD_SPLITK", "1") == "0":
-        return 1
-    if M >= 16384:
-        s = 8 if tiles <= 16 else (4 if tiles <= 64 else 1)
-    elif M >= 8192:
-        s = 4 if tiles <= 16 else 1
-    else:
-        s = 1
-    while s > 1 and (M % s or (M // s) % 64):
-        s //= 2
-    return s
-
-
 def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
-    """acc (fp32, shape of a @ b) += a @ b in one GEMM pass where the torch build allows it.
+    """acc (fp32, shape of a @ b) += a @ b.
 
-    ``a`` is usually X^T (a transposed view of a row-major [M, K] activation): then the product
-    may be split along M into S fp32 partials by one batched GEMM and reduced into ``acc`` by one
-    native pass (wgrad_split)."""
-    global _MM_F32_OK, _ADDMM_F32_OK
+    ``a`` is usually X^T (a transposed view of a row-major [M, K] activation) and ``b`` dY: on the
+    GPU the product runs on the native persistent 4-wave MFMA kernel (csrc/gemm.hip gemm_p4) with the
+    token reduction split so the output tiles x slices fill the CUs in whole rounds, fp32 slices
+    reduced into ``acc`` by one native pass (1.02-1.28x the hipBLASLt batched path on the GPT-2-medium
+    weight gradients at 64k tokens: profiles/r3_gemm_lab.jsonl)."""
     if not a.is_cuda:
         acc.add_((a @ b).float().view(acc.shape))
         return
-    K, M = a.shape
-    N = b.shape[1]
-    S = wgrad_split(M, K, N)
-    if S > 1 and a.t().is_contiguous() and b.is_contiguous() and acc.is_contiguous():
-        a3 = a.t().view(S, M // S, K).transpose(1, 2)
-        b3 = b.view(S, M // S, N)
-        part = torch.empty((S, K, N), dtype=torch.float32, device=acc.device)
-        torch.bmm(a3, b3, out_dtype=torch.float32, out=part)
-        _lib.call("tdl_splitk_reduce_add", ptr(acc), ptr(part), S, acc.numel(), stream_ptr(acc.device))
+    from . import gemm
+    if acc.dtype == torch.float32 and acc.is_contiguous() and acc.dim() == 2 and gemm.supported(a, b):
+        gemm.matmul_f32_acc(acc, a, b)
         return
-    if _ADDMM_F32_OK is not False:
-        # beta=1 GEMM epilogue accumulating in place into the fp32 buffer (one pass)
-        try:
-            torch.ops.aten.addmm.dtype_out(acc, a, b, torch.float32, beta=1, alpha=1, out=acc)
-            _ADDMM_F32_OK = True
-            return
-        except (RuntimeError, TypeError):
-            _ADDMM_F32_OK = False
-    if _MM_F32_OK is not False:
-        try:
-            acc.add_(torch.mm(a, b, out_dtype=torch.float32).view(acc.shape))
-            _MM_F32_OK = True
-            return
-        except (RuntimeError, TypeError):
-            _MM_F32_OK = False
-    acc.add_(torch.mm(a, b).float().view(acc.shape))
+    # shapes the native kernel does not take (K % 64, unaligned rows): one library GEMM, fp32 out
+    acc.add_(torch.mm(a, b, out_dtype=torch.float32).view(acc.shape))
 
 
 def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
@@ -285,10 +238,7 @@ class _Linear(torch.autograd.Function):
             x2 = x2.contiguous()
         backend = _gemm_backend(x)
         pre = None
-        if backend == "blaslt":
-            from . import blaslt
-            y, pre = blaslt.linear_fwd(x2, weight, bias, act)
-        elif backend == "cpu":
+        if backend == "cpu":
             y = x2 @ weight
             if bias is not None:
                 y = y + bias
@@ -317,11 +267,7 @@ class _Linear(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         backend = ctx.backend
-        if backend == "blaslt":
-            from . import blaslt
-            dx, gw, gb = blaslt.linear_bwd(x2, weight, bias, pre, dy2, ctx.act,
-                                           ctx.needs_input_grad[0])
-        elif backend == "cpu":
+        if backend == "cpu":
             if ctx.act == "gelu":
                 pre_ = pre.detach().requires_grad_(True)
                 with torch.enable_grad():
@@ -515,10 +461,7 @@ class _LinearT(torch.autograd.Function):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1]).contiguous()
         backend = _gemm_backend(x)
-        if backend == "blaslt":
-            from . import blaslt
-            y = blaslt.linear_t_fwd(x2, weight)
-        elif backend == "cpu":
+        if backend == "cpu":
             y = x2 @ weight.t()
         else:
             y = torch.mm(x2, weight.t())
@@ -532,16 +475,12 @@ class _LinearT(torch.autograd.Function):
         dy2 = dy.reshape(-1, weight.shape[0])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        if ctx.backend == "blaslt":
-            from . import blaslt
-            dx, gw = blaslt.linear_t_bwd(x2, weight, dy2, ctx.needs_input_grad[0])
+        dx = (dy2 @ weight) if ctx.needs_input_grad[0] else None
+        if _wants_main_grad(weight):
+            run_or_defer(lambda: _wgrad_into(weight, dy2.t(), x2))
+            gw = None
         else:
-            dx = (dy2 @ weight) if ctx.needs_input_grad[0] else None
-            if _wants_main_grad(weight):
-                run_or_defer(lambda: _wgrad_into(weight, dy2.t(), x2))
-                gw = None
-            else:
-                gw = _wgrad_into(weight, dy2.t(), x2)
+            gw = _wgrad_into(weight, dy2.t(), x2)
         return (dx.reshape(ctx.shape) if dx is not None else None), gw
 
 

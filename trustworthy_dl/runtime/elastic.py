@@ -25,6 +25,7 @@ never exec()s: workers are children, and the supervisor exits with the job's cod
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import logging
 import os
@@ -69,11 +70,40 @@ def blame(codes: Dict[int, int]) -> List[int]:
     return []
 
 
+def node_ids_from_env(world: int) -> List[int]:
+    """Physical identity of each rank of this generation: the original (generation-0) rank of the
+    node now running as rank i (TDL_ELASTIC_NODE_IDS, set by the supervisor; identity otherwise).
+    Checkpoints record it so a resume on survivors re-attaches trust / detection state to the same
+    physical nodes, whichever ranks were lost (utils/checkpoint._resize_trust)."""
+    raw = os.environ.get("TDL_ELASTIC_NODE_IDS", "")
+    try:
+        ids = [int(x) for x in raw.split(",") if x.strip()]
+    except ValueError:
+        ids = []
+    return ids if len(ids) == world else list(range(world))
+
+
+def default_devices(nproc: int, env: Optional[Dict[str, str]] = None) -> Optional[List[str]]:
+    """GPU list when --devices is not given: the inherited HIP_VISIBLE_DEVICES, else 0..nproc-1 on a
+    host with GPUs (so that dropping a lost rank drops ITS GPU, not the last one); None without GPUs
+    (CPU / gloo jobs)."""
+    env = os.environ if env is None else env
+    vis = env.get("HIP_VISIBLE_DEVICES") or env.get("ROCR_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+    if vis:
+        devs = [d.strip() for d in vis.split(",") if d.strip()]
+        if len(devs) >= nproc:
+            return devs[:nproc]
+    if os.path.exists("/dev/kfd") and glob.glob("/dev/dri/renderD*"):
+        return [str(i) for i in range(nproc)]
+    return None
+
+
 @dataclass
 class Generation:
     index: int
     world: int
     devices: Optional[List[str]]
+    node_ids: List[int] = field(default_factory=list)
     exit_codes: Dict[int, Optional[int]] = field(default_factory=dict)
     lost: List[int] = field(default_factory=list)
     wall_s: float = 0.0
@@ -86,10 +116,10 @@ class ElasticSupervisor:
                  env: Optional[Dict[str, str]] = None, python: str = sys.executable, log_dir: Optional[str] = None):
         self.train_args = list(train_args)
         self.nproc, self.min_nproc, self.max_restarts = nproc, max(1, min_nproc), max_restarts
-        self.devices = list(devices) if devices else None
+        self.env = dict(os.environ if env is None else env)
+        self.devices = list(devices) if devices else default_devices(nproc, self.env)
         self.grace_s, self.timeout_s = grace_s, timeout_s
         self.window_s = 2.0  # exits this close to the first one count as "went down together"
-        self.env = dict(os.environ if env is None else env)
         self.python = python
         self.log_dir = log_dir
         self.generations: List[Generation] = []
@@ -99,8 +129,20 @@ class ElasticSupervisor:
         args = list(self.train_args)
         if "--abort-on-offline" not in args:
             args.append("--abort-on-offline")
-        if gen > 0 and "--resume" not in args:
-            args += ["--resume", "latest"]
+        if gen > 0:
+            # a restart resumes from the newest complete checkpoint — including those the failed
+            # generation wrote — never from the user's original --resume path again
+            out, i = [], 0
+            while i < len(args):
+                if args[i] == "--resume":
+                    i += 2
+                    continue
+                if args[i].startswith("--resume="):
+                    i += 1
+                    continue
+                out.append(args[i])
+                i += 1
+            args = out + ["--resume", "latest"]
         return [self.python, "-m", "trustworthy_dl.cli", *args]
 
     def _report_dir(self, g: Generation) -> str:
@@ -130,7 +172,8 @@ class ElasticSupervisor:
             env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(g.world), "LOCAL_WORLD_SIZE": str(g.world),
                         "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                         "TDL_ELASTIC_GENERATION": str(g.index), "TDL_ELASTIC_RESTARTS": str(g.index),
-                        "TDL_ELASTIC_REPORT_DIR": rdir})
+                        "TDL_ELASTIC_REPORT_DIR": rdir,
+                        "TDL_ELASTIC_NODE_IDS": ",".join(str(n) for n in (g.node_ids or range(g.world)))})
             if g.devices is not None:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(g.devices)
             out = None
@@ -213,9 +256,9 @@ class ElasticSupervisor:
 
     # ------------------------------------------------------------------ driver
     def run(self) -> Dict:
-        world, devices = self.nproc, self.devices
+        world, devices, ids = self.nproc, self.devices, list(range(self.nproc))
         for gi in range(self.max_restarts + 1):
-            g = self._run_generation(Generation(gi, world, devices))
+            g = self._run_generation(Generation(gi, world, devices, list(ids)))
             self.generations.append(g)
             logger.info("elastic: generation %d world %d -> %s (lost %s, %.1fs)", gi, world,
                         "ok" if g.ok else "failed", g.lost, g.wall_s)
@@ -227,13 +270,15 @@ class ElasticSupervisor:
                 break
             if devices is not None:
                 devices = [devices[r] for r in survivors]
+            ids = [ids[r] for r in survivors]
             world = len(survivors)
         return self.summary()
 
     def summary(self) -> Dict:
         return {"ok": bool(self.generations and self.generations[-1].ok),
                 "final_world": self.generations[-1].world if self.generations else 0,
-                "generations": [{"gen": g.index, "world": g.world, "devices": g.devices, "ok": g.ok, "lost": g.lost,
+                "generations": [{"gen": g.index, "world": g.world, "devices": g.devices, "node_ids": g.node_ids,
+                                 "ok": g.ok, "lost": g.lost,
                                  "exit_codes": g.exit_codes, "wall_s": round(g.wall_s, 2)} for g in self.generations]}
 
 
@@ -247,7 +292,8 @@ def main(argv=None) -> int:
     ap.add_argument("--nproc", type=int, required=True)
     ap.add_argument("--min-nproc", type=int, default=1)
     ap.add_argument("--max-restarts", type=int, default=3)
-    ap.add_argument("--devices", type=str, default=None, help="comma list of GPU ids (default: 0..nproc-1 on GPU hosts)")
+    ap.add_argument("--devices", type=str, default=None,
+                    help="comma list of GPU ids (default: the inherited HIP_VISIBLE_DEVICES, else 0..nproc-1 on GPU hosts)")
     ap.add_argument("--grace", type=float, default=60.0, help="seconds the survivors get to abort after a loss")
     ap.add_argument("--log-dir", type=str, default=None)
     ap.add_argument("--summary", type=str, default=None, help="write the generation summary JSON here")

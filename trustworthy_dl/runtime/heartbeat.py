@@ -40,6 +40,8 @@ class HeartbeatMonitor:
         self._paused = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.events = []
+        self._store_fail_since: Optional[float] = None  # first of the current run of store errors
+        self.store_host = 0  # the rank hosting the c10d TCPStore (torch.distributed: rank 0)
 
     def _report_offline(self):
         """Tell the elastic supervisor (runtime/elastic.py) whom this rank saw go silent: the vote
@@ -89,14 +91,43 @@ class HeartbeatMonitor:
                         os._exit(17)
                 self._last_change.setdefault(r, now)
 
+    def store_failed(self, exc: Exception, now: Optional[float] = None):
+        """The store itself is unreachable.  It lives in the store host's process (rank 0), so when
+        that rank dies every survivor's beat / poll fails: after ``timeout`` seconds of consecutive
+        failures the host is declared OFFLINE like any silent peer (with ``abort_on_offline`` the
+        survivors report it and exit 17 instead of sitting in RCCL until the supervisor's grace
+        period runs out).  A single failure (store busy, shutdown) only starts the clock."""
+        now = time.monotonic() if now is None else now
+        if self._store_fail_since is None:
+            self._store_fail_since = now
+            logger.debug("heartbeat: store error (%s)", exc)
+            return
+        host = self.store_host
+        if host == self.rank or now - self._store_fail_since <= self.timeout:
+            return
+        with self._lock:
+            if host in self._offline:
+                return
+            self._offline.add(host)
+            self.events.append({"node_id": host, "event": "offline", "time": time.time(), "reason": "store"})
+        logger.error("heartbeat: store on rank %d unreachable for > %.1fs -> node %d OFFLINE (%s)", host,
+                     self.timeout, host, exc)
+        if self.on_offline:
+            self.on_offline(host)
+        if self.abort_on_offline:
+            self._report_offline()
+            os._exit(17)
+
     def _run(self):
         while not self._stop.is_set():
             if not self._paused.is_set():
                 try:
                     self.beat()
                     self.poll()
-                except Exception as e:  # noqa: BLE001 - store gone during shutdown
-                    logger.debug("heartbeat thread: %s", e)
+                    self._store_fail_since = None
+                except Exception as e:  # noqa: BLE001 - store gone (host died, or shutdown)
+                    if not self._stop.is_set():
+                        self.store_failed(e)
             self._stop.wait(self.interval)
 
     def start(self) -> "HeartbeatMonitor":

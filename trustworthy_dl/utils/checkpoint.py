@@ -25,6 +25,8 @@ from typing import Dict, Optional, Sequence, Set, Tuple
 import torch
 import torch.distributed as dist
 
+from ..runtime.elastic import node_ids_from_env
+
 logger = logging.getLogger(__name__)
 
 
@@ -47,6 +49,9 @@ def _base_dict(trainer) -> Dict:
         "device_trust": e.trust_state(),
         "detector": _jsonable(trainer.attack_detector.state_dict()),
         "config": _jsonable(asdict(trainer.config)),
+        # physical identity of each node (its generation-0 rank under the elastic supervisor)
+        "node_ids": node_ids_from_env(trainer.config.num_nodes),
+        "excluded": [int(n) for n in getattr(e, "excluded", [])],
     }
 
 
@@ -149,22 +154,59 @@ def _layer_states(path: str, ck: Dict, saved_plan, want: Set[int]) -> Tuple[Dict
     return out, step
 
 
+def _node_map(saved_ids, live_ids) -> Dict[int, int]:
+    """live node index -> saved node index of the same physical node (absent: a node the saved job
+    did not have, which starts fresh)."""
+    where = {int(p): j for j, p in enumerate(saved_ids)}
+    return {i: where[int(p)] for i, p in enumerate(live_ids) if int(p) in where}
+
+
 def _resize_trust(trainer, ck: Dict, live: int):
-    """Trust state of a job resumed on ``live`` nodes: nodes beyond it are retired (their records
-    stay in the attack / reassignment histories), missing ones start fresh."""
+    """Trust state of a job resumed on ``live`` nodes.  Node records follow the PHYSICAL node: the
+    checkpoint's ``node_ids`` and this job's (TDL_ELASTIC_NODE_IDS) map each live node to the saved
+    record of the same node, so losing rank 0 or 1 of 3 does not hand the lost node's trust or
+    COMPROMISED status to whichever survivor inherits its index.  Retired nodes' records stay in the
+    attack / reassignment histories; nodes the saved job did not have start fresh."""
     tm = trainer.trust_manager
+    saved_n = int(ck["device_trust"]["values"].numel()) if "device_trust" in ck else \
+        int(ck.get("trust_manager", {}).get("num_nodes", live))
+    saved_ids = ck.get("node_ids") or list(range(saved_n))
+    live_ids = node_ids_from_env(live)
+    m = _node_map(saved_ids, live_ids)
     if "trust_manager" in ck:
         tm.load_state_dict(ck["trust_manager"])
-    for n in [n for n in list(tm.trust_scores) if n >= live]:
-        tm.trust_scores.pop(n, None)
-        tm.node_status.pop(n, None)
-        tm.node_metrics.pop(n, None)
-    tm.num_nodes = min(tm.num_nodes, live)
+        old_scores, old_status, old_metrics = tm.trust_scores, tm.node_status, tm.node_metrics
+        old_attacks, old_last = tm.attack_history, tm._last_step
+        tm.trust_scores, tm.node_status, tm.node_metrics = {}, {}, {}
+        tm.attack_history = type(old_attacks)(list)
+        tm._last_step = {}
+        tm.num_nodes = 0
+        for i in range(live):
+            j = m.get(i)
+            if j is not None and j in old_scores:
+                tm.trust_scores[i] = old_scores[j]
+                tm.node_status[i] = old_status[j]
+                tm.node_metrics[i] = old_metrics[j]
+                if j in old_attacks:
+                    tm.attack_history[i] = list(old_attacks[j])
+                if j in old_last:
+                    tm._last_step[i] = old_last[j]
+        tm.num_nodes = live
+        for i in range(live):
+            if i not in tm.trust_scores:
+                tm.initialize_node(i)
     tm.resize(live)
     if "device_trust" in ck:
         sd = ck["device_trust"]
-        k = min(live, int(sd["values"].numel()))
-        trainer.engine.load_trust_state({key: v[:k] for key, v in sd.items()}, partial=True)
+        cur = trainer.engine.trust_state()
+        for key in cur:
+            for i, j in m.items():
+                if j < sd[key].numel() and i < cur[key].numel():
+                    cur[key][i] = sd[key][j]
+        trainer.engine.load_trust_state(cur)
+    # nodes excluded for compromise stay excluded — the same physical nodes, under their new ranks
+    saved_ex = {int(n) for n in ck.get("excluded", [])}
+    trainer.engine.excluded = sorted(i for i, j in m.items() if j in saved_ex)
 
 
 def load_checkpoint(trainer, path: str):
