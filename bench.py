@@ -264,10 +264,16 @@ def run(args):
     progress.mark("report")
     el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}" if use_cuda else "cpu")
     hwq_all = [hwq]
+    inv = engine.comm_inventory()
+    inv_all = [inv]
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         hwq_all = [None] * world
         dist.all_gather_object(hwq_all, hwq)
+        inv_all = [None] * world
+        dist.all_gather_object(inv_all, inv)
+    if use_cuda and not all(i["within_queue_budget"] for i in inv_all):
+        print(f"[bench] WARNING: a rank's HIP streams exceed its hardware queues: {inv_all}", file=sys.stderr, flush=True)
     elapsed = float(el)
     tokens = global_batch * args.seq_len * args.steps
     tps = tokens / elapsed
@@ -287,7 +293,14 @@ def run(args):
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
                        "native_gemm": os.environ.get("TDL_NATIVE_GEMM", "mlp"),
+                       "native_wgrad": os.environ.get("TDL_WGRAD_KERNEL", "p4"),
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
+                       # per-rank RCCL communicators / HIP streams (compute + verification + one per
+                       # communicator) vs the hardware-queue budget (PipelineEngine.comm_inventory)
+                       "rccl_comms_per_rank": [i["rccl_comms"] for i in inv_all],
+                       "hip_streams_per_rank": [i["hip_streams"] for i in inv_all],
+                       "process_groups_created": inv["groups_created"],
+                       "within_queue_budget": all(i["within_queue_budget"] for i in inv_all),
                        "reassignments": [{"step": r["step"], "from_nodes": r["from_nodes"],
                                           "migration_ms": round(1000 * r["migration_time"], 2),
                                           "plan": r["plan"]} for r in engine.reassignment_history]},

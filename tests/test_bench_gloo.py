@@ -49,6 +49,17 @@ def test_bench_multirank_json_line(n, mode):
     assert d["config"]["p2p_mode"] == mode and d["config"]["p2p_mode_requested"] == mode
     assert len(d["config"]["hw_queues_per_rank"]) == n
     assert out.stderr.count("GPU_MAX_HW_QUEUES=") == n        # every rank logs its queue setting
+    # communicator / stream inventory per rank: interior stages talk to 2 neighbours, end stages to 1
+    comms, streams = d["config"]["rccl_comms_per_rank"], d["config"]["hip_streams_per_rank"]
+    assert len(comms) == n and len(streams) == n
+    per_peer = 2 if mode == "async" else 1            # async: one activation + one gradient communicator per peer
+    groups = 2 if mode == "async" else 0              # the two direction groups
+    tie = 1                                           # the tied embedding / LM head all-reduce group
+    for r, c in enumerate(comms):
+        peers = (r > 0) + (r < n - 1)
+        assert c == 1 + groups + (tie if r in (0, n - 1) else 0) + per_peer * peers, (r, comms)
+        assert streams[r] == c + 2                    # + compute stream + verification side stream
+    assert max(streams) <= 32
 
 
 def test_bench_midrun_reassign():
@@ -59,6 +70,8 @@ def test_bench_midrun_reassign():
     assert r["from_nodes"] == [3] and r["step"] == 2
     assert "@rank3" not in r["plan"] and r["plan"].count("stage") == 3
     assert d["config"]["last_loss"] is not None and d["value"] > 0
+    # the re-plan reused the direction groups and created ONE new tie group (ranks 0 and 2)
+    assert d["config"]["process_groups_created"] == 2 + 1 + 1
 
 
 @pytest.mark.parametrize("fault", ["hang", "raise"])

@@ -184,3 +184,46 @@ def test_distributed_reshard_restores_from_shadow_and_matches_local():
         assert abs(got[li] - ref[li]) <= 1e-4 * max(1.0, abs(ref[li])), (li, got[li], ref[li])
     assert max(abs(v) for v in ref.values()) < 1e6
     assert res[0]["last_loss"] is not None and abs(res[0]["last_loss"] - eng.last_loss) < 1e-3
+
+
+def _replan_worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _build("gpt2-tiny", world, 2)
+    batches = _make_batches("gpt2-tiny", 6, 4)
+    inv = [eng.comm_inventory()]
+    eng.train_step(batches[0])
+    eng.flush()
+    eng.reassign([world - 1], 1)              # re-shard away from the last rank: a new tie group
+    inv.append(eng.comm_inventory())
+    for i in range(3):                         # three more re-plans onto member sets seen before
+        eng._build()
+        eng.train_step(batches[1 + i])
+        eng.flush()
+        inv.append(eng.comm_inventory())
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump({"inv": inv, "loss": eng.last_loss}, f)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replans_reuse_process_groups():
+    """Re-plans do not leak communicators: groups are cached by member set, so re-planning onto a
+    member set seen before creates nothing; each rank's communicator and stream counts stay bounded
+    and within the 32 hardware queues (verdict r2: every _build created new tie / DP groups)."""
+    world = 4
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "inv")
+        mp.spawn(_replan_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    for r in res:
+        created = [i["groups_created"] for i in r["inv"]]
+        assert created[0] == 3                   # act + grad direction groups + tie group (0, 3)
+        assert created[1] == 4                   # + tie group (0, 2) after the re-shard
+        assert created[2:] == [4, 4, 4]          # re-plans onto known member sets reuse them
+        assert all(i["hip_streams"] <= 32 for i in r["inv"])
+        assert r["inv"][-1]["rccl_comms"] == r["inv"][1]["rccl_comms"]
+        assert r["loss"] is not None

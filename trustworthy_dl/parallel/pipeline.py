@@ -292,6 +292,10 @@ class PipelineEngine:
                         tied.add(id(prm))
         for st in self.stages.values():
             st.set_early_stats(tied)
+            # early tied all-reduce only with hardware queues to spare (the p2p "async" mode): its
+            # RCCL kernel waits on a stream of its own for the embedding stage, and on a queue
+            # shared with the compute stream it would block the rest of this stage's backward
+            st.on_tied_ready = self._launch_tied_allreduce if self.distributed and self.p2p_mode == "async" else None
 
     def _set_clip_exclusions(self):
         """Count every tied weight once in the global clipping norm: the stage owning the first
@@ -308,22 +312,40 @@ class PipelineEngine:
             st.set_clip_exclusions(ex)
 
     def _build_comm(self):
+        """Communicators and streams of one rank (every one of them, by purpose):
+
+        * default group (init_process_group): digest all-gather, plan broadcast, clip-norm / step
+          all-reduces, migration and shadow-snapshot P2P (RCCL creates one 2-rank communicator per
+          peer pair it sends to or receives from);
+        * ``_dir_groups`` (async P2P mode): one group for activations (stage s -> s+1) and one for
+          activation gradients (s+1 -> s), each with a 2-rank communicator per neighbour pair;
+        * tie group (tied embedding / LM head on different ranks): the tied-gradient all-reduce;
+        * DP group (data_parallel > 1): the replica gradient all-reduce and direction check.
+        Under torch's RCCL backend every communicator has one stream of its own; add the compute
+        stream and one verification side stream per local stage (security/stage_verifier.py).
+        Groups are cached by member set and reused across re-plans (a re-shard creates a group only
+        for a member set never seen before; ``comm_inventory`` reports the totals against the
+        hardware-queue budget, runtime/hwqueues.py)."""
         self.comm = None
         self.tie_group = None
         self.tie_members: List[int] = []
+        if not hasattr(self, "_group_cache"):
+            self._group_cache: Dict[Tuple[str, Tuple[int, ...]], object] = {}
+            self._p2p_peers: Dict[str, set] = {}
         if not self.distributed:
             return
         s = self.plan.stage_of_rank(self.rank)
         prev = self.plan.ranks[s - 1] if s is not None and s > 0 else None
         nxt = self.plan.ranks[s + 1] if s is not None and s + 1 < self.plan.num_stages else None
         self.comm = P2PComm(prev, nxt, self.device)
+        for peer in (prev, nxt):
+            if peer is not None:
+                self._p2p_peers.setdefault("default" if self.p2p_mode != "async" else "dir", set()).add(peer)
         if self.p2p_mode == "async" and getattr(self, "_dir_groups", None) is None:
             # one communicator for activations (stage s -> s+1), one for activation gradients
             # (s+1 -> s): each carries one-way, in-order traffic per neighbour pair
             everyone = list(range(self.world))
-            self._dir_groups = (dist.new_group(ranks=everyone), dist.new_group(ranks=everyone))
-            for g in self._dir_groups:
-                self._warm_group(g, everyone)
+            self._dir_groups = (self._group("act", everyone), self._group("grad", everyone))
         # tied parameters living on different ranks need a gradient all-reduce group (one per
         # replica; new_group is collective over the whole world, so every rank creates them all)
         base = self.replica * self.pp
@@ -331,16 +353,46 @@ class PipelineEngine:
         self.tie_members = [base + r for r in local] if len(local) > 1 else []
         if len(local) > 1:
             for d in range(self.dp):
-                g = dist.new_group(ranks=[d * self.pp + r for r in local])
-                self._warm_group(g, [d * self.pp + r for r in local])
+                g = self._group("tie", [d * self.pp + r for r in local])
                 if d == self.replica:
                     self.tie_group = g
         if self.dp > 1 and self.dp_group is None:
             for pos in range(self.pp):
-                g = dist.new_group(ranks=[d * self.pp + pos for d in range(self.dp)])
-                self._warm_group(g, [d * self.pp + pos for d in range(self.dp)])
+                g = self._group("dp", [d * self.pp + pos for d in range(self.dp)])
                 if pos == self.rank % self.pp:
                     self.dp_group = g
+
+    def _group(self, purpose: str, members: List[int]):
+        """The process group of ``members`` for ``purpose``, created (collectively, in the same
+        order on every rank) and warmed only the first time this member set is asked for."""
+        key = (purpose, tuple(members))
+        g = self._group_cache.get(key)
+        if g is None:
+            g = dist.new_group(ranks=list(members))
+            self._warm_group(g, list(members))
+            self._group_cache[key] = g
+        return g
+
+    def _note_peers(self, sends, recvs):
+        peers = getattr(self, "_p2p_peers", None)
+        if peers is not None:
+            peers.setdefault("default", set()).update(int(p) for _, p in list(sends) + list(recvs))
+
+    def comm_inventory(self) -> Dict[str, object]:
+        """Per-rank communicator / stream count by purpose, against the HIP hardware-queue budget.
+        Communicators: the default group's, one per cached group this rank belongs to, and one
+        2-rank P2P communicator per (group, peer) this rank has exchanged with."""
+        groups = [{"purpose": p, "members": list(m)} for (p, m) in getattr(self, "_group_cache", {})]
+        mine = [g for g in groups if self.rank in g["members"]]
+        p2p = {k: sorted(v) for k, v in getattr(self, "_p2p_peers", {}).items()}
+        n_p2p = sum(len(v) * (2 if k == "dir" else 1) for k, v in p2p.items())
+        n_comms = (1 if self.distributed else 0) + len(mine) + n_p2p
+        streams = 1 + len(self.stages) + n_comms   # compute + verification side streams + RCCL streams
+        from ..runtime.hwqueues import effective_hw_queues
+        q = effective_hw_queues() if self.device.type == "cuda" else None
+        return {"groups_created": len(groups), "groups_member": len(mine), "p2p_peers": p2p,
+                "rccl_comms": n_comms, "hip_streams": streams, "hw_queues": q,
+                "within_queue_budget": q is None or streams <= q}
 
     def _choose_p2p_mode(self, cfg: EngineConfig) -> str:
         """Pre-posted receives ("async") need the RCCL streams on hardware queues of their own:
@@ -780,8 +832,36 @@ class PipelineEngine:
         return in_shape, out_shape
 
     # ------------------------------------------------------------------ step epilogue
+    def _tied_grad(self):
+        st = self.my_stage()
+        if st is None:
+            return None
+        for grp in self.ties:
+            for li, attr in grp:
+                p = st.local_param(li, attr)
+                if p is not None:
+                    return p.main_grad
+        return None
+
+    def _launch_tied_allreduce(self):
+        """Called from the autograd hook that sees this stage's tied weight's last gradient
+        contribution of the step (the LM head's, early in the last stage's final backward): the
+        tied-gradient all-reduce starts right away on its communicator's stream, overlapping the
+        rest of the backward, instead of after the drain.  The embedding's side joins when its
+        gradient is final (its backward is the stage's last); ``_allreduce_tied`` waits."""
+        if getattr(self, "_tie_work", None) is not None or not self.tie_members or self.rank not in self.tie_members:
+            return
+        g = self._tied_grad()
+        if g is not None:
+            self._tie_work = dist.all_reduce(g, group=self.tie_group, async_op=True)
+
     def _allreduce_tied(self):
         if not self.ties:
+            return
+        work = getattr(self, "_tie_work", None)
+        if work is not None:
+            self._tie_work = None
+            work.wait()
             return
         if not self.distributed:
             # local mode: tied copies on different stages -> sum their grads into both
@@ -1331,6 +1411,7 @@ class PipelineEngine:
                     packed[li] = buf
                 if src != dst:
                     moved += self._layer_numel(li)
+            self._note_peers(sends, recvs)
             batched_transfer(sends, recvs, meter=self.link_meter)
             step_t = torch.tensor([float(step_count)], device=self.device)
             dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
@@ -1414,6 +1495,7 @@ class PipelineEngine:
             vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
             buf = torch.empty(sum(self._packed_numel(li) for li in range(a, b)), dtype=torch.float32,
                               device=self.device)
+            self._note_peers([(vec, self._shadow_holder(self.rank))], [(buf, pred)])
             batched_transfer([(vec, self._shadow_holder(self.rank))], [(buf, pred)], meter=self.link_meter)
             self._shadow_pend[pred] = (step, buf)
         else:

@@ -118,8 +118,10 @@ class Stage:
         gradient changes in the tied all-reduce after the backward) are left to the final pass."""
         ex = set(excluded_ids)
         per_layer: Dict[int, List[int]] = {}
+        self._tied_layers = set()
         for j, (name, q) in enumerate(zip(self.flat.names, self.flat.params)):
             if id(q) in ex:
+                self._tied_layers.add(int(name.split(".", 1)[0]))
                 continue
             per_layer.setdefault(int(name.split(".", 1)[0]), []).append(j)
         self._layer_seg_runs = {}
@@ -139,6 +141,9 @@ class Stage:
             runs += self._layer_seg_runs.get(li, [])
         if runs:
             self.verifier.grad_ready(self.flat.grad, runs)
+        cb = getattr(self, "on_tied_ready", None)
+        if cb is not None and any(li in getattr(self, "_tied_layers", ()) for li in self._runner_layer_idx[runner_idx]):
+            cb()  # a tied weight's gradient is final: its cross-stage all-reduce can start
 
     def forward(self, x, labels=None, observe=None, arm_grad_stats: bool = False):
         """Returns (output, monitored_activation).  Loss stages return the (scalar) loss.
