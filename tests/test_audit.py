@@ -1,0 +1,111 @@
+"""Deterministic stage cross-check (recompute audit): the next stage recomputes a stage's monitored
+micro-batch from its input and weights and compares the output it received.  Blame for a tampered
+forward comes only from a mismatch (or a failed weight-integrity check), never from output
+z-scores, so echoes downstream and clean stages are never blamed (verdict r2: configs 4 / 5 blamed
+clean stages on output statistics).  Local mode and 3 gloo ranks (CPU)."""
+import json
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        ids = torch.randint(0, 1000, (4, 33), generator=g)
+        out.append({"input": ids[:, :-1].contiguous(), "target": ids[:, 1:].contiguous()})
+    return out
+
+
+def _engine(nodes, attack=None, targets=(), start=6, **cfg):
+    from trustworthy_dl.attacks.adversarial_attacks import AdversarialAttacker, AttackConfig
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    att = None
+    if attack:
+        att = AdversarialAttacker(AttackConfig(attack_types=[attack], target_nodes=list(targets), intensity=0.5,
+                                               start_step=start, probability=1.0, seed=3))
+        att.activate_attacks()
+    m = get_model("gpt2-tiny", seq_len=32, seed=1)
+    return PipelineEngine(m, EngineConfig(num_nodes=nodes, micro_batches=2, device="cpu", seq_len=32, reassign=False,
+                                          monitor_seed=0, **cfg), attacker=att)
+
+
+def _blamed(eng):
+    return sorted({(a["step"], a["node_id"], a["attack_type"]) for a in eng.attack_history})
+
+
+def test_local_byzantine_blames_only_the_tampering_stages():
+    eng = _engine(4, "byzantine", targets=(0, 2))
+    for b in _batches(10):
+        eng.train_step(b)
+    eng.flush()
+    got = _blamed(eng)
+    assert {n for _, n, _ in got} == {0, 2}, got           # not their downstream echoes 1 / 3
+    assert all(k == "output_tampering" for _, _, k in got)
+    assert {s for s, _, _ in got} == set(range(6, 11))       # every attacked step, nothing before
+
+
+def test_local_clean_run_blames_nobody():
+    eng = _engine(4)
+    for b in _batches(12):
+        eng.train_step(b)
+    eng.flush()
+    assert eng.attack_history == []
+
+
+def test_local_param_perturbation_is_integrity_not_audit():
+    eng = _engine(3, "model_poisoning", targets=(1,))
+    for b in _batches(9):
+        eng.train_step(b)
+    eng.flush()
+    got = _blamed(eng)
+    assert {n for _, n, _ in got} == {1}, got
+    assert all(k == "model_poisoning" for _, _, k in got)
+
+
+def _worker(rank, world, port, out_path, attack, targets):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _engine(world, attack, targets=targets)
+    for b in _batches(9):
+        eng.train_step(b)
+    eng.flush()
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump({"blamed": _blamed(eng), "inv": eng.comm_inventory()["p2p_peers"]}, f)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("attack,targets", [("byzantine", (1,)), ("byzantine", (0,)), (None, ())])
+def test_distributed_audit(attack, targets):
+    world = 3
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "r")
+        mp.spawn(_worker, args=(world, _free_port(), out, attack, targets), nprocs=world, join=True)
+        res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    assert res[0]["blamed"] == res[1]["blamed"] == res[2]["blamed"]   # every rank agrees
+    got = res[0]["blamed"]
+    if attack is None:
+        assert got == []
+    else:
+        assert {n for _, n, _ in got} == set(targets), got
+        assert all(k == "output_tampering" for _, _, k in got)
+        assert {s for s, _, _ in got} == set(range(6, 10))

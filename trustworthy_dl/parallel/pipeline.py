@@ -82,6 +82,13 @@ class EngineConfig:
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
                                          # (0 = off); a compromised stage is restored from it, not from itself
+    audit: bool = True                   # deterministic stage cross-check: the next stage recomputes every
+                                         # non-loss stage's monitored micro-batch from its input and weights and
+                                         # compares the output it received; blame for a tampered forward comes
+                                         # only from such a mismatch or a failed weight-integrity check, output
+                                         # z-scores no longer blame (they stay in the trust metrics)
+    audit_prob: float = 1.0              # fraction of steps audited (drawn from the private monitor RNG)
+    audit_tol: float = 1e-2              # relative max error above which a recomputed output mismatches
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     soft_output_z: float = 5.0           # with an output flag in a replica, an EARLIER stage whose output z
                                          # exceeds this (below its own decision threshold) is the source: a
@@ -373,10 +380,10 @@ class PipelineEngine:
             self._group_cache[key] = g
         return g
 
-    def _note_peers(self, sends, recvs):
+    def _note_peers(self, sends, recvs, kind: str = "default"):
         peers = getattr(self, "_p2p_peers", None)
         if peers is not None:
-            peers.setdefault("default", set()).update(int(p) for _, p in list(sends) + list(recvs))
+            peers.setdefault(kind, set()).update(int(p) for _, p in list(sends) + list(recvs))
 
     def comm_inventory(self) -> Dict[str, object]:
         """Per-rank communicator / stream count by purpose, against the HIP hardware-queue budget.
@@ -474,6 +481,16 @@ class PipelineEngine:
         targets = split_micro(tgt, M)
         oc = self.cfg.output_check
         self._mon_idx = -1 if oc == "none" else (self._mon_rng.randrange(M) if oc == "random" else 0)
+        # audited steps: the same decision on every rank (a hash of the step; every step at the
+        # default audit_prob = 1); WHICH micro-batch is audited is the auditor's private choice
+        self._audit_now = bool(self.cfg.audit and self.plan.num_stages > 1 and (
+            self.cfg.audit_prob >= 1.0 or
+            (hash((self.cfg.seed, self.global_step)) % 1_000_003) / 1_000_003 < self.cfg.audit_prob))
+        self._audit_rec: Dict[int, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
+        self._audit_inputs: Dict[int, torch.Tensor] = {}   # distributed: this stage's received inputs
+        self._audit_batch = inputs
+        if self._audit_now and not self.distributed and self._mon_idx < 0:
+            self._audit_now = False
         if self.distributed:
             loss = self._run_1f1b(inputs, targets, truth)
         else:
@@ -536,12 +553,16 @@ class PipelineEngine:
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
                 watch = i == self._mon_idx
                 obs = st.output_observer() if watch else None
+                if watch and self._audit_now:
+                    x_in = x.detach().clone()
                 with self.tracer.phase("fwd"):
                     y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1)
                 if not st.computes_loss:
                     y = self._attack_output(node, y, truth)
                     if watch:
                         mon = y
+                        if self._audit_now:
+                            self._audit_rec[node] = (x_in, y.detach().clone())
                 if watch and mon is not None:
                     st.verifier.observe_output(mon)
                     if st.computes_loss and st.verifier.side is not None:
@@ -590,6 +611,10 @@ class PipelineEngine:
             labels = targets[i].to(st.device, non_blocking=True) if last else None
             watch = i == self._mon_idx
             obs = st.output_observer() if watch else None
+            if self._audit_now and not first:
+                # every received input stays referenced until the audit (no copy): it is the previous
+                # stage's output as seen here (audited here) and my input (the next stage audits me)
+                self._audit_inputs[i] = x.detach()
             y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1 and not defer_w)
             if last:
                 y = y / M
@@ -726,6 +751,10 @@ class PipelineEngine:
             labels = targets[i].to(st.device, non_blocking=True) if last else None
             watch = i == self._mon_idx
             obs = st.output_observer() if watch else None
+            if self._audit_now and not first:
+                # every received input stays referenced until the audit (no copy): it is the previous
+                # stage's output as seen here (audited here) and my input (the next stage audits me)
+                self._audit_inputs[i] = x.detach()
             y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1 and not defer_w)
             if last:
                 y = y / M
@@ -901,6 +930,11 @@ class PipelineEngine:
             if self.cfg.param_integrity:
                 d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].copy_(self._integrity_flag(st))
             rows.append((node, d))
+        if getattr(self, "_audit_now", False):
+            ta = self.tracer.begin("audit")
+            progress.mark(f"step {self.global_step}: recompute audit")
+            self._audit(dict(rows))
+            self.tracer.end(ta)
         if self.distributed:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
             if self.heartbeat is not None:
@@ -970,7 +1004,11 @@ class PipelineEngine:
         if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
             self._audit_params()
         # queue the host report (pinned, non-blocking)
-        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float(), blame.float()])
+        if getattr(self, "_audit_now", False):
+            abad, adone = self._audit_vectors(D)
+        else:
+            abad = adone = torch.zeros(N, dtype=torch.float32, device=self.device)
+        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float(), blame.float(), abad, adone])
         if rep.is_cuda:
             host = torch.empty(rep.shape, dtype=rep.dtype, pin_memory=True)
             host.copy_(rep, non_blocking=True)
@@ -979,6 +1017,141 @@ class PipelineEngine:
         else:
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
+
+    # ================================================================== deterministic stage cross-check
+    @torch.no_grad()
+    def _recompute(self, st: Stage, x: torch.Tensor) -> torch.Tensor:
+        """``st``'s forward of one micro-batch, as in training (BatchNorm in batch-statistics mode),
+        without leaving a trace: module buffers (running statistics) are restored afterwards."""
+        bufs = [b.detach().clone() for b in st.module.buffers()]
+        try:
+            y, _ = st.forward(x, None)
+        finally:
+            for b, v in zip(st.module.buffers(), bufs):
+                b.copy_(v)
+        return y
+
+    def _audit_verdict(self, y_seen: torch.Tensor, y_ref: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(mismatch flag, relative max error) of a received output against its recomputation —
+        device tensors, no host sync.  Non-finite values count as a mismatch."""
+        a, b = y_seen.float(), y_ref.float()
+        err = (a - b).abs().amax() / b.abs().amax().clamp_min(1e-12)
+        err = torch.nan_to_num(err, nan=1e30, posinf=1e30)
+        return (err > self.cfg.audit_tol).float().reshape(1), err.reshape(1)
+
+    def _audit(self, rows: Dict[int, torch.Tensor]):
+        """Recompute audit of every non-loss stage's monitored micro-batch (the private-RNG choice
+        of ``_mon_idx``): the output the next stage received must equal f(input; weights).
+
+        Local mode: the engine holds every stage, the verdict on stage p is computed right here.
+        Distributed: each stage sends its weights (bf16 compute copy) and its input for that
+        micro-batch to the next stage, which rebuilds the previous stage's layers once per plan (a
+        mirror on its own GPU), recomputes and compares with what it received; stage 0's input is
+        the token batch every rank has.  The verdict on stage p rides in its auditor's digest row
+        (``D_AUDIT_PREV``), so no collective is added.  A tampered activation (Byzantine output)
+        mismatches deterministically; a weight perturbation recomputes consistently but fails the
+        weight-integrity checksum; a clean stage always matches."""
+        order = [n for n in self.plan.ranks]
+        if not self.distributed:
+            for k in range(1, len(order)):
+                p, aud = order[k - 1], order[k]
+                rec = self._audit_rec.get(p)
+                if rec is None or rec[1] is None or aud not in rows:
+                    continue
+                st = self.stages[p]
+                y_ref = self._recompute(st, rec[0])
+                flag, err = self._audit_verdict(rec[1], y_ref)
+                d = rows[aud]
+                d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag.to(d.device))
+                d[SV.D_AUDITED_PREV] = 1.0
+                d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err.to(d.device))
+            return
+        st = self.my_stage()
+        if st is None:
+            return
+        s = st.stage_id
+        prev, nxt = self.comm.prev, self.comm.next
+        group = self._dir_groups[0] if self.p2p_mode == "async" else None
+        M = len(self._audit_batch)
+        if not hasattr(self, "_audit_rng"):
+            seed = self.cfg.monitor_seed
+            self._audit_rng = __import__("random").Random(
+                int.from_bytes(os.urandom(8), "little") if seed is None else seed * 7919 + self.rank)
+        # round 1: the auditor names the micro-batch (its private choice) to the previous stage,
+        # which answers with that input's shape
+        req_in = torch.zeros(8, dtype=torch.int64, device=self.device)    # from the next stage: [m]
+        req_out = torch.zeros(8, dtype=torch.int64, device=self.device)   # to the previous stage
+        shp_out = torch.zeros(8, dtype=torch.int64, device=self.device)   # my input's shape, to the next stage
+        shp_in = torch.zeros(8, dtype=torch.int64, device=self.device)
+        m_mine = self._audit_rng.randrange(M)
+        req_out[0] = m_mine
+        sends, recvs = [], []
+        if prev is not None:
+            sends.append((req_out, prev))
+        if nxt is not None:
+            recvs.append((req_in, nxt))
+        self._note_peers(sends, recvs, "dir" if group is not None else "default")
+        batched_transfer(sends, recvs, group=group)
+        sends, recvs = [], []
+        if nxt is not None:                      # I am audited by the next stage
+            if s > 0:
+                shp = list(self._audit_inputs[int(req_in[0].item())].shape)
+                shp_out[0] = len(shp)
+                shp_out[1:1 + len(shp)] = torch.tensor(shp, dtype=torch.int64)
+            sends.append((shp_out, nxt))
+        if prev is not None:
+            recvs.append((shp_in, prev))
+        # (the shape answer travels in its own small exchange: the auditee learns m only now)
+        self._note_peers(sends, recvs, "dir" if group is not None else "default")
+        batched_transfer(sends, recvs, group=group)
+        # round 2: weights (bf16 compute copy) and the requested input
+        sends, recvs = [], []
+        if nxt is not None:
+            sends.append((st.flat.data, nxt))
+            if s > 0:
+                sends.append((self._audit_inputs[int(req_in[0].item())].contiguous(), nxt))
+        mirror, x_prev = None, None
+        if prev is not None:                     # I audit the previous stage
+            mirror = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
+            recvs.append((mirror.flat.data, prev))
+            if s - 1 > 0:
+                shape = torch.Size([int(v) for v in shp_in[1:1 + int(shp_in[0].item())].tolist()])
+                x_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
+                recvs.append((x_prev, prev))
+        self._note_peers(sends, recvs, "dir" if group is not None else "default")
+        batched_transfer(sends, recvs, group=group)
+        if mirror is not None:
+            if x_prev is None:
+                x_prev = self._stage_input(self._audit_batch[m_mine], mirror)
+            y_ref = self._recompute(mirror, x_prev)
+            flag, err = self._audit_verdict(self._audit_inputs[m_mine], y_ref)
+            d = rows[self.rank]
+            d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag)
+            d[SV.D_AUDITED_PREV] = 1.0
+            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err)
+        self._audit_inputs = {}
+
+    def _audit_mirror(self, rng: Tuple[int, int], sid: int) -> Stage:
+        """The previous stage's layers on this GPU (weights overwritten by every audit)."""
+        key = (self.plan.version, rng)
+        if getattr(self, "_mirror_key", None) != key:
+            self._mirror = Stage(self.model, rng, sid, self.plan.num_stages, self.device, self.dtype,
+                                 {"output_detection": False, "gradient_verification": False,
+                                  "serialize_streams": True})
+            self._mirror.remove_hooks()
+            self._mirror_key = key
+        return self._mirror
+
+    def _audit_vectors(self, D: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Per-node (audit mismatch, audited) from the digest: a stage's verdict sits in the row of
+        the next stage of its pipeline replica."""
+        bad = torch.zeros(D.shape[0], dtype=torch.float32, device=D.device)
+        done = torch.zeros_like(bad)
+        for idx in self._replica_orders():
+            if idx.numel() > 1:
+                bad[idx[:-1]] = D[idx[1:], SV.D_AUDIT_PREV]
+                done[idx[:-1]] = D[idx[1:], SV.D_AUDITED_PREV]
+        return bad, done
 
     # ================================================================== integrity + attribution
     @torch.no_grad()
@@ -1015,11 +1188,23 @@ class PipelineEngine:
         blame = torch.zeros_like(of)
         evidence = torch.zeros_like(of)
         self.t_taint.copy_(torch.maximum(self.t_taint, (pf > 0).float()))
+        audited = getattr(self, "_audit_now", False)
+        if audited:
+            abad, _ = self._audit_vectors(D)
         for r, idx in enumerate(self._replica_orders()):
             o, g, p = of[idx], gf[idx], pf[idx]
             taint = self.t_taint[idx]
             ev = torch.maximum(o.max(), p.max())
-            if self.cfg.attribute_flags:
+            if audited:
+                # deterministic attribution: a tampered forward is blamed only on a recompute
+                # mismatch (its own stage, never the downstream echoes) or a failed weight-integrity
+                # check; output z-scores do not blame.  Gradient anomalies count only in a replica
+                # without such evidence (gradient poisoning does not propagate, tampering does)
+                a = abad[idx]
+                ev = torch.maximum(p.max(), a.max())
+                b = torch.maximum(torch.maximum(p, a), g * (1.0 - ev))
+                o = a   # "forward anomaly" below = a recompute mismatch
+            elif self.cfg.attribute_flags:
                 # earliest anomalous stage; a stage with tampered (integrity-failed, not yet
                 # restored) weights counts as anomalous, so the output echoes it causes downstream
                 # are neither blamed nor skip the step (its own flag already compromised it)
@@ -1220,7 +1405,8 @@ class PipelineEngine:
         D = host[: N * SV.DIGEST].view(N, SV.DIGEST).tolist()
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
         statuses = [int(v) for v in host[N * SV.DIGEST + N:N * SV.DIGEST + 2 * N].tolist()]
-        blamed = [v > 0 for v in host[N * SV.DIGEST + 2 * N:].tolist()]
+        blamed = [v > 0 for v in host[N * SV.DIGEST + 2 * N:N * SV.DIGEST + 3 * N].tolist()]
+        audit_bad = [v > 0 for v in host[N * SV.DIGEST + 3 * N:N * SV.DIGEST + 4 * N].tolist()]
         present = set(self.all_ranks())
         lasts = [n for n in self.last_ranks() if D[n][SV.D_PRESENT] > 0]
         self.last_loss = sum(D[n][SV.D_LOSS] for n in lasts) / len(lasts) if lasts else None
@@ -1234,7 +1420,8 @@ class PipelineEngine:
             param_flag = row[SV.D_PARAM_FLAG] > 0
             flagged = blamed[n]
             if flagged:
-                kind = "model_poisoning" if param_flag else ("output_anomaly" if out_flag else "gradient_poisoning")
+                kind = "model_poisoning" if param_flag else ("output_tampering" if audit_bad[n] else (
+                    "output_anomaly" if out_flag and not self.cfg.audit else "gradient_poisoning"))
                 rec = {"node_id": n, "timestamp": time.time(), "step": step, "attack_type": kind,
                        "output_stats": {"mean": row[SV.D_OUT_MEAN], "std": row[SV.D_OUT_STD],
                                         "z": row[SV.D_OUT_Z]},
@@ -1250,7 +1437,8 @@ class PipelineEngine:
                 ds = self.detector.detection_stats
                 if flagged:
                     ds["total_detections"] += 1
-                    k = "model_poisoning" if param_flag else ("byzantine" if out_flag else "gradient_poisoning")
+                    k = "model_poisoning" if param_flag else ("byzantine" if audit_bad[n] or (out_flag and not self.cfg.audit)
+                                                              else "gradient_poisoning")
                     ds["attack_types"][k] = ds["attack_types"].get(k, 0) + 1
                 key = ("true_positives" if gt else "false_positives") if flagged else \
                       ("false_negatives" if gt else "true_negatives")

@@ -30,7 +30,11 @@ D_GRAD_SUMSQ, D_OUT_MEAN, D_OUT_STD, D_GRAD_L2, D_NONFINITE, D_GRAD_COS = 11, 12
 D_ATTACK_TRUTH, D_PRESENT, D_STAGE, D_OUT_CONF, D_GRAD_CONF = 17, 18, 19, 20, 21
 D_OFFLINE_MASK = 22  # bitmask of the peers this rank's heartbeat watchdog sees offline
 D_PARAM_FLAG = 23    # compute weights changed outside the optimizer (integrity checksum mismatch)
-DIGEST = 24
+D_AUDIT_PREV = 24    # recompute audit of the PREVIOUS stage's monitored micro-batch: 1 = its output did
+                     # not match f(input; weights) recomputed here (parallel/pipeline.py _audit)
+D_AUDITED_PREV = 25  # 1 when that audit ran this step
+D_AUDIT_ERR = 26     # its relative max error
+DIGEST = 27
 
 
 class StageVerifier:
