@@ -42,15 +42,20 @@ CONFIGS = {
 }
 
 
-def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, seq_len: int, p_attack: float,
-        small: bool = False, warmup: int = 50):
+CONFIGS["clean"] = dict(model="gpt2-medium", attack=None, targets=[], lr=1e-4)
+
+
+def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_len: int, p_attack: float,
+        small: bool = False, warmup: int = 50, seed: int = 3, reassign: bool = True, audit: bool = True):
     c = dict(CONFIGS[cfg_id])
     batch, mbs = c.get("batch", batch), c.get("mbs", mbs)
     if small:   # CPU smoke: same flow on the tiny models
         c["model"] = {"gpt2-medium": "gpt2-tiny", "resnet50": "resnet32"}[c["model"]]
-    att = AdversarialAttacker(AttackConfig(target_nodes=c["targets"], start_step=start, probability=p_attack, seed=3,
-                                           **c["attack"]))
-    att.activate_attacks()
+    att = None
+    if c["attack"] is not None:
+        att = AdversarialAttacker(AttackConfig(target_nodes=c["targets"], start_step=start, probability=p_attack,
+                                               seed=seed, **c["attack"]))
+        att.activate_attacks()
     gpt = c["model"].startswith("gpt2")
     img = 32 if c["model"] == "resnet32" else 224
     ncls = 10 if img == 32 else 1000
@@ -59,12 +64,13 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
     extra = {"seq_len": seq_len} if gpt else {}
     cfg = EngineConfig(num_nodes=8, micro_batches=max(1, batch // mbs), device=device,
                        adamw=AdamWConfig(lr=c["lr"], weight_decay=0.01, max_grad_norm=1.0, warmup_steps=20),
-                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=True,
+                       attack_detection=True, gradient_verification=True, quarantine=True, reassign=reassign,
+                       audit=audit,
                        # detector warm-up of 50 clean steps before the attacks start at step 100 (the
                        # reference protocol warms up on 100 clean steps: BASELINE.md); at 20 the
                        # baselines of GPT-2 hidden states caught early-training transients as z ~ 30
                        # output anomalies; the monitored micro-batch RNG is pinned for reproducibility
-                       verifier={"warmup": warmup}, monitor_seed=0, **extra)
+                       verifier={"warmup": warmup}, monitor_seed=seed, **extra)
     eng = PipelineEngine(model, cfg, attacker=att, metrics=MetricsCollector())
     del model
     plan0 = eng.plan.describe()
@@ -77,19 +83,26 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    m = att.detection_metrics()
+    m = att.detection_metrics() if att is not None else {}
     losses = [(r["step"], round(r["loss"], 4)) for r in eng.metrics.batch_metrics if r.get("loss") is not None]
     rs = eng.reassignment_history
-    first_attack = min(att.first_attack_step.values()) if att.first_attack_step else None
+    first_attack = min(att.first_attack_step.values()) if att is not None and att.first_attack_step else None
+    clean_blamed = sorted({r["node_id"] for r in eng.attack_history if not r.get("ground_truth")})
+    compromised = [n for n in range(8) if eng.trust.get_node_status(n).value == "compromised"]
     rec = {
-        "config": cfg_id, "model": c["model"], "attack": c["attack"], "targets": c["targets"],
+        "config": cfg_id, "seed": seed, "reassign": reassign, "audit": audit,
+        "model": c["model"], "attack": c["attack"], "targets": c["targets"],
         "p_attack": p_attack, "attack_start_step": start, "first_attack_step": first_attack, "steps": steps,
         "batch": batch, "micro_batch": mbs, "seq_len": seq_len if gpt else None, "device": device,
         "data": "markov tokens (order 1, branching 4, 8192 ids)" if gpt else "class-conditional synthetic images",
         "lr": c["lr"], "lr_warmup_steps": 20, "detector_warmup": warmup,
         "detection": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in m.items()
                       if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
-        "injections": len(att.injections),
+        "injections": len(att.injections) if att is not None else 0,
+        "clean_nodes_blamed": clean_blamed,
+        "clean_nodes_compromised": [n for n in compromised if n not in c["targets"]],
+        "clean_nodes_resharded": sorted({n for r in rs for n in r["from_nodes"] if n not in c["targets"]}),
+        "ms_per_step": round(1000 * wall / max(1, steps), 2),
         "reshards": [{"step": r["step"], "from_nodes": r["from_nodes"], "to_nodes": r["to_nodes"],
                       "migration_ms": round(1000 * r["migration_time"], 2),
                       "estimated_ms": round(1000 * r["estimated_migration_time"], 2),
@@ -109,7 +122,11 @@ def run(cfg_id: int, device: str, steps: int, start: int, batch: int, mbs: int, 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="3,4,5")
+    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean")
+    ap.add_argument("--seeds", default="3", help="comma list of attacker / monitor seeds")
+    ap.add_argument("--no-reassign", action="store_true", help="detection only: the target keeps its layers, so "
+                    "every injection is scored (a re-shard ends the attack after the first detections)")
+    ap.add_argument("--no-audit", action="store_true")
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--start", type=int, default=100)
@@ -121,16 +138,18 @@ def main():
     ap.add_argument("--small", action="store_true", help="tiny models (CPU smoke of the same flow)")
     ap.add_argument("--detector-warmup", type=int, default=50)
     args = ap.parse_args()
-    for cid in [int(x) for x in args.configs.split(",")]:
-        rec = run(cid, args.device, args.steps, args.start, args.batch, args.mbs, args.seq_len, args.p_attack,
-                  args.small, args.detector_warmup)
-        line = json.dumps(rec)
-        print(line, flush=True)
-        if args.out:
-            with open(args.out, "a") as f:
-                f.write(line + "\n")
-        if args.device.startswith("cuda"):
-            torch.cuda.empty_cache()
+    for cid in [x if x == "clean" else int(x) for x in args.configs.split(",")]:
+        for seed in [int(x) for x in args.seeds.split(",")]:
+            rec = run(cid, args.device, args.steps, args.start, args.batch, args.mbs, args.seq_len, args.p_attack,
+                      args.small, args.detector_warmup, seed=seed, reassign=not args.no_reassign,
+                      audit=not args.no_audit)
+            line = json.dumps(rec)
+            print(line, flush=True)
+            if args.out:
+                with open(args.out, "a") as f:
+                    f.write(line + "\n")
+            if args.device.startswith("cuda"):
+                torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
