@@ -106,6 +106,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
         "reshards": [{"step": r["step"], "from_nodes": r["from_nodes"], "to_nodes": r["to_nodes"],
                       "migration_ms": round(1000 * r["migration_time"], 2),
                       "estimated_ms": round(1000 * r["estimated_migration_time"], 2),
+                      "phases_ms": {k: round(1000 * v, 2) for k, v in r.get("phases", {}).items() if k.endswith("_s")},
                       "moved_params": r["moved_params"], "restored_from_shadow": r.get("restored_from_shadow"),
                       "plan": r["plan"]} for r in rs],
         "plan_before": plan0, "plan_after": eng.plan.describe(), "num_stages_after": eng.plan.num_stages,

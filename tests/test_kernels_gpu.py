@@ -463,6 +463,38 @@ def test_fused_gpt2_block_matches_fp32(native_gemm, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_fused_gpt2_block_production_shape_matches_fp32():
+    """The benched block shape (GPT-2-medium: width 1024, 16 heads, T = 1024; B = 2) with the
+    default GEMM routing, fused bf16 forward + backward vs the fp32 CPU op-by-op module: output, dx
+    and every parameter's fp32 main_grad."""
+    import copy
+    from trustworthy_dl.models.gpt2 import GPT2Config, GPT2Block
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_embd=1024, n_head=16, n_layer=1)
+    ref = GPT2Block(cfg)
+    for p in ref.parameters():
+        torch.nn.init.normal_(p, std=0.02)
+    ref.fused = False
+    blk = copy.deepcopy(ref).to(DEV).bfloat16()
+    blk.fused = True
+    for p in blk.parameters():
+        p.main_grad = torch.zeros(p.shape, device=DEV)
+    x = torch.randn(2, 1024, 1024)
+    g = torch.randn(2, 1024, 1024)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(g)
+    xd = x.to(DEV).bfloat16().requires_grad_(True)
+    yd = blk(xd)
+    yd.backward(g.to(DEV).bfloat16())
+    assert _rel(yd.float().cpu(), yr.detach()) < 2e-2
+    assert _rel(xd.grad.float().cpu(), xr.grad) < 3e-2
+    for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
+        assert p.grad is None, n
+        assert _rel(p.main_grad.cpu(), q.grad) < 3e-2, n
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,K,N", [(65536, 1024, 3072), (65536, 1024, 1024), (65536, 1024, 4096),
                                    (65536, 4096, 1024), (8192, 1024, 1024), (4096, 1000, 264)])
 def test_wgrad_native_accumulates(M, K, N):

@@ -195,6 +195,7 @@ class PipelineEngine:
         self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
         self._init_trust_state()
         self._build()
+        self._init_build_times = dict(self._build_times)
         self.link_meter = LinkMeter(150e9 if self.device.type == "cuda" else 2e9)
         self.heartbeat = None
         self.node_events: List[Dict] = []
@@ -265,19 +266,76 @@ class PipelineEngine:
         vk.setdefault("early_gate", getattr(self, "_built_once", False))
         return vk
 
-    def _build(self, layer_modules: Optional[Dict[int, List[nn.Module]]] = None):
-        self.stages: Dict[int, Stage] = {}
+    def _build(self, layer_modules: Optional[Dict[int, nn.Module]] = None):
+        """Build this rank's stages of the current plan.  ``layer_modules`` (re-shard): layer index
+        -> a module this rank already holds on a device; those are re-used (re-bound to the new
+        stage's flat buffers), every other layer is deep-copied from the host model and moved to
+        the device.  The two costs are timed separately (``_build_times``): they calibrate the
+        rebuild term of ``estimate_migration_time``."""
+        self._sync_all()
+        t0 = time.perf_counter()
+        built = []
+        fresh = 0
         for sid, (node, rng) in enumerate(zip(self.plan.ranks, self.plan.ranges)):
             if self.distributed and node != self.rank:
                 continue
-            layers = layer_modules.get(node) if layer_modules else None
-            st = Stage(self.model, rng, sid, self.plan.num_stages, self._stage_device(node), self.dtype,
-                       self._verifier_kwargs(), layers=layers)
+            a, b = rng
+            layers = []
+            memo: Dict[int, Any] = {}   # one memo per stage: parameters tied inside it stay shared
+            for li in range(a, b):
+                m = layer_modules.get(li) if layer_modules else None
+                if m is None:
+                    m = copy.deepcopy(self.layers[li], memo)
+                    fresh += self._layer_numel(li)
+                layers.append(m)
+            if layer_modules:
+                self._retie(layers, a, b)
+            dev = self._stage_device(node)
+            layers = [m.to(dev) for m in layers]
+            built.append((sid, node, rng, layers, dev))
+        self._sync_all()
+        t1 = time.perf_counter()
+        self.stages: Dict[int, Stage] = {}
+        total = 0
+        for sid, node, rng, layers, dev in built:
+            st = Stage(self.model, rng, sid, self.plan.num_stages, dev, self.dtype, self._verifier_kwargs(),
+                       layers=layers)
+            total += st.flat.numel
             self.stages[node] = st
         self._set_clip_exclusions()
         self._set_early_stats()
+        self._sync_all()
+        t2 = time.perf_counter()
         self._build_comm()
+        t3 = time.perf_counter()
         self._built_once = True
+        self._build_times = {"materialize_s": t1 - t0, "materialized_params": fresh, "flatten_s": t2 - t1,
+                             "flattened_params": total, "stages": len(built), "groups_s": t3 - t2}
+
+    def _sync_all(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def _retie(self, layers: List[nn.Module], a: int, b: int):
+        """Re-used layer modules may come from different old stages (or share a tied parameter with a
+        layer that now lives on another stage): every tie group's members inside [a, b) get one
+        fresh, stage-private parameter (its value is overwritten by the migrated master weights)."""
+        for grp in self.ties:
+            members = [(li, attr) for li, attr in grp if a <= li < b]
+            if not members:
+                continue
+            src = layers[members[0][0] - a]
+            *path, leaf = members[0][1].split(".")
+            for part in path:
+                src = getattr(src, part)
+            old = getattr(src, leaf)
+            fresh = nn.Parameter(old.detach().clone(), requires_grad=old.requires_grad)
+            for li, attr in members:
+                obj = layers[li - a]
+                *path, leaf = attr.split(".")
+                for part in path:
+                    obj = getattr(obj, part)
+                setattr(obj, leaf, fresh)
 
     def _set_early_stats(self):
         """Per-layer gradient-statistics triggers (verification overlapped with the backward).
@@ -1475,14 +1533,52 @@ class PipelineEngine:
             self._host_metrics[n] = [self._comm_wait, max(0.0, min(1.0, util)), 0.0, 1.0]
 
     # ================================================================== re-sharding (task reassignment)
-    def estimate_migration_time(self, layer_numel: int, links: int = 1) -> float:
-        """Seconds to move ``layer_numel`` parameters' fp32 master + 2 AdamW moments (12 B/param)
-        over ``links`` peer links at the per-link throughput MEASURED on this job's own bulk
-        transfers (shadow snapshots, earlier migrations: ``comm.LinkMeter``); before the first
-        measurement, a prior of one xGMI link (~150 GB/s; gloo: 2 GB/s).  The reference uses a fixed
-        1 GiB/s + 2 s (distributed_trainer.py:354-365)."""
+    def estimate_migration_time(self, layer_numel: int, links: int = 1, plan: Optional[PlacementPlan] = None) -> float:
+        """Predicted wall time of a re-shard that moves ``layer_numel`` parameters to ``plan``.
+
+        transfer: fp32 master + 2 AdamW moments (12 B/param) over ``links`` peer links at the per-link
+        throughput MEASURED on this job's own bulk transfers (shadow snapshots, earlier migrations:
+        ``comm.LinkMeter``; before the first one, a prior of one xGMI link, ~150 GB/s; gloo 2 GB/s);
+        pack + unpack: the rank's share of the packed state, at the device copy rate;
+        rebuild: stage modules, flat buffers and verifiers of the new plan, at the per-parameter
+        rates measured when this engine built its stages (``_build_times``) and refitted from every
+        re-shard's measured phases (``_migrate_phases``);
+        groups: communicator set-up of the new plan (cached groups cost nothing).
+        The reference uses a fixed 1 GiB/s + 2 s (distributed_trainer.py:354-365)."""
         bw = self.link_meter.bytes_per_s() * max(1, links)
-        return layer_numel * 12 / bw + 1e-3
+        cal = self._reshard_calibration()
+        if plan is None:
+            plan = self.plan
+        mine = [li for li in range(self.num_layers) if not self.distributed or plan.owner_of_layer(li) == self.rank]
+        params = sum(self._layer_numel(li) for li in mine)
+        local_bytes = sum(self._packed_numel(li) * 4 for li in mine)
+        fresh = layer_numel if self.distributed else 0   # layers new to a rank are deep-copied there
+        one_device = not self.distributed and len({st.device for st in self.stages.values()}) <= 1
+        xfer = 0.0 if one_device else layer_numel * 12 / bw   # local, one GPU: the state stays in HBM
+        est = (xfer
+               + local_bytes * cal["copy_s_per_byte"]
+               + params * cal["flatten_s_per_param"] + fresh * cal["materialize_s_per_param"]
+               + cal["groups_s"])
+        return est
+
+    def _reshard_calibration(self) -> Dict[str, float]:
+        """Rates behind ``estimate_migration_time``: from the last re-shard's measured phases when
+        there is one, else from this engine's initial build."""
+        ph = getattr(self, "_migrate_phases", None)
+        bt = getattr(self, "_init_build_times", None) or getattr(self, "_build_times", {})
+        flat_rate = bt.get("flatten_s", 0.0) / max(1, bt.get("flattened_params", 1))
+        mat_rate = bt.get("materialize_s", 0.0) / max(1, bt.get("materialized_params", 1))
+        copy_rate = 1.0 / (600e9 if self.device.type == "cuda" else 4e9)   # pack + unpack prior
+        groups = 0.0
+        if ph:
+            if ph.get("local_bytes"):
+                copy_rate = (ph["pack_s"] + ph["unpack_s"]) / ph["local_bytes"]
+            if ph.get("flattened_params"):
+                flat_rate = (ph["rebuild_s"] - ph["materialized_params"] * mat_rate) / ph["flattened_params"]
+                flat_rate = max(flat_rate, 0.0)
+            groups = ph.get("groups_s", 0.0)
+        return {"copy_s_per_byte": copy_rate, "flatten_s_per_param": flat_rate,
+                "materialize_s_per_param": mat_rate, "groups_s": groups}
 
     def reassign(self, compromised: Sequence[int], step: Optional[int] = None):
         """Exclude ``compromised`` nodes and re-partition every layer over the remaining trusted
@@ -1508,8 +1604,12 @@ class PipelineEngine:
             # same all-gathered report, but floats / trust state must not be able to split the job)
             new_plan = PlacementPlan.from_list(broadcast_ints(new_plan.to_list() if self.rank == 0 else None, 0,
                                                               self.device))
-        t0 = time.perf_counter()
         restored = {c: self._shadow_meta[c][0] for c in compromised if self._shadow_usable(c)}
+        to_move = sum(self._layer_numel(li) for li in range(self.num_layers)
+                      if self.plan.owner_of_layer(li) != new_plan.owner_of_layer(li) or
+                      any(self.plan.owner_of_layer(li) == c for c in restored))
+        predicted = self.estimate_migration_time(to_move, plan=new_plan)   # before the move: a prediction
+        t0 = time.perf_counter()
         moved = self._migrate(new_plan, restore=list(restored))
         dt = time.perf_counter() - t0
         self.excluded = sorted(set(self.excluded) | set(compromised))
@@ -1520,7 +1620,8 @@ class PipelineEngine:
                            if self._old_owner.get(li) in compromised})
         rec = {"from_node": compromised[0], "from_nodes": list(compromised), "to_node": to_nodes[0] if to_nodes else None,
                "to_nodes": to_nodes, "timestamp": time.time(), "migration_time": dt,
-               "estimated_migration_time": self.estimate_migration_time(moved),
+               "estimated_migration_time": predicted,
+               "phases": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in self._migrate_phases.items()},
                "moved_params": moved, "step": step if step is not None else self.global_step,
                "restored_from_shadow": restored,
                "plan": new_plan.describe()}
@@ -1569,7 +1670,13 @@ class PipelineEngine:
 
     def _migrate(self, new_plan: PlacementPlan, restore: Sequence[int] = ()) -> int:
         """Move every layer to its new owner.  Layers of the nodes in ``restore`` come from their
-        last committed shadow snapshot (held by a trusted neighbour), not from the node itself."""
+        last committed shadow snapshot (held by a trusted neighbour), not from the node itself.
+
+        Phases (timed into ``self._migrate_phases``, seconds, device-synchronised at each boundary):
+        pack (fp32 master + moments + buffers of every layer leaving or staying, one device vector per
+        layer), transfer (P2P over xGMI; local mode: none, the vectors stay in HBM), rebuild (stage
+        modules re-used where this rank already holds the layer, else deep-copied; flat buffers,
+        verifiers, hooks), groups (communicators of the new plan, cached by member set), unpack."""
         old_plan = self.plan
         self._old_owner = {li: old_plan.owner_of_layer(li) for li in range(self.num_layers)}
         from_shadow: Dict[int, int] = {}     # layer -> holder rank serving it from a shadow
@@ -1580,6 +1687,10 @@ class PipelineEngine:
         step_count = next(iter(self.stages.values())).flat.step_count if self.stages else 0
         packed: Dict[int, torch.Tensor] = {}
         moved = 0
+        ph: Dict[str, float] = {}
+        self._sync_all()
+        t0 = time.perf_counter()
+        xfer_bytes = 0
         if self.distributed:
             sends, recvs = [], []
             for li in range(self.num_layers):
@@ -1593,30 +1704,51 @@ class PipelineEngine:
                         packed[li] = vec
                     else:
                         sends.append((vec, dst))
+                        xfer_bytes += vec.numel() * 4
                 if dst == self.rank and src != self.rank:
                     buf = torch.empty(self._packed_numel(li), dtype=torch.float32, device=self.device)
                     recvs.append((buf, src))
                     packed[li] = buf
                 if src != dst:
                     moved += self._layer_numel(li)
+            self._sync_all()
+            t1 = time.perf_counter()
             self._note_peers(sends, recvs)
             batched_transfer(sends, recvs, meter=self.link_meter)
             step_t = torch.tensor([float(step_count)], device=self.device)
             dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
             step_count = int(step_t.item())
         else:
+            # every stage is local: the packed vectors stay on the device (no host round trip)
             for li in range(self.num_layers):
                 src, dst = old_plan.owner_of_layer(li), new_plan.owner_of_layer(li)
-                packed[li] = (self._shadow_slice(li).cpu() if li in from_shadow
-                              else self._pack_layer(self.stages[src], li).cpu())
+                packed[li] = (self._shadow_slice(li) if li in from_shadow
+                              else self._pack_layer(self.stages[src], li))
                 if src != dst:
                     moved += self._layer_numel(li)
+            self._sync_all()
+            t1 = time.perf_counter()
+        self._sync_all()
+        t2 = time.perf_counter()
+        ph["pack_s"], ph["transfer_s"] = t1 - t0, t2 - t1
         old_verifiers = {n: st.verifier for n, st in self.stages.items()}
         old_ranges = {n: tuple(st.layer_range) for n, st in self.stages.items()}
+        # layer modules this rank already holds (a restored node's layers are rebuilt from the
+        # snapshot's values, so its modules are re-used too: only the values are untrusted)
+        reuse: Dict[int, nn.Module] = {}
         for st in self.stages.values():
             st.remove_hooks()
+            a, _ = st.layer_range
+            for k, m in enumerate(st.module):
+                reuse[a + k] = m
         self.plan = new_plan
-        self._build()
+        self.stages = {}
+        self._build(layer_modules=reuse)
+        del reuse
+        bt = self._build_times
+        ph["rebuild_s"] = bt["materialize_s"] + bt["flatten_s"]
+        ph["groups_s"] = bt["groups_s"]
+        t3 = time.perf_counter()
         for node, st in self.stages.items():
             a, b = st.layer_range
             for li in range(a, b):
@@ -1629,8 +1761,18 @@ class PipelineEngine:
             ov = old_verifiers.get(node)
             if ov is not None and old_ranges.get(node) == tuple(st.layer_range) and ov.S == st.verifier.S:
                 st.verifier.adopt(ov)
+        del packed
+        self._sync_all()
+        ph["unpack_s"] = time.perf_counter() - t3
         self._shape_cache = {}
         self._reset_shadows()                # the snapshot ring follows the plan: re-taken next interval
+        ph["transfer_bytes"] = xfer_bytes
+        ph["local_bytes"] = sum(self._packed_numel(li) * 4 for li in range(self.num_layers)
+                                if not self.distributed or self.plan.owner_of_layer(li) == self.rank)
+        ph["flattened_params"] = bt["flattened_params"]
+        ph["materialized_params"] = bt["materialized_params"]
+        ph["stages"] = bt["stages"]
+        self._migrate_phases = ph
         return moved
 
     # ================================================================== trusted shadow snapshots
