@@ -1562,23 +1562,23 @@ class PipelineEngine:
         return est
 
     def _reshard_calibration(self) -> Dict[str, float]:
-        """Rates behind ``estimate_migration_time``: from the last re-shard's measured phases when
-        there is one, else from this engine's initial build."""
-        ph = getattr(self, "_migrate_phases", None)
+        """Rates behind ``estimate_migration_time``: the median over this engine's initial build and
+        every re-shard measured so far (``_reshard_samples``; a median keeps one slow outlier, e.g.
+        an allocator flush during a rebuild, from skewing the next prediction)."""
         bt = getattr(self, "_init_build_times", None) or getattr(self, "_build_times", {})
-        flat_rate = bt.get("flatten_s", 0.0) / max(1, bt.get("flattened_params", 1))
         mat_rate = bt.get("materialize_s", 0.0) / max(1, bt.get("materialized_params", 1))
-        copy_rate = 1.0 / (600e9 if self.device.type == "cuda" else 4e9)   # pack + unpack prior
-        groups = 0.0
-        if ph:
+        flat = [bt.get("flatten_s", 0.0) / max(1, bt.get("flattened_params", 1))]
+        copy = [1.0 / (600e9 if self.device.type == "cuda" else 4e9)]   # pack + unpack prior
+        groups = [0.0]
+        for ph in getattr(self, "_reshard_samples", []):
             if ph.get("local_bytes"):
-                copy_rate = (ph["pack_s"] + ph["unpack_s"]) / ph["local_bytes"]
+                copy.append((ph["pack_s"] + ph["unpack_s"]) / ph["local_bytes"])
             if ph.get("flattened_params"):
-                flat_rate = (ph["rebuild_s"] - ph["materialized_params"] * mat_rate) / ph["flattened_params"]
-                flat_rate = max(flat_rate, 0.0)
-            groups = ph.get("groups_s", 0.0)
-        return {"copy_s_per_byte": copy_rate, "flatten_s_per_param": flat_rate,
-                "materialize_s_per_param": mat_rate, "groups_s": groups}
+                flat.append(max(0.0, ph["rebuild_s"] - ph["materialized_params"] * mat_rate) / ph["flattened_params"])
+            groups.append(ph.get("groups_s", 0.0))
+        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        return {"copy_s_per_byte": med(copy), "flatten_s_per_param": med(flat),
+                "materialize_s_per_param": mat_rate, "groups_s": med(groups)}
 
     def reassign(self, compromised: Sequence[int], step: Optional[int] = None):
         """Exclude ``compromised`` nodes and re-partition every layer over the remaining trusted
@@ -1773,6 +1773,7 @@ class PipelineEngine:
         ph["materialized_params"] = bt["materialized_params"]
         ph["stages"] = bt["stages"]
         self._migrate_phases = ph
+        self._reshard_samples = getattr(self, "_reshard_samples", []) + [ph]
         return moved
 
     # ================================================================== trusted shadow snapshots
