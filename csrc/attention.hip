@@ -19,6 +19,8 @@
 //          dQ^T += K^T.dS^T with dS^T as the B operand.  +2 recomputed products, zero atomics.
 #include "common.h"
 
+#include <type_traits>
+
 #include <cstdlib>
 #include <cstring>
 
@@ -299,10 +301,43 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 // the LDS (64 KB, still 2 workgroups per CU) but measures slower (see dkdv_ns).
 // Products per 32-row sub-tile and wave: S = Q.K^T, dP = dO.V^T (row-read A, K/V fragments
 // resident in registers), dV^T += dO^T.P and dK^T += Q^T.dS (tr-read A, S/dP accumulators as B).
+// ---- fused qkv-bias gradient (column sums of dqkv over tokens, SURVEY 2.8: no colsum pass over
+// the [tokens, 3 * width] gradient).  Each workgroup reduces the bf16-rounded values it stores over
+// its 128 rows and writes them to its own row of a partial matrix [B * T / 128][3 * H * HD]
+// (every entry written once, fixed order: deterministic); tdl_colsum_f32 reduces the rows.
+// Butterfly over the 32 lanes of a half-wave: at each step a lane keeps one half of its values
+// (by its lane bit) and adds the partner's copy of that half, so N values cost N - N/32 shuffles
+// instead of 5 N.  Afterwards lane r holds the sums of values (N / 32) * r + j, j < N / 32.
+template <int N>
+__device__ __forceinline__ void half_wave_colsum(float (&v)[N], int r) {
+    static_assert(N % 32 == 0, "N multiple of 32");
+    auto step = [&](auto oc) {
+        constexpr int O = decltype(oc)::value, M = N * O / 32;   // values still held: 2 M -> M
+        const bool up = (r & O) != 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            const float send = up ? v[i] : v[i + M];
+            const float keep = up ? v[i + M] : v[i];
+            v[i] = keep + __shfl_xor(send, O, 64);
+        }
+    };
+    step(std::integral_constant<int, 16>{});
+    step(std::integral_constant<int, 8>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 1>{});
+}
+__device__ __forceinline__ float bf16_round(float x) {
+    float a[4] = {x, 0.f, 0.f, 0.f}, b[4];
+    unpack4(pack4(a), b);
+    return b[0];
+}
+
 template <bool CAUSAL, int NS, int PF>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
-                                                            bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
+                                                            bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale,
+                                                            float* __restrict__ bias_part) {
     constexpr int BK = 128, BQ = 32 * NS;
     // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
     // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
@@ -493,6 +528,32 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         float v2[4] = {dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]};
         *(uint2*)(dvrow + 32 + d) = pack4(v2);
     }
+    if (bias_part != nullptr) {
+        // value i = 16 kind + 4 g + e, kind 0/1: dK columns (32 kind + 8 g + 4 h + e), 2/3: dV
+        __shared__ float cs[4][2][64];
+        float v[64];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[4 * g + e] = bf16_round(dk0[4 * g + e] * scale);
+                v[16 + 4 * g + e] = bf16_round(dk1[4 * g + e] * scale);
+                v[32 + 4 * g + e] = bf16_round(dv0[4 * g + e]);
+                v[48 + 4 * g + e] = bf16_round(dv1[4 * g + e]);
+            }
+        half_wave_colsum<64>(v, r);
+        cs[w][h][2 * r] = v[0];
+        cs[w][h][2 * r + 1] = v[1];
+        __syncthreads();
+        if (tid < 128) {
+            const int hh = tid >> 6, i = tid & 63;
+            const float t = cs[0][hh][i] + cs[1][hh][i] + cs[2][hh][i] + cs[3][hh][i];
+            const int kind = i >> 4, g = (i >> 2) & 3, e = i & 3;
+            const int c = 32 * (kind & 1) + 8 * g + 4 * hh + e;
+            const int col = (kind < 2 ? H * HD : 2 * H * HD) + hd * HD + c;
+            bias_part[((size_t)b * (T / BK) + kbi) * (3 * H * HD) + col] = t;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------- dQ (query-owned)
@@ -503,7 +564,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale) {
+                                                          bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale,
+                                                          float* __restrict__ bias_part) {
     constexpr int BM = 128, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Kr[2][BN * HD];  // swizzled, row reads
     __shared__ __attribute__((aligned(16))) bf16_t Kp[2][BN * HD];  // plain, transposed reads
@@ -621,28 +683,61 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         float a2[4] = {dq1[4 * g] * scale, dq1[4 * g + 1] * scale, dq1[4 * g + 2] * scale, dq1[4 * g + 3] * scale};
         *(uint2*)(qrow + 32 + d) = pack4(a2);
     }
+    if (bias_part != nullptr) {
+        // value i = 16 kind + 4 g + e: dQ column 32 kind + 8 g + 4 h + e
+        __shared__ float cs[4][2][32];
+        float v[32];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[4 * g + e] = bf16_round(dq0[4 * g + e] * scale);
+                v[16 + 4 * g + e] = bf16_round(dq1[4 * g + e] * scale);
+            }
+        half_wave_colsum<32>(v, r);
+        cs[w][h][r] = v[0];
+        __syncthreads();
+        if (tid < 64) {
+            const int hh = tid >> 5, i = tid & 31;
+            const float t = cs[0][hh][i] + cs[1][hh][i] + cs[2][hh][i] + cs[3][hh][i];
+            const int kind = i >> 4, g = (i >> 2) & 3, e = i & 3;
+            const int col = hd * HD + 32 * kind + 8 * g + 4 * hh + e;
+            bias_part[((size_t)b * (T / BM) + qb) * (3 * H * HD) + col] = t;
+        }
+    }
 }
 
-TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* unused,
-                         float* delta, int B, int T, int H, int D, float scale, int causal, hipStream_t s) {
-    (void)unused;
+TDL_API int tdl_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s);  // norm_act.hip
+
+// bias_acc (nullable): fp32 [3 H HD] accumulator of the qkv bias gradient (+= column sums of dqkv,
+// computed inside the two kernels); bias_part: workspace of (B T / 128) x 3 H HD floats.
+TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* bias_acc,
+                         float* bias_part, float* delta, int B, int T, int H, int D, float scale, int causal,
+                         hipStream_t s) {
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
+    if ((bias_acc == nullptr) != (bias_part == nullptr)) return (int)hipErrorInvalidValue;
     attn_delta_kernel<<<(unsigned)(((size_t)B * T * H * (HD / 8) + 255) / 256), 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
     const int grid = B * H * (T / 128);
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;
     auto dQKV = (bf16_t*)dqkv;
     const int nb = attn_nbh_arg(B * H);
+    float* bp = bias_part;
     if (causal) {
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<false, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        else attn_bwd_dkdv_kernel<false, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
-        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale);
+        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<false, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else attn_bwd_dkdv_kernel<false, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+    }
+    if (bias_acc != nullptr) {
+        const int rc = (int)hipGetLastError();
+        if (rc) return rc;
+        return tdl_colsum_f32(bias_part, B * (T / 128), 3 * H * HD, 3 * H * HD, bias_acc, s);
     }
     TDL_LAUNCH_CHECK();
 }

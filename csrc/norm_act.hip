@@ -678,6 +678,13 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restri
     }
 }
 
+// acc[n] += sum over g < G of part[g * ld + n] (fp32 partial rows from another kernel)
+TDL_API int tdl_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s) {
+    if (G <= 0 || N <= 0) return (int)hipErrorInvalidValue;
+    launch_colsum_f32(part, G, N, ld, acc, s);
+    TDL_LAUNCH_CHECK();
+}
+
 TDL_API int tdl_colsum_bf16(const void* dy, float* acc, int M, int N, float* part, hipStream_t s) {
     // part: (ceil(M/16) * N) floats of per-block partials, then one short column-sum pass
     if (N % 8) return (int)hipErrorInvalidValue;

@@ -331,13 +331,20 @@ TDL_API int64_t tdl_grad_stats_ws_bytes(int C, int S) {
     return (int64_t)sizeof(Moments) * C + 40ll * C + (int64_t)sizeof(Moments) * S + 16 + 4 * NHIST;
 }
 
-__global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restrict__ g, float* __restrict__ ref,
-                                                           const int64_t* __restrict__ chunks, int c0, int ref_valid,
-                                                           float beta, Moments* __restrict__ part,
-                                                           double* __restrict__ part_seg) {
+// REDUCE = false: the gradient g is final in memory (grad_partial_kernel).
+// REDUCE = true : the chunk's gradient is completed here first — g[i] += sum over the split-K slabs of
+//   a weight-gradient GEMM (slabs: [nsplit][segment numel], element i - seg_off; same fold order as
+//   tdl_splitk_reduce_add, so the stored gradient and every statistic are bit-identical to the
+//   reduce-then-partial sequence) — and the statistics are taken from the registers, so the final
+//   gradient is never re-read (grad_reduce_partial_kernel; ops/gemm.py matmul_f32_acc with a sink).
+template <bool REDUCE>
+__device__ __forceinline__ void grad_partial_body(float* __restrict__ g, float* __restrict__ ref,
+                                                  const int64_t* __restrict__ chunks, int c, int ref_valid, float beta,
+                                                  Moments* __restrict__ part, double* __restrict__ part_seg,
+                                                  const float* __restrict__ slabs, int nsplit, int64_t seg_off,
+                                                  int64_t seg_n) {
     __shared__ Moments sh[16];
     __shared__ float red[16];
-    const int c = c0 + blockIdx.x;
     const int64_t start = chunks[3 * c + 1], end = chunks[3 * c + 2];
     // the EMA reference (cosine feature) is kept on every REF_STRIDE-th chunk only: a 1/8 sample
     // of a stage's parameters estimates the cosine to well within its step-to-step noise at an
@@ -358,12 +365,34 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
         }
         return isfinite(v) ? v : 0.f;
     };
+    auto load1 = [&](int64_t i) -> float {
+        float v = g[i];
+        if constexpr (REDUCE) {
+            for (int s = 0; s < nsplit; ++s) v += slabs[(int64_t)s * seg_n + (i - seg_off)];
+            g[i] = v;
+        }
+        return v;
+    };
+    auto load4 = [&](int64_t i) -> float4 {
+        float4 v = *(const float4*)(g + i);
+        if constexpr (REDUCE) {
+            for (int s = 0; s < nsplit; ++s) {
+                const float4 w = *(const float4*)(slabs + (int64_t)s * seg_n + (i - seg_off));
+                v.x += w.x;
+                v.y += w.y;
+                v.z += w.z;
+                v.w += w.w;
+            }
+            *(float4*)(g + i) = v;
+        }
+        return v;
+    };
     // 16-byte vector body over the 4-aligned part of the chunk, scalar head / tail
     int64_t vbeg = (start + 3) & ~(int64_t)3;
     if (vbeg > end) vbeg = end;
     const int64_t vend = vbeg + ((end - vbeg) & ~(int64_t)3);
     for (int64_t i = start + threadIdx.x; i < vbeg; i += blockDim.x) {
-        const float nr = proc(g[i], ref ? ref[i] : 0.f);
+        const float nr = proc(load1(i), ref ? ref[i] : 0.f);
         if (ref) ref[i] = nr;
     }
     // main body: 4 float4 per lane per trip, every load issued before any math (a layer's chunks
@@ -373,7 +402,7 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
     for (; i + 3 * step < vend; i += 4 * step) {
         float4 v[4], r[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *(const float4*)(g + i + u * step);
+        for (int u = 0; u < 4; ++u) v[u] = load4(i + u * step);
         if (ref) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) r[u] = *(const float4*)(ref + i + u * step);
@@ -392,7 +421,7 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
         }
     }
     for (; i < vend; i += step) {
-        const float4 v = *(const float4*)(g + i);
+        const float4 v = load4(i);
         const float4 r = ref ? *(const float4*)(ref + i) : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 nr;
         nr.x = proc(v.x, r.x);
@@ -402,7 +431,7 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
         if (ref) *(float4*)(ref + i) = nr;
     }
     for (int64_t i = vend + threadIdx.x; i < end; i += blockDim.x) {
-        const float nr = proc(g[i], ref ? ref[i] : 0.f);
+        const float nr = proc(load1(i), ref ? ref[i] : 0.f);
         if (ref) ref[i] = nr;
     }
     Moments r = block_merge(acc.to_moments(), sh);
@@ -418,6 +447,23 @@ __global__ __launch_bounds__(256) void grad_partial_kernel(const float* __restri
         part_seg[5 * c + 3] = nb;
         part_seg[5 * c + 4] = ref ? sq : 0.0;   // |g|^2 over the reference-tracked chunks
     }
+}
+
+__global__ __launch_bounds__(256) void grad_partial_kernel(float* __restrict__ g, float* __restrict__ ref,
+                                                           const int64_t* __restrict__ chunks, int c0, int ref_valid,
+                                                           float beta, Moments* __restrict__ part,
+                                                           double* __restrict__ part_seg) {
+    grad_partial_body<false>(g, ref, chunks, c0 + blockIdx.x, ref_valid, beta, part, part_seg, nullptr, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void grad_reduce_partial_kernel(float* __restrict__ g, float* __restrict__ ref,
+                                                                  const int64_t* __restrict__ chunks, int c0,
+                                                                  int ref_valid, float beta, Moments* __restrict__ part,
+                                                                  double* __restrict__ part_seg,
+                                                                  const float* __restrict__ slabs, int nsplit,
+                                                                  int64_t seg_off, int64_t seg_n) {
+    grad_partial_body<true>(g, ref, chunks, c0 + blockIdx.x, ref_valid, beta, part, part_seg, slabs, nsplit, seg_off,
+                            seg_n);
 }
 
 // One wave per segment (4 per block): lanes stride over the segment's chunks in a fixed order,
@@ -509,7 +555,21 @@ TDL_API int tdl_grad_stats_partial(const float* g, float* ref, const int64_t* ta
     if (c0 < 0 || c1 > C || c0 > c1) return (int)hipErrorInvalidValue;
     if (c1 == c0) return 0;
     GradWs w = grad_ws(ws, C, S);
-    grad_partial_kernel<<<c1 - c0, 256, 0, s>>>(g, ref, table, c0, ref_valid, beta, w.part, w.part_seg);
+    grad_partial_kernel<<<c1 - c0, 256, 0, s>>>((float*)g, ref, table, c0, ref_valid, beta, w.part, w.part_seg);
+    TDL_LAUNCH_CHECK();
+}
+
+// Split-K reduce of one segment's weight gradient fused with its partial pass: chunks [c0, c1) must
+// be exactly the chunks of the segment starting at flat offset seg_off (seg_n elements), slabs =
+// [nsplit][seg_n] fp32.  g[seg_off ..] += sum of the slabs, statistics from the summed values.
+TDL_API int tdl_grad_stats_reduce_partial(float* g, const float* slabs, int nsplit, long long seg_off, long long seg_n,
+                                          float* ref, const int64_t* table, int C, int S, int c0, int c1, float beta,
+                                          void* ws, int ref_valid, hipStream_t s) {
+    if (c0 < 0 || c1 > C || c0 >= c1 || nsplit < 1) return (int)hipErrorInvalidValue;
+    if ((seg_off & 3) || (seg_n & 3) || ((uintptr_t)g & 15) || ((uintptr_t)slabs & 15)) return (int)hipErrorInvalidValue;
+    GradWs w = grad_ws(ws, C, S);
+    grad_reduce_partial_kernel<<<c1 - c0, 256, 0, s>>>(g, ref, table, c0, ref_valid, beta, w.part, w.part_seg, slabs,
+                                                       nsplit, seg_off, seg_n);
     TDL_LAUNCH_CHECK();
 }
 

@@ -90,3 +90,34 @@ def test_early_grad_stats_actually_split():
     eng.train_step(_batches(1, seed=5)[0])
     eng.flush()
     assert all(len(p) >= 2 for p in counts), counts
+
+
+def _run_big(monkeypatch, fused: str, steps=3):
+    """32 x 128-token micro-batch (4096 tokens) through the fused blocks (width 256): the weight
+    gradients run split-K with slabs."""
+    monkeypatch.setenv("TDL_FUSED_GRAD_STATS", fused)
+    m = get_model("gpt2-mini", seq_len=128, seed=0, vocab_size=1024)
+    cfg = EngineConfig(num_nodes=1, micro_batches=1, seq_len=128, device="cuda:0", adamw=AdamWConfig(lr=1e-3),
+                       reassign=False, early_grad_stats=True, output_check="first", monitor_seed=1)
+    eng = PipelineEngine(m, cfg, TrustManager(1))
+    st = next(iter(eng.stages.values()))
+    gs = st.verifier.grad_stats
+    calls = []
+    orig = gs.reduce_partial
+    gs.reduce_partial = lambda *a, orig=orig, calls=calls: (calls.append(a[1]), orig(*a))[1]
+    for b in _batches(steps, bs=32, T=128):
+        eng.train_step(b)
+    eng.flush()
+    torch.cuda.synchronize()
+    return eng.last_loss, st.verifier.digest.detach().clone(), st.flat.master.detach().clone(), calls
+
+
+def test_fused_wgrad_reduce_stats_bit_identical(monkeypatch):
+    """The verifier's partial pass fused into the weight-gradient split-K reduce (the final gradient
+    is never re-read) gives bit-identical digests and weights to the reduce + side-stream pass."""
+    l1, d1, w1, calls1 = _run_big(monkeypatch, "1")
+    l0, d0, w0, calls0 = _run_big(monkeypatch, "0")
+    assert calls0 == [] and len(calls1) >= 3 * 4 * 4, calls1      # every block weight, every step
+    assert l0 == l1
+    assert torch.equal(d0, d1), (d0 - d1).abs().max()
+    assert torch.equal(w0, w1), (w0 - w1).abs().max()

@@ -121,6 +121,27 @@ def test_flash_attention_production_shape():
         assert fro(gq[:, :, i], gr[:, :, i]) < 2e-2, name
 
 
+@pytest.mark.parametrize("B,T,H", [(2, 256, 4), (4, 1024, 16)])
+def test_attention_bwd_fused_bias_grad(B, T, H):
+    """The qkv bias gradient accumulated inside the attention backward kernels equals the fp64
+    column sums of the bf16 gradient they return (every column, both causal and full)."""
+    from trustworthy_dl.ops.layers import attn_bwd, attn_fwd
+    torch.manual_seed(2)
+    D = 64
+    for causal in (True, False):
+        qkv = torch.randn(B, T, 3 * H * D, device=DEV).bfloat16()
+        out, lse, scale = attn_fwd(qkv, H, causal)
+        dout = torch.randn_like(out)
+        acc = torch.randn(3 * H * D, device=DEV)
+        acc0 = acc.clone()
+        dq = attn_bwd(qkv, out, lse, dout, H, causal, scale, bias_acc=acc)
+        dq_plain = attn_bwd(qkv, out, lse, dout, H, causal, scale)
+        assert torch.equal(dq, dq_plain)
+        ref = acc0.double() + dq.double().reshape(-1, 3 * H * D).sum(0)
+        err = float((acc.double() - ref).abs().max() / ref.abs().max())
+        assert err < 1e-5, (causal, err)
+
+
 def test_attention_rescale_branch():
     """Force the online-softmax running max to jump inside a row (rule 26)."""
     from trustworthy_dl.ops import causal_attention

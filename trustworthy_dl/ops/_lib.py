@@ -82,6 +82,7 @@ _SIGNATURES = {
     "tdl_embedding_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "tdl_embedding_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "tdl_add_into_f32": [_P, _P, _L, _I, _P],
+    "tdl_colsum_f32": [_P, _I, _I, _I, _P, _P],
     "tdl_colsum_bf16": [_P, _P, _I, _I, _P, _P],
     "tdl_transpose_bf16": [_P, _P, _I, _I, _P],
     # xent.hip
@@ -98,6 +99,7 @@ _SIGNATURES = {
     "tdl_grad_stats": [_P, _P, _P, _I, _P, _L, _F, _I, _P, _I, _I, _P],
     "tdl_grad_stats_ws_bytes": [_I, _I],
     "tdl_grad_stats_partial": [_P, _P, _P, _I, _I, _I, _I, _F, _P, _I, _P],
+    "tdl_grad_stats_reduce_partial": [_P, _P, _I, _L, _L, _P, _P, _I, _I, _I, _I, _F, _P, _I, _P],
     "tdl_grad_stats_final": [_P, _P, _I, _P, _L, _I, _P, _I, _I, _P],
     "tdl_grad_sumsq": [_P, _P, _I, _P, _P, _P, _P],
     "tdl_gram_ws_bytes": [],
@@ -111,7 +113,7 @@ _SIGNATURES = {
     "tdl_attack_inject": [_P, _I, _L, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P],
     # attention.hip
     "tdl_attn_fwd": [_P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
-    "tdl_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
+    "tdl_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
     # gemm.hip
     "tdl_gemm": [_P] * 6 + [_I] * 10 + [_L, _P],
     # conv.hip / bn.hip

@@ -39,7 +39,7 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import ptr, stream_ptr
 from .layers import (_f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, bump_weight_generation,  # noqa: F401
-                     fwd_weight, run_or_defer, wgrad_acc)
+                     fwd_weight, run_or_defer, take_stats_sink, wgrad_acc)
 
 _FUSED_WIDTHS = (256, 512, 768, 1024, 1280, 1536, 2048)
 
@@ -224,7 +224,8 @@ class _GPT2BlockFn(torch.autograd.Function):
         # them behind the input-gradient send (layers.defer_weight_grads); run inline otherwise
         wdefer = run_or_defer if all(_wants_main_grad(p) for p in (w_qkv, b_qkv, w_o, w_fc, w_p)) else (lambda fn: fn())
         # MLP branch
-        wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2))
+        sk = {id(g): take_stats_sink(g) for g in (g_wp, g_wfc, g_wo, g_wqkv)}   # verifier's fused reduces
+        wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2, sink=sk[id(g_wp)]))
         if ctx.fused_mlp and _native_mlp(dy2, w_p.t(), b_fc):
             from . import gemm   # dpre = (dy @ Wp^T) * gelu'(pre), bfc grad as column sums
             dpre = gemm.matmul(dy2, w_p.t(), epi="dgelu", aux=pre, colsum=g_bfc)
@@ -235,22 +236,23 @@ class _GPT2BlockFn(torch.autograd.Function):
             else:
                 dpre = _bias_gelu_bwd(df, pre, b_fc, g_bfc)
             del df
-        wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre))
+        wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre, sink=sk[id(g_wfc)]))
         dh2 = _mm(dpre, w_fc.t())
         del dpre
         # dy1 = dy + LN2_bwd(dh2); bp grad = colsum(dy), bo grad = colsum(dy1) from the same pass
         dy1 = _ln_bwd(dh2, y1, ln2_w, mean2, rstd2, g_ln2w, g_ln2b, dres=dy2, sres_acc=g_bp, sdx_acc=g_bo)
         del dh2
         # attention branch
-        wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1))
+        wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1, sink=sk[id(g_wo)]))
         do = _mm(dy1, w_o.t())
-        dqkv = attn_bwd(qkv.view(B, T, 3 * C), o2.view(B, T, C), lse, do.view(B, T, C), H, True, scale)
+        # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
+        dqkv = attn_bwd(qkv.view(B, T, 3 * C), o2.view(B, T, C), lse, do.view(B, T, C), H, True, scale,
+                        bias_acc=g_bqkv)
         del do
         dqkv2 = dqkv.view(B * T, 3 * C)
 
         def _qkv_grads(dqkv2=dqkv2):
-            _colsum_into(g_bqkv, dqkv2)
-            wgrad_acc(g_wqkv, h1.t(), dqkv2)
+            wgrad_acc(g_wqkv, h1.t(), dqkv2, sink=sk[id(g_wqkv)])
         wdefer(_qkv_grads)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -127,10 +127,11 @@ def wgrad_split(K: int, M: int, N: int, num_cu: Optional[int] = None) -> int:
 
 
 def matmul_f32_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, split: Optional[int] = None,
-                   mode: Optional[str] = None, kernel: Optional[str] = None) -> torch.Tensor:
+                   mode: Optional[str] = None, kernel: Optional[str] = None, sink=None) -> torch.Tensor:
     """``acc (fp32) += a @ b``.  With a split reduction the partial products go to fp32 slabs
     reduced by one native pass (``mode='slab'``, default) or straight into ``acc`` with fp32
-    atomics (``mode='atomic'``)."""
+    atomics (``mode='atomic'``).  ``sink(slabs, S) -> bool`` (the gradient verifier's fused
+    reduce: this is the parameter's last accumulation of the step) may take over the slab reduce."""
     M, K = a.shape
     N = b.shape[1]
     if acc.dtype != torch.float32 or tuple(acc.shape) != (M, N) or not acc.is_contiguous():
@@ -147,6 +148,8 @@ def matmul_f32_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, split: O
         return acc
     slabs = torch.empty(S, M, N, dtype=torch.float32, device=acc.device)
     _launch(a, b, slabs, N, "f32", split=S, split_stride=M * N, kernel=kernel)
+    if sink is not None and sink(slabs, S):
+        return acc
     _lib.call("tdl_splitk_reduce_add", ptr(acc), ptr(slabs), S, acc.numel(), stream_ptr(acc.device))
     return acc
 

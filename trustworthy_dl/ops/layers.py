@@ -199,7 +199,17 @@ def _bias_grad_into(bias: torch.Tensor, dy2: torch.Tensor):
     return _accumulate(bias, dy2.float().sum(0))
 
 
-def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+def take_stats_sink(acc: torch.Tensor):
+    """The gradient verifier's fused-reduce hook armed on ``acc`` (a ``main_grad``) for this step's
+    last accumulation, removed so it is used at most once.  Taken when the backward op runs (not
+    when a deferred weight-gradient closure runs): backward order is micro-batch order."""
+    sink = getattr(acc, "_tdl_stats_sink", None)
+    if sink is not None:
+        acc._tdl_stats_sink = None
+    return sink
+
+
+def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, sink=None):
     """acc (fp32, shape of a @ b) += a @ b.
 
     ``a`` is usually X^T (a transposed view of a row-major [M, K] activation) and ``b`` dY: on the
@@ -212,7 +222,7 @@ def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
         return
     from . import gemm
     if acc.dtype == torch.float32 and acc.is_contiguous() and acc.dim() == 2 and gemm.supported(a, b):
-        gemm.matmul_f32_acc(acc, a, b)
+        gemm.matmul_f32_acc(acc, a, b, sink=sink)
         return
     # shapes the native kernel does not take (K % 64, unaligned rows): one library GEMM, fp32 out
     acc.add_(torch.mm(a, b, out_dtype=torch.float32).view(acc.shape))
@@ -321,8 +331,11 @@ def attn_fwd(qkv: torch.Tensor, n_head: int, causal: bool):
     return out, lse, scale
 
 
-def attn_bwd(qkv, out, lse, dout, n_head: int, causal: bool, scale: float) -> torch.Tensor:
-    """Gradient w.r.t. the packed qkv (same layout as ``qkv``)."""
+def attn_bwd(qkv, out, lse, dout, n_head: int, causal: bool, scale: float,
+             bias_acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Gradient w.r.t. the packed qkv (same layout as ``qkv``).  ``bias_acc`` (fp32 [3 H D]): the
+    qkv bias gradient (column sums of the returned gradient) is accumulated into it — on the GPU
+    from inside the two backward kernels (no pass over the [tokens, 3 H D] gradient)."""
     B, T, C3 = qkv.shape
     H = n_head
     D = C3 // (3 * H)
@@ -330,8 +343,11 @@ def attn_bwd(qkv, out, lse, dout, n_head: int, causal: bool, scale: float) -> to
     if qkv.is_cuda:
         dqkv = torch.empty_like(qkv)
         delta = torch.empty(B * H, T, dtype=torch.float32, device=qkv.device)
-        _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), None, ptr(delta),
-                  B, T, H, D, scale, int(causal), stream_ptr(qkv.device))
+        part = None
+        if bias_acc is not None:
+            part = _scratch(B * (T // 128) * 3 * H * D, qkv.device)
+        _lib.call("tdl_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(dqkv), ptr(bias_acc), ptr(part),
+                  ptr(delta), B, T, H, D, scale, int(causal), stream_ptr(qkv.device))
         return dqkv
     with torch.enable_grad():
         x = qkv.detach().float().requires_grad_(True)
@@ -341,7 +357,10 @@ def attn_bwd(qkv, out, lse, dout, n_head: int, causal: bool, scale: float) -> to
             att = att.masked_fill(torch.ones(T, T, dtype=torch.bool).triu(1), float("-inf"))
         o = (torch.softmax(att, -1) @ v).transpose(1, 2).reshape(B, T, H * D)
         (g,) = torch.autograd.grad(o, x, dout.reshape(o.shape).float())
-    return g.to(qkv.dtype)
+    g = g.to(qkv.dtype)
+    if bias_acc is not None:
+        bias_acc.add_(g.float().reshape(-1, C3).sum(0))
+    return g
 
 
 class _Attention(torch.autograd.Function):

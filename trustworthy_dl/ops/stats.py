@@ -110,6 +110,10 @@ class FlatGradStats:
             self.seg_first.append(self.seg_first[-1] + (n + CHUNK - 1) // CHUNK)
         self._done = 0               # chunks whose partial already ran this step (prefix-free count)
         self._ranges: List[Tuple[int, int]] = []
+        self.fused_segs = set()      # segments whose partial ran inside their weight-gradient reduce
+        self._offs = [0]
+        for n in self.sizes:
+            self._offs.append(self._offs[-1] + n)
         if self.device.type == "cuda":
             self.table, self.C = build_chunk_table(self.sizes, self.device)
             nbytes = int(_lib.lib().tdl_grad_stats_ws_bytes(self.C, self.S)) + 64
@@ -129,6 +133,25 @@ class FlatGradStats:
                   stream.cuda_stream if stream is not None else stream_ptr(flat_grad.device))
         self._ranges.append((c0, c1))
         self._done += c1 - c0
+
+    def reduce_partial(self, flat_grad: torch.Tensor, seg: int, slabs: torch.Tensor, nsplit: int) -> bool:
+        """Complete segment ``seg``'s gradient from split-K slabs ([nsplit][numel] fp32; the
+        weight-gradient GEMM's partial products) AND run its chunks' partial pass in the same
+        kernel, on the current stream: the final gradient is never re-read.  Bit-identical to
+        ``tdl_splitk_reduce_add`` followed by ``partial``.  False when the segment's offset / size
+        are not 16-byte multiples (the caller then reduces the plain way)."""
+        off = sum(self.sizes[:seg]) if not hasattr(self, "_offs") else self._offs[seg]
+        n = self.sizes[seg]
+        c0, c1 = self.seg_first[seg], self.seg_first[seg + 1]
+        if off % 4 or n % 4 or c1 <= c0 or not flat_grad.is_cuda:
+            return False
+        _lib.call("tdl_grad_stats_reduce_partial", ptr(flat_grad), ptr(slabs), int(nsplit), int(off), int(n),
+                  ptr(self.ref), ptr(self.table), self.C, self.S, c0, c1, self.ref_beta, ptr(self.ws),
+                  int(self.ref_valid), stream_ptr(flat_grad.device))
+        self._ranges.append((c0, c1))
+        self._done += c1 - c0
+        self.fused_segs.add(seg)
+        return True
 
     def compute(self, flat_grad: torch.Tensor, with_quantiles: bool = True) -> torch.Tensor:
         """Returns the device vector [18 + 2S]: GRAD_STATS(17), nonfinite, norms[S], cos[S]."""
@@ -154,6 +177,7 @@ class FlatGradStats:
             self.out.copy_(self._cpu(flat_grad))
         self._done = 0
         self._ranges = []
+        self.fused_segs = set()
         if self.ref is not None:
             self.ref_valid = True
         return self.out

@@ -1135,45 +1135,36 @@ class PipelineEngine:
             seed = self.cfg.monitor_seed
             self._audit_rng = __import__("random").Random(
                 int.from_bytes(os.urandom(8), "little") if seed is None else seed * 7919 + self.rank)
-        # round 1: the auditor names the micro-batch (its private choice) to the previous stage,
-        # which answers with that input's shape
-        req_in = torch.zeros(8, dtype=torch.int64, device=self.device)    # from the next stage: [m]
-        req_out = torch.zeros(8, dtype=torch.int64, device=self.device)   # to the previous stage
-        shp_out = torch.zeros(8, dtype=torch.int64, device=self.device)   # my input's shape, to the next stage
-        shp_in = torch.zeros(8, dtype=torch.int64, device=self.device)
+        # The auditor's private choice of micro-batch and the auditee's input shape travel host to
+        # host through the c10d store (no device sync, no GPU collective): every output of this
+        # step already reached the auditor before it reveals its choice, so the auditee cannot
+        # tailor what it sent to it.
+        store = dist.distributed_c10d._get_default_store()
+        tag = f"tdl_audit/{self.plan.version}/{self.global_step}"
         m_mine = self._audit_rng.randrange(M)
-        req_out[0] = m_mine
-        sends, recvs = [], []
         if prev is not None:
-            sends.append((req_out, prev))
-        if nxt is not None:
-            recvs.append((req_in, nxt))
-        self._note_peers(sends, recvs, "dir" if group is not None else "default")
-        batched_transfer(sends, recvs, group=group)
-        sends, recvs = [], []
-        if nxt is not None:                      # I am audited by the next stage
-            if s > 0:
-                shp = list(self._audit_inputs[int(req_in[0].item())].shape)
-                shp_out[0] = len(shp)
-                shp_out[1:1 + len(shp)] = torch.tensor(shp, dtype=torch.int64)
-            sends.append((shp_out, nxt))
-        if prev is not None:
-            recvs.append((shp_in, prev))
-        # (the shape answer travels in its own small exchange: the auditee learns m only now)
-        self._note_peers(sends, recvs, "dir" if group is not None else "default")
-        batched_transfer(sends, recvs, group=group)
-        # round 2: weights (bf16 compute copy) and the requested input
+            store.set(f"{tag}/req/{prev}", str(m_mine))
+        x_send = None
+        if nxt is not None and s > 0:           # I am audited by the next stage: which input?
+            k = f"{tag}/req/{self.rank}"
+            m_req = int(store.get(k))
+            store.delete_key(k)
+            x_send = self._audit_inputs[m_req].contiguous()
+            store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send.shape))
+        # weights (bf16 compute copy) and the requested input
         sends, recvs = [], []
         if nxt is not None:
             sends.append((st.flat.data, nxt))
-            if s > 0:
-                sends.append((self._audit_inputs[int(req_in[0].item())].contiguous(), nxt))
+            if x_send is not None:
+                sends.append((x_send, nxt))
         mirror, x_prev = None, None
         if prev is not None:                     # I audit the previous stage
             mirror = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
             recvs.append((mirror.flat.data, prev))
             if s - 1 > 0:
-                shape = torch.Size([int(v) for v in shp_in[1:1 + int(shp_in[0].item())].tolist()])
+                k = f"{tag}/shape/{prev}"
+                shape = torch.Size([int(v) for v in store.get(k).decode().split(",")])
+                store.delete_key(k)
                 x_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
                 recvs.append((x_prev, prev))
         self._note_peers(sends, recvs, "dir" if group is not None else "default")

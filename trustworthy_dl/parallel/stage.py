@@ -8,6 +8,8 @@ an ``nn.Sequential`` of (deep copies of) those layers, so stage-local parameter 
 from __future__ import annotations
 
 import copy
+import functools
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -133,12 +135,44 @@ class Stage:
                     lo = b
             self._layer_seg_runs[li] = runs
 
+    def _arm_sinks(self, runner_idx: int):
+        """Autograd hook body: runner ``runner_idx`` is about to run its backward for the step's
+        last micro-batch -> arm the verifier's fused split-K reduce on its (untied) weight
+        gradients: that backward's weight-gradient GEMM then completes each gradient and takes its
+        statistics in one kernel (ops/stats.py reduce_partial), instead of a reduce pass plus a
+        side-stream pass re-reading the final gradient."""
+        gs = self.verifier.grad_stats
+        if gs is None or not self.verifier.verify_on or os.environ.get("TDL_FUSED_GRAD_STATS", "1") == "0":
+            return
+        for li in self._runner_layer_idx[runner_idx]:
+            for lo, hi in self._layer_seg_runs.get(li, []):
+                for j in range(lo, hi):
+                    mg = getattr(self.flat.params[j], "main_grad", None)
+                    if mg is not None and mg.dim() == 2:
+                        mg._tdl_stats_sink = functools.partial(self._fused_sink, j)
+
+    def _fused_sink(self, seg: int, slabs, nsplit: int) -> bool:
+        return self.verifier.grad_stats.reduce_partial(self.flat.grad, seg, slabs, nsplit)
+
     def _grad_ready(self, runner_idx: int):
         """Autograd hook body: runner ``runner_idx``'s backward (incl. weight gradients) of the
-        step's last micro-batch is done -> its layers' gradient statistics can start."""
+        step's last micro-batch is done -> its layers' gradient statistics can start (segments
+        already covered by a fused reduce are skipped)."""
         runs = []
+        gs = self.verifier.grad_stats
+        fused = gs.fused_segs if gs is not None else ()
         for li in self._runner_layer_idx[runner_idx]:
-            runs += self._layer_seg_runs.get(li, [])
+            for lo, hi in self._layer_seg_runs.get(li, []):
+                j = lo
+                while j < hi:
+                    if j in fused:
+                        j += 1
+                        continue
+                    k = j
+                    while k < hi and k not in fused:
+                        k += 1
+                    runs.append((j, k))
+                    j = k
         if runs:
             self.verifier.grad_ready(self.flat.grad, runs)
         cb = getattr(self, "on_tied_ready", None)
@@ -161,9 +195,20 @@ class Stage:
             if arm and x.requires_grad:
                 x.register_hook(lambda g, k=k: self._grad_ready(k))
             x = layer(x)
+            if arm and x.requires_grad:   # fires right before runner k's backward
+                x.register_hook(lambda g, k=k: self._arm_sinks(k))
         last = layers[-1]
         if arm and x.requires_grad:
             x.register_hook(lambda g, k=len(layers) - 1: self._grad_ready(k))
+        out = self._forward_last(last, x, labels, observe)
+        if arm:
+            y = out[0]
+            if isinstance(y, torch.Tensor) and y.requires_grad:
+                y.register_hook(lambda g, k=len(layers) - 1: self._arm_sinks(k))
+        return out
+
+    def _forward_last(self, last, x, labels, observe):
+        layers = self._runners()
         if self.computes_loss:
             mon = x if len(layers) > 1 else None
             if mon is None and observe is not None and getattr(last, "accepts_observer", False):
