@@ -670,7 +670,7 @@ __device__ __forceinline__ float wave_median(const float* v, int n, int lane) {
 }
 
 constexpr int ZS_EARLY_MIN = 8;
-constexpr float ZS_EARLY_FACTOR = 2.f;
+constexpr float ZS_EARLY_FACTOR = 3.f;
 
 __global__ __launch_bounds__(256) void zscore_kernel(float* __restrict__ ring, int* __restrict__ state,
                                                      const float* __restrict__ cur, int K, int H, int warmup,

@@ -4,7 +4,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/prof_fuse
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py tests/test_kernels_gpu.py -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > $R/gpurun_out/pytest_fuse.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py tests/test_kernels_gpu.py tests/test_conv_gpu.py -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > $R/gpurun_out/pytest_fuse.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $R/gpurun_out/pytest_fuse.log; [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do
   for f in 0 1; do

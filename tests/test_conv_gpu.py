@@ -245,3 +245,24 @@ def test_vgg16_224_gpu_matches_cpu_fp32():
     assert gpu[1] == pytest.approx(cpu[1], rel=1e-1)       # same first update
     assert all(l < 9.0 for l in gpu), gpu                   # no divergence (ln 1000 = 6.9)
     assert gpu[-1] < gpu[0]
+
+
+@pytest.mark.parametrize("k,stride,pad,shape", [(3, 2, 1, (4, 64, 56, 56)), (3, 2, 1, (2, 16, 15, 13)),
+                                                (2, 2, 0, (2, 64, 32, 32)), (2, 2, 0, (1, 8, 7, 9))])
+def test_max_pool_nhwc_matches_torch(k, stride, pad, shape):
+    """Native NHWC max-pool forward / backward vs fp32 torch (small-integer inputs, exact in bf16;
+    ties go to the first window position in row-major order in both)."""
+    from trustworthy_dl.ops import max_pool2d
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    base = (torch.randperm(N * C * H * W) % 251).float().reshape(shape) - 125.0
+    x = base.bfloat16().to("cuda").contiguous(memory_format=torch.channels_last)
+    x = x.requires_grad_(True)
+    y = max_pool2d(x, k, stride, pad)
+    g = torch.randn(y.shape, device="cuda").bfloat16()
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, k, stride, pad)
+    yr.backward(g.float())
+    assert torch.equal(y.float(), yr)
+    assert float((x.grad.float() - xr.grad).abs().max()) <= 2e-2 * float(xr.grad.abs().max())

@@ -100,7 +100,7 @@ class Stem(nn.Module):
 
     def forward(self, x):
         x = ops.conv_bn_act(x, self.conv, self.bn, relu=True)
-        return F.max_pool2d(x, 3, 2, 1) if self.pool else x
+        return ops.max_pool2d(x, 3, 2, 1) if self.pool else x
 
 
 class _PipelineNet(nn.Module):
@@ -220,7 +220,7 @@ class ConvUnit(nn.Module):
 
     def forward(self, x):
         x = ops.conv_bn_act(x, self.conv, self.bn, relu=True)
-        return F.max_pool2d(x, 2) if self.pool else x
+        return ops.max_pool2d(x, 2) if self.pool else x
 
 
 def vgg(depth: int = 16, num_classes: int = 10, seed: Optional[int] = 0, image_size: int = 32) -> _PipelineNet:

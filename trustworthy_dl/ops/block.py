@@ -18,10 +18,9 @@ is one ``torch.autograd.Function`` whose forward/backward call the gfx950 kernel
 * the MLP's elementwise work rides in the native MFMA GEMM's epilogue (csrc/gemm.hip, ping-pong
   kernel with LDS-staged row-contiguous epilogues): forward ``f = gelu(h2 @ Wfc + bfc)`` stores the
   pre-activation and the activation from one kernel, backward ``dpre = (dy @ Wp^T) * gelu'(pre)``
-  accumulates the ``bfc`` gradient as column sums in the same kernel (TDL_NATIVE_GEMM=mlp, the
-  default: 1.005x / 1.20x of hipBLASLt + the separate pass, profiles/r2_gemm_fused_lds_epilogue.jsonl;
-  +1.5 % per step, profiles/r2_native_mlp_ab.txt).  ``all`` also routes the plain projections to
-  it (0.81-0.88x of hipBLASLt per product: slower), ``off`` keeps hipBLASLt + the bias/GELU kernels;
+  accumulates the ``bfc`` gradient as column sums in the same kernel (1.005x / 1.20x of hipBLASLt +
+  the separate pass, profiles/r2_gemm_fused_lds_epilogue.jsonl; +1.5 % per step,
+  profiles/r2_native_mlp_ab.txt); every weight gradient runs on the native persistent kernel;
 * autograd bookkeeping is one node per block instead of ~12 (host time matters at 8 stages x
   64 micro-batches per step).
 
@@ -143,37 +142,26 @@ def _colsum_into(acc, d):
         acc.add_(d.float().sum(0))
 
 
-def _native_gemm_mode() -> str:
-    # default "mlp": the MLP's fc forward (bias + GELU epilogue, pre-activation stored) and its
-    # proj dgrad (dGELU epilogue + bias-gradient column sums) run on the native MFMA GEMM — +1.5 %
-    # per step over hipBLASLt + separate passes (profiles/r2_native_mlp_ab.txt); "all" also routes
-    # the plain projections (slower: 0.81-0.88x of hipBLASLt), "off" keeps every product on the library
-    return os.environ.get("TDL_NATIVE_GEMM", "mlp")
-
-
+# GEMM routing (fixed, measured): products with an elementwise epilogue to fuse (the MLP's fc forward
+# with bias + GELU, its proj dgrad with dGELU + bias-gradient column sums) and every weight gradient
+# (fp32 main_grad, split-K) run on the native MFMA kernels (csrc/gemm.hip); the plain projections
+# (qkv / out / proj forward, qkv / out / fc dgrad) stay on the library GEMM, which the native kernel
+# reaches only 0.83-0.93x of on those shapes (profiles/r3_gemm_lab.jsonl).
 def _native_mlp(h2, wfc, bfc) -> bool:
-    if not h2.is_cuda or _native_gemm_mode() == "off" or bfc.dtype != torch.bfloat16:
+    if not h2.is_cuda or bfc.dtype != torch.bfloat16:
         return False
     from . import gemm
     return gemm.supported(h2, wfc)
 
 
 def _mm(a, b, bias=None):
-    """a @ b (+ bias): the native kernel under TDL_NATIVE_GEMM=all, the library GEMM otherwise."""
-    if a.is_cuda and _native_gemm_mode() == "all":
-        from . import gemm
-        if gemm.supported(a, b) and (bias is None or bias.dtype == torch.bfloat16):
-            return gemm.matmul(a, b, bias=bias)
+    """a @ b (+ bias) on the library GEMM (plain projection)."""
     return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)
 
 
 def _addmm_inplace(c, a, b):
     """c += a @ b (c is a fresh, un-saved buffer)."""
     if c.is_cuda:
-        if _native_gemm_mode() == "all":
-            from . import gemm
-            if gemm.supported(a, b):
-                return gemm.matmul(a, b, out=c, epi="resadd")
         return c.addmm_(a, b)
     return c.copy_((c.float() + a.float() @ b.float()).to(c.dtype))
 

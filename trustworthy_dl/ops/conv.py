@@ -44,6 +44,34 @@ def _out_hw(H: int, W: int, R: int, S: int, stride: int, pad: int):
     return (H + 2 * pad - R) // stride + 1, (W + 2 * pad - S) // stride + 1
 
 
+def _weight_layout(weight: torch.Tensor, cp: int, kind: str) -> torch.Tensor:
+    """The kernel layouts of a conv weight [Cout, C, R, S]: ``"krsc"`` = [Cout][R][S][cp] (forward),
+    ``"crsk"`` = [cp][R][S][Cout] (data gradient), input channels zero-padded to ``cp``.  Cached on
+    the parameter per weight generation (every optimizer update / engine step bumps it, in-place
+    torch writes bump the tensor version: ops/layers.py fwd_weight), so micro-batches after the
+    first and the backward reuse one permuted copy instead of re-permuting per call."""
+    from .layers import _WEIGHT_GEN
+    key = (_WEIGHT_GEN[0], weight._version, weight.data_ptr(), cp, kind)
+    cache = getattr(weight, "_tdl_conv_layouts", None)
+    if cache is None:
+        cache = {}
+        try:
+            weight._tdl_conv_layouts = cache
+        except (AttributeError, RuntimeError):
+            pass
+    hit = cache.get(kind)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    Cout, C, R, S = weight.shape
+    wp = weight
+    if cp != C:
+        wp = torch.zeros((Cout, cp, R, S), dtype=weight.dtype, device=weight.device)
+        wp[:, :C].copy_(weight)
+    out = wp.permute(0, 2, 3, 1).contiguous() if kind == "krsc" else wp.permute(1, 2, 3, 0).contiguous()
+    cache[kind] = (key, out)
+    return out
+
+
 def _pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
     N, C, H, W = x.shape
     xp = torch.empty((N, cp, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last).zero_()
@@ -62,12 +90,9 @@ class _Conv2dNHWC(torch.autograd.Function):
             raise ValueError(f"native conv: unsupported shapes x={tuple(x.shape)} w={tuple(weight.shape)}")
         cp = (C + 7) // 8 * 8
         xs = x.contiguous(memory_format=torch.channels_last)
-        wp = weight
         if cp != C:
             xs = _pad_channels(xs, cp)
-            wp = torch.zeros((Cout, cp, R, S), dtype=weight.dtype, device=weight.device)
-            wp[:, :C].copy_(weight)
-        wk = wp.permute(0, 2, 3, 1).contiguous()
+        wk = _weight_layout(weight, cp, "krsc")
         P, Q = _out_hw(H, W, R, S, stride, pad)
         y = torch.empty((N, Cout, P, Q), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         stats = ws = None
@@ -77,7 +102,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                              device=x.device)
         _lib.call("tdl_conv_nt", ptr(xs), ptr(wk), ptr(y), ptr(stats), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
                   pad, 0, stream_ptr(x.device))
-        ctx.save_for_backward(xs, wp, weight)
+        ctx.save_for_backward(xs, weight)
         ctx.geom = (N, C, cp, H, W, Cout, R, S, P, Q, stride, pad)
         if stats is None:
             stats = torch.zeros(0, dtype=torch.float32, device=x.device)
@@ -86,7 +111,7 @@ class _Conv2dNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
-        xs, wp, weight = ctx.saved_tensors
+        xs, weight = ctx.saved_tensors
         N, C, cp, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
         if dy.dtype != xs.dtype:
@@ -94,7 +119,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         dev = dy.device
         dx = None
         if ctx.needs_input_grad[0]:
-            wd = wp.permute(1, 2, 3, 0).contiguous()  # [cp][R][S][Cout]
+            wd = _weight_layout(weight, cp, "crsk")  # [cp][R][S][Cout]
             dxp = torch.empty((N, cp, H, W), dtype=dy.dtype, device=dev, memory_format=torch.channels_last)
             _lib.call("tdl_conv_nt", ptr(dy), ptr(wd), ptr(dxp), None, None, N, P, Q, Cout, H, W, cp, R, S, stride,
                       pad, 1, stream_ptr(dev))
@@ -197,7 +222,7 @@ class _BNActConvNHWC(torch.autograd.Function):
         _lib.call("tdl_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
                   ptr(running_mean if upd else None), ptr(running_var if upd else None), ptr(pro), ptr(sums), M, C,
                   float(eps), float(momentum), stream_ptr(dev))
-        wk = weight.permute(0, 2, 3, 1).contiguous()
+        wk = _weight_layout(weight, C, "krsc")
         P, Q = _out_hw(H, W, R, S, stride, pad)
         out = torch.empty((N, Cout, P, Q), dtype=y.dtype, device=dev, memory_format=torch.channels_last)
         st = ws = None
@@ -225,7 +250,7 @@ class _BNActConvNHWC(torch.autograd.Function):
         if dout.dtype != ys.dtype:
             dout = dout.to(ys.dtype)
         # data gradient of the conv = gradient w.r.t. the (never stored) BN output
-        wd = weight.permute(1, 2, 3, 0).contiguous()  # [C][R][S][Cout]
+        wd = _weight_layout(weight, C, "crsk")  # [C][R][S][Cout]
         dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
         _lib.call("tdl_conv_nt", ptr(dout), ptr(wd), ptr(dbn), None, None, N, P, Q, Cout, H, W, C, R, S, stride, pad, 1,
                   stream_ptr(dev))
@@ -286,6 +311,42 @@ def conv_bn_chain(x: torch.Tensor, units, relu: bool = True, residual: Optional[
     momentum = bn.momentum if bn.momentum is not None else 0.1
     return _BatchNormActNHWC.apply(y, stats, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, True,
                                    momentum, bn.eps, relu)
+
+
+class _MaxPoolNHWC(torch.autograd.Function):
+    """Max-pool on NHWC bf16 (csrc/pool.hip): the window argmax is kept as one byte per output
+    element and the backward gathers (deterministic, no atomics)."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        N, C, H, W = x.shape
+        xs = x.contiguous(memory_format=torch.channels_last)
+        P, Q = _out_hw(H, W, k, k, stride, pad)
+        y = torch.empty((N, C, P, Q), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        arg = torch.empty((N, P, Q, C), dtype=torch.uint8, device=x.device)
+        _lib.call("tdl_maxpool_fwd", ptr(xs), ptr(y), ptr(arg), N, H, W, C, P, Q, k, k, stride, pad,
+                  stream_ptr(x.device))
+        ctx.save_for_backward(arg)
+        ctx.geom = (N, C, H, W, P, Q, k, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, C, H, W, P, Q, k, stride, pad = ctx.geom
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        _lib.call("tdl_maxpool_bwd", ptr(dy), ptr(arg), ptr(dx), N, H, W, C, P, Q, k, k, stride, pad,
+                  stream_ptr(dy.device))
+        return dx, None, None, None
+
+
+def max_pool2d(x: torch.Tensor, kernel_size: int, stride: Optional[int] = None, padding: int = 0) -> torch.Tensor:
+    """``F.max_pool2d`` (square window, floor mode); native NHWC kernels for CUDA bf16 with C % 8 == 0."""
+    stride = kernel_size if stride is None else stride
+    if native_conv_ok(x) and x.shape[1] % 8 == 0:
+        return _MaxPoolNHWC.apply(x, int(kernel_size), int(stride), int(padding))
+    return F.max_pool2d(x, kernel_size, stride, padding)
 
 
 def _single(v) -> int:

@@ -282,7 +282,10 @@ def _lower_upper_median(x: torch.Tensor) -> torch.Tensor:
 class DeviceZScore:
     """Device ring-buffer baseline + z-score decision for one monitored signal (K4)."""
 
-    EARLY_MIN, EARLY_FACTOR = 8, 2.0   # csrc/stats.hip ZS_EARLY_MIN / ZS_EARLY_FACTOR
+    # csrc/stats.hip ZS_EARLY_MIN / ZS_EARLY_FACTOR.  3x: the clean ResNet-50 stages of attack config 4
+    # reached |z| 12-17 right after a re-shard (profiles/r3_cfg_reshard.jsonl), gradient poisoning
+    # reads 28-42
+    EARLY_MIN, EARLY_FACTOR = 8, 3.0
 
     def __init__(self, k: int, device, history: int = 1000, warmup: int = 10, z_decision: float = 2.5,
                  exclude_current: bool = True, max_quarantine: int = 50, robust=True, window: int = 100,
@@ -309,6 +312,13 @@ class DeviceZScore:
         self.ring = torch.zeros(history, k, dtype=torch.float32, device=self.device)
         self.state = torch.zeros(4, dtype=torch.int32, device=self.device)
         self.out = torch.zeros(4 + k, dtype=torch.float32, device=self.device)
+
+    def rewarm(self, keep: Optional[int] = None) -> None:
+        """Re-enter warm-up keeping only the ``keep`` (default EARLY_MIN) most recent baseline entries:
+        the baseline refills from the new regime while the early gate still flags gross outliers
+        (used after a re-plan: the training dynamics of a re-sharded pipeline shift)."""
+        keep = self.EARLY_MIN if keep is None else int(keep)
+        self.state[0:1].clamp_(max=keep)
 
     def observe(self, cur: torch.Tensor) -> torch.Tensor:
         """Returns device vector [4 + k]: flag, mean_z, confidence, n_valid, z[k] (-1 = skipped)."""

@@ -1083,7 +1083,8 @@ class PipelineEngine:
         without leaving a trace: module buffers (running statistics) are restored afterwards."""
         bufs = [b.detach().clone() for b in st.module.buffers()]
         try:
-            y, _ = st.forward(x, None)
+            with torch.no_grad():   # no autograd graph / saved activations for the recompute
+                y, _ = st.forward(x, None)
         finally:
             for b, v in zip(st.module.buffers(), bufs):
                 b.copy_(v)
@@ -1752,6 +1753,7 @@ class PipelineEngine:
             ov = old_verifiers.get(node)
             if ov is not None and old_ranges.get(node) == tuple(st.layer_range) and ov.S == st.verifier.S:
                 st.verifier.adopt(ov)
+                st.verifier.rewarm()   # the re-sharded pipeline's dynamics shift: re-warm, gated
         del packed
         self._sync_all()
         ph["unpack_s"] = time.perf_counter() - t3

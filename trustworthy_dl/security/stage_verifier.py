@@ -272,6 +272,12 @@ class StageVerifier:
             self.grad_stats.ref = other.grad_stats.ref.to(self.device)
             self.grad_stats.ref_valid = other.grad_stats.ref_valid
 
+    def rewarm(self):
+        """After a re-plan: the detectors keep their most recent baseline entries but re-enter the
+        early-gated warm-up (only gross outliers flag until the baseline has refilled)."""
+        self.out_det.rewarm()
+        self.grad_det.rewarm()
+
     def state_dict(self):
         return {k: v.detach().cpu() for k, v in {
             "out_ring": self.out_det.ring, "out_state": self.out_det.state,
