@@ -265,34 +265,6 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
 }
 
 // ============================================================================ backward
-// delta[bh, t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
-// Lane = 8 consecutive elements, so a wave instruction reads 1 KB contiguous of O and of dO (8 heads
-// of one token); the 8 lanes of a head reduce by xor-shuffles and one of them stores the head's delta.
-static_assert(HD / 8 == 8, "delta kernel: 8 lanes per head row");
-__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                         float* __restrict__ delta, int B, int T, int H) {
-    const size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;   // 16-byte vector index over B*T*H*HD/8
-    const size_t nvec = (size_t)B * T * H * (HD / 8);
-    float acc = 0.f;
-    if (v < nvec) {
-        float a[8], g[8];
-        unpack8(((const uint4*)o)[v], a);
-        unpack8(((const uint4*)dout)[v], g);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
-    }
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    acc += __shfl_xor(acc, 4, 64);
-    if (v < nvec && (threadIdx.x & 7) == 0) {
-        const size_t row = v >> 3;                               // (b * T + t) * H + h
-        const int hd = (int)(row % H);
-        const size_t bt = row / H;
-        const int b = (int)(bt / T), t = (int)(bt - (size_t)b * T);
-        delta[((size_t)b * H + hd) * T + t] = acc;
-    }
-}
-
 // ---------------------------------------------------------------------------- dK, dV (key-owned)
 // Workgroup = 128 keys (4 waves x 32, key on the MFMA lane); walks query tiles of BQ = 32 NS rows
 // with a double-buffered LDS pipeline: the next tile's Q / dO / lse / delta are loaded into
@@ -563,7 +535,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 // No atomics, no LDS round trip for dS.
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
+                                                          const float* __restrict__ lse, const bf16_t* __restrict__ out,
+                                                          float* __restrict__ delta,
                                                           bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale,
                                                           float* __restrict__ bias_part) {
     constexpr int BM = 128, BN = 64;
@@ -583,15 +556,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     const int q0 = qblk + 32 * w;
     const int qi = q0 + r;
     const float lse_q = lse[(size_t)bh * T + qi] * 1.4426950408889634f;
-    const float dl_q = delta[(size_t)bh * T + qi];
     const float sl2 = scale * 1.4426950408889634f;
 
+    // delta = rowsum(dO * O) of this lane's query, from the dO fragments the lane loads anyway plus
+    // the same slice of O (the two half-waves h hold the two halves of the row); written for the
+    // dK/dV kernel, which runs after this one (no separate delta pass over O and dO)
     bf16x8_t qf[4], df[4];
+    float dl_q = 0.f;
+    const bf16_t* obase = out + (size_t)b * T * ldo + hd * HD;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         qf[s] = as_bf16x8(*(const uint4*)(qbase + (size_t)qi * ldq + 16 * s + 8 * h));
-        df[s] = as_bf16x8(*(const uint4*)(dobase + (size_t)qi * ldo + 16 * s + 8 * h));
+        const uint4 dr = *(const uint4*)(dobase + (size_t)qi * ldo + 16 * s + 8 * h);
+        df[s] = as_bf16x8(dr);
+        float gv[8], ov[8];
+        unpack8(dr, gv);
+        unpack8(*(const uint4*)(obase + (size_t)qi * ldo + 16 * s + 8 * h), ov);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dl_q += gv[k] * ov[k];
     }
+    dl_q += __shfl_xor(dl_q, 32, 64);
+    if (h == 0) delta[(size_t)bh * T + qi] = dl_q;
     f32x16 dq0 = {}, dq1 = {};
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     int nkb = T / BN;
@@ -716,23 +701,24 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                          hipStream_t s) {
     if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
     if ((bias_acc == nullptr) != (bias_part == nullptr)) return (int)hipErrorInvalidValue;
-    attn_delta_kernel<<<(unsigned)(((size_t)B * T * H * (HD / 8) + 255) / 256), 256, 0, s>>>((const bf16_t*)out, (const bf16_t*)dout, delta, B, T, H);
+    // the dQ kernel also produces delta = rowsum(dO * O) for the dK/dV kernel, so it runs first
     const int grid = B * H * (T / 128);
+    auto Ob = (const bf16_t*)out;
     auto Q = (const bf16_t*)qkv;
     auto dO = (const bf16_t*)dout;
     auto dQKV = (bf16_t*)dqkv;
     const int nb = attn_nbh_arg(B * H);
     float* bp = bias_part;
     if (causal) {
+        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
+        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<false, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dkdv_kernel<false, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     }
     if (bias_acc != nullptr) {
         const int rc = (int)hipGetLastError();

@@ -286,6 +286,39 @@ def test_grad_stats_in_pieces_match_one_pass():
     assert float(sq) == pytest.approx(ref, rel=1e-5)
 
 
+def test_grad_stats_reduce_partial_bit_identical():
+    """Split-K slabs reduced into the flat gradient AND its segment's partial statistics in one
+    kernel == tdl_splitk_reduce_add followed by the plain partial pass: the same stored gradient and
+    the same final statistics, bit for bit (one segment fused, the others plain)."""
+    from trustworthy_dl.ops import _lib
+    from trustworthy_dl.ops._lib import ptr, stream_ptr
+    from trustworthy_dl.ops.stats import FlatGradStats
+    torch.manual_seed(3)
+    sizes = [1000, 3 * 65536 + 8, 4096, 77, 65536 * 2]
+    g0 = torch.randn(sum(sizes), device=DEV)
+    seg = 1
+    off = sum(sizes[:seg])
+    S = 4
+    slabs = torch.randn(S, sizes[seg], device=DEV)
+    outs = []
+    for fused in (False, True):
+        gs = FlatGradStats(sizes, DEV)
+        for step in range(2):                 # the second step exercises the EMA reference
+            g = g0.clone() * (1 + step)
+            if fused:
+                assert gs.reduce_partial(g, seg, slabs, S)
+            else:
+                _lib.call("tdl_splitk_reduce_add", ptr(g[off:off + sizes[seg]]), ptr(slabs), S, sizes[seg],
+                          stream_ptr(g.device))
+                c0, c1 = gs.chunk_range_of(seg, seg + 1)
+                gs.partial(g, c0, c1)
+            out = gs.compute(g).clone()
+        outs.append((g, out, gs.ref.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1]), (outs[0][1] - outs[1][1]).abs().max()
+    assert torch.equal(outs[0][2], outs[1][2])
+
+
 @pytest.mark.parametrize("kw", [{}, {"robust": "detrend", "window": 32},
                                 {"robust": "detrend", "agg": "max", "abs_floor": 0.02, "rel_floor": 0.0,
                                  "z_decision": 8.0, "max_quarantine": 5},
