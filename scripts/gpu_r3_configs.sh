@@ -20,5 +20,7 @@ if [ "${PART:-a}" = a ]; then
     run clean_noaudit 300 --configs clean --seeds 3 --steps 500 --no-audit &&
     run reshard 560 --configs 3,4,5 --seeds 1,2,3 --steps 200
 else
-    run detect 1100 --configs 3,4,5 --seeds 1,2,3 --steps 300 --no-reassign
+    run detect 900 --configs 3,4,5 --seeds 1,2,3 --steps 300 --no-reassign &&
+    run clean200 150 --configs clean --seeds 4 --steps 200 &&
+    run clean200_noaudit 150 --configs clean --seeds 4 --steps 200 --no-audit
 fi

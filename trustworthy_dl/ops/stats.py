@@ -19,7 +19,7 @@ from ._lib import ptr, stream_ptr
 N_TENSOR_STATS = 12
 N_GRAD_STATS = 17
 NHIST = 2048
-CHUNK = 1 << 15
+CHUNK = 1 << 13    # elements per partial-statistics block: >= 4 blocks per CU for a GPT-2-medium weight
 REF_STRIDE = 8       # the EMA reference gradient is kept on one chunk in REF_STRIDE (csrc/stats.hip)
 
 _ws_cache = {}

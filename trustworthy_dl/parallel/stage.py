@@ -140,9 +140,12 @@ class Stage:
         last micro-batch -> arm the verifier's fused split-K reduce on its (untied) weight
         gradients: that backward's weight-gradient GEMM then completes each gradient and takes its
         statistics in one kernel (ops/stats.py reduce_partial), instead of a reduce pass plus a
-        side-stream pass re-reading the final gradient."""
+        side-stream pass re-reading the final gradient.  Opt-in (TDL_FUSED_GRAD_STATS=1): it saves
+        the re-read but puts the statistics on the compute stream, and measured 1.4 % slower per
+        step than the overlapped side-stream pass (GPT-2-medium N=1, 3 interleaved rounds:
+        profiles/r3_fused_grad_stats_ab.txt)."""
         gs = self.verifier.grad_stats
-        if gs is None or not self.verifier.verify_on or os.environ.get("TDL_FUSED_GRAD_STATS", "1") == "0":
+        if gs is None or not self.verifier.verify_on or os.environ.get("TDL_FUSED_GRAD_STATS", "0") != "1":
             return
         for li in self._runner_layer_idx[runner_idx]:
             for lo, hi in self._layer_seg_runs.get(li, []):
