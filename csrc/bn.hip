@@ -365,6 +365,20 @@ TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, con
     return bn_act_bwd_impl(dout, out, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, M, C, relu, nullptr, s);
 }
 
+// Backward of a folded BN (+ ReLU) whose two per-channel sums were already reduced (into the first
+// replica row of sums) by the producing data-gradient convolution (tdl_conv_dgrad_bnsums): fold +
+// the elementwise pass only.
+TDL_API int tdl_bn_act_bwd_pro_summed(const void* dout, const void* x, const float* mean, const float* rstd,
+                                      const void* gamma, const float* pro, float* sums, void* dx, float* dgamma,
+                                      float* dbeta, int64_t M, int C, hipStream_t s) {
+    if (C % 8 != 0 || pro == nullptr) return (int)hipErrorInvalidValue;
+    bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
+    bn_act_bwd_dx_kernel<<<grid_for(M * (C / 8)), 256, 0, s>>>(
+        (const bf16_t*)dout, nullptr, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma, sums + (size_t)NREP * 2 * C,
+        (bf16_t*)dx, nullptr, M, C, 1, pro);
+    TDL_LAUNCH_CHECK();
+}
+
 // Backward of a folded BN (+ ReLU): no stored output, the mask is recomputed from x with pro.
 TDL_API int tdl_bn_act_bwd_pro(const void* dout, const void* x, const float* mean, const float* rstd, const void* gamma,
                                const float* pro, float* sums, void* dx, float* dgamma, float* dbeta, int64_t M, int C,

@@ -81,11 +81,18 @@ __device__ __forceinline__ uint4 pro_apply(uint4 v, const float* sc, const float
     return pack8(f);
 }
 
-template <int BCO, bool TRANSPOSED, bool STATS, bool PRO = false>
+// BNB (data gradient of a convolution whose input was relu(BN(y)) folded into its operand load): the
+// epilogue also reduces the BN backward's two per-channel sums over the stored gradient g of the
+// never-materialised BN output — sum(dv) and sum(dv * xhat) with dv = g where y * scale + shift > 0
+// (the ReLU mask, recomputed from y = bx) and xhat = (y - mean) * rstd; bnp = [scale | shift | mean |
+// rstd] fp32 [4 C] — into the STATS partial rows, so the BN backward needs no reduction pass.
+template <int BCO, bool TRANSPOSED, bool STATS, bool PRO = false, bool BNB = false>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restrict__ act, const bf16_t* __restrict__ wk,
                                                          bf16_t* __restrict__ out, float* __restrict__ part,
-                                                         ConvDims d, const float* __restrict__ pro) {
+                                                         ConvDims d, const float* __restrict__ pro,
+                                                         const bf16_t* __restrict__ bx = nullptr) {
     static_assert(!(PRO && TRANSPOSED), "the BN prologue applies to forward activations only");
+    static_assert(!BNB || (TRANSPOSED && STATS), "BN-backward sums: data-gradient kernels with the STATS rows");
     constexpr int TCO = BCO / 64;   // 32-row cout tiles per wave (waves are 2 x 2)
     constexpr int AROWS = BCO / 32; // weight rows staged per thread (BCO rows x 8 chunks / 256 threads)
     __shared__ __attribute__((aligned(16))) bf16_t As[2][BCO * BK];
@@ -228,6 +235,15 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
         for (int g = 0; g < 4; ++g) {
             const int co = co0 + cl + 8 * g + 4 * h;
             float sv[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+            float bsc[4] = {}, bsh[4] = {}, bmu[4] = {}, brs[4] = {};
+            if (BNB && co < d.Cout) {   // Cout % 8 == 0: the 4 channels are all in range
+                const float4 a = *(const float4*)(pro + co), b = *(const float4*)(pro + d.Cout + co);
+                const float4 c = *(const float4*)(pro + 2 * d.Cout + co), e = *(const float4*)(pro + 3 * d.Cout + co);
+                bsc[0] = a.x, bsc[1] = a.y, bsc[2] = a.z, bsc[3] = a.w;
+                bsh[0] = b.x, bsh[1] = b.y, bsh[2] = b.z, bsh[3] = b.w;
+                bmu[0] = c.x, bmu[1] = c.y, bmu[2] = c.z, bmu[3] = c.w;
+                brs[0] = e.x, brs[1] = e.y, brs[2] = e.z, brs[3] = e.w;
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int m = m0 + wm * 64 + 32 * j + lr;
@@ -238,10 +254,21 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                 if (STATS && mok) {
                     float r[4];
                     unpack4(pk, r);
+                    if constexpr (BNB) {
+                        float xv[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (co < d.Cout) unpack4(*(const uint2*)(bx + (size_t)m * d.Cout + co), xv);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        sv[e] += r[e];
-                        sq[e] += r[e] * r[e];
+                        for (int e = 0; e < 4; ++e) {
+                            const float dv = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? r[e] : 0.f;
+                            sv[e] += dv;
+                            sq[e] += dv * (xv[e] - bmu[e]) * brs[e];
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            sv[e] += r[e];
+                            sq[e] += r[e] * r[e];
+                        }
                     }
                 }
             }
@@ -460,9 +487,11 @@ TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) { return (int64_t)((M 
 
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
                         int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
-                        const float* pro, hipStream_t s) {
+                        const float* pro, hipStream_t s, const void* bnb_x = nullptr, bool stats_accumulate = false) {
     ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
-    if (!dims_ok(d) || (pro != nullptr && transposed)) return (int)hipErrorInvalidValue;
+    const bool bnb = bnb_x != nullptr;
+    if (!dims_ok(d) || (pro != nullptr && transposed && !bnb)) return (int)hipErrorInvalidValue;
+    if (bnb && (!transposed || pro == nullptr || stats == nullptr || Cout % 8)) return (int)hipErrorInvalidValue;
     const int M = N * P * Q;
     const bool st = stats != nullptr;
     if (st && stats_ws == nullptr) return (int)hipErrorInvalidValue;
@@ -474,7 +503,12 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     auto O = (bf16_t*)out;
 #define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr)
 #define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro)
-    if (pro != nullptr) {
+#define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, \
+                                                                                    (const bf16_t*)bnb_x)
+    if (bnb) {
+        if (big) LAUNCHB(128);
+        else LAUNCHB(64);
+    } else if (pro != nullptr) {
         if (big) { if (st) LAUNCHP(128, true); else LAUNCHP(128, false); }
         else { if (st) LAUNCHP(64, true); else LAUNCHP(64, false); }
     } else if (big) {
@@ -486,9 +520,12 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     }
 #undef LAUNCH
 #undef LAUNCHP
+#undef LAUNCHB
     if (st) {
-        hipError_t e = hipMemsetAsync(stats, 0, sizeof(float) * 2 * Cout, s);
-        if (e != hipSuccess) return (int)e;
+        if (!stats_accumulate) {
+            hipError_t e = hipMemsetAsync(stats, 0, sizeof(float) * 2 * Cout, s);
+            if (e != hipSuccess) return (int)e;
+        }
         const int rpb = 64;
         const dim3 g((2 * Cout + 63) / 64, (ntm + rpb - 1) / rpb);
         stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats);
@@ -556,6 +593,17 @@ TDL_API int tdl_conv_nt_pro(const void* act, const void* wk, void* out, float* s
                             const float* pro, hipStream_t s) {
     if (pro == nullptr) return (int)hipErrorInvalidValue;
     return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 0, pro, s);
+}
+
+// Data gradient dbn of a convolution whose input relu(BN(y)) was folded into its operand load, with
+// the BN backward's per-channel sums reduced in its epilogue (see BNB): sums (fp32 [2 C], the first
+// replica row of the BN's zeroed backward buffer) += (sum dv, sum dv * xhat); bnp = [scale | shift |
+// mean | rstd] fp32 [4 C]; y = the BN input (NHWC, same shape as dbn).  Pair with tdl_bn_act_bwd_pro_summed.
+TDL_API int tdl_conv_dgrad_bnsums(const void* dy, const void* wd, void* dbn, float* ws, int N, int Hin, int Win, int Cin,
+                                  int P, int Q, int Cout, int R, int S, int stride, int pad, const void* y,
+                                  const float* bnp, float* sums, hipStream_t s) {
+    if (y == nullptr || bnp == nullptr || sums == nullptr || ws == nullptr) return (int)hipErrorInvalidValue;
+    return conv_nt_impl(dy, wd, dbn, sums, ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 1, bnp, s, y, true);
 }
 
 TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,

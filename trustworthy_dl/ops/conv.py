@@ -249,11 +249,15 @@ class _BNActConvNHWC(torch.autograd.Function):
         dout = dout.contiguous(memory_format=torch.channels_last)
         if dout.dtype != ys.dtype:
             dout = dout.to(ys.dtype)
-        # data gradient of the conv = gradient w.r.t. the (never stored) BN output
+        # data gradient of the conv = gradient w.r.t. the (never stored) BN output; its epilogue also
+        # reduces the BN backward's per-channel sums (ReLU mask recomputed from y), so the BN
+        # backward below is the elementwise pass only
         wd = _weight_layout(weight, C, "crsk")  # [C][R][S][Cout]
         dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
-        _lib.call("tdl_conv_nt", ptr(dout), ptr(wd), ptr(dbn), None, None, N, P, Q, Cout, H, W, C, R, S, stride, pad, 1,
-                  stream_ptr(dev))
+        bnp = torch.cat([pro, mean, rstd])
+        ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * H * W, C)), dtype=torch.float32, device=dev)
+        _lib.call("tdl_conv_dgrad_bnsums", ptr(dout), ptr(wd), ptr(dbn), ptr(ws), N, P, Q, Cout, H, W, C, R, S, stride,
+                  pad, ptr(ys), ptr(bnp), ptr(ctx.sums), stream_ptr(dev))
         # weight gradient against relu(BN(y)) recomputed on load
         gw = None
         if ctx.needs_input_grad[8]:
@@ -274,8 +278,8 @@ class _BNActConvNHWC(torch.autograd.Function):
         mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
         dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
         db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
-        _lib.call("tdl_bn_act_bwd_pro", ptr(dbn), ptr(ys), ptr(mean), ptr(rstd), ptr(gamma), ptr(pro), ptr(ctx.sums),
-                  ptr(dy), ptr(dg), ptr(db), N * H * W, C, 1, stream_ptr(dev))
+        _lib.call("tdl_bn_act_bwd_pro_summed", ptr(dbn), ptr(ys), ptr(mean), ptr(rstd), ptr(gamma), ptr(pro),
+                  ptr(ctx.sums), ptr(dy), ptr(dg), ptr(db), N * H * W, C, stream_ptr(dev))
         gg = None if mg_g is not None else dg.to(gamma.dtype)
         gb = None if mg_b is not None else db.to(beta.dtype)
         return dy, None, gg, gb, None, None, None, None, gw, None, None, None
