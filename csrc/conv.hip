@@ -595,6 +595,35 @@ TDL_API int tdl_conv_nt_pro(const void* act, const void* wk, void* out, float* s
     return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 0, pro, s);
 }
 
+// Both kernel layouts of a conv weight w [Cout][C][R][S] (bf16, the nn.Conv2d parameter) in one pass:
+// krsc [Cout][R][S][Cp] (forward) and crsk [Cp][R][S][Cout] (data gradient), input channels zero-
+// padded to Cp (>= C).  Either output may be null.
+__global__ __launch_bounds__(256) void conv_weight_layouts_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ krsc,
+                                                                  bf16_t* __restrict__ crsk, int Cout, int C, int Cp,
+                                                                  int RS) {
+    const int64_t n = (int64_t)Cout * Cp * RS;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        // i enumerates the krsc image: co, rs, c (c fastest)
+        const int c = (int)(i % Cp);
+        const int64_t t = i / Cp;
+        const int rs = (int)(t % RS);
+        const int co = (int)(t / RS);
+        const bf16_t v = c < C ? w[((int64_t)co * C + c) * RS + rs] : (bf16_t)0;
+        if (krsc) krsc[i] = v;
+        if (crsk) crsk[((int64_t)c * RS + rs) * Cout + co] = v;
+    }
+}
+
+TDL_API int tdl_conv_weight_layouts(const void* w, void* krsc, void* crsk, int Cout, int C, int Cp, int RS, hipStream_t s) {
+    if (Cp < C || Cout <= 0 || RS <= 0) return (int)hipErrorInvalidValue;
+    const int64_t n = (int64_t)Cout * Cp * RS;
+    int64_t g = (n + 255) / 256;
+    if (g > 8192) g = 8192;
+    conv_weight_layouts_kernel<<<(int)(g > 0 ? g : 1), 256, 0, s>>>((const bf16_t*)w, (bf16_t*)krsc, (bf16_t*)crsk, Cout, C,
+                                                                   Cp, RS);
+    TDL_LAUNCH_CHECK();
+}
+
 // Data gradient dbn of a convolution whose input relu(BN(y)) was folded into its operand load, with
 // the BN backward's per-channel sums reduced in its epilogue (see BNB): sums (fp32 [2 C], the first
 // replica row of the BN's zeroed backward buffer) += (sum dv, sum dv * xhat); bnp = [scale | shift |

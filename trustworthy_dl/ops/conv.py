@@ -46,30 +46,33 @@ def _out_hw(H: int, W: int, R: int, S: int, stride: int, pad: int):
 
 def _weight_layout(weight: torch.Tensor, cp: int, kind: str) -> torch.Tensor:
     """The kernel layouts of a conv weight [Cout, C, R, S]: ``"krsc"`` = [Cout][R][S][cp] (forward),
-    ``"crsk"`` = [cp][R][S][Cout] (data gradient), input channels zero-padded to ``cp``.  Cached on
-    the parameter per weight generation (every optimizer update / engine step bumps it, in-place
-    torch writes bump the tensor version: ops/layers.py fwd_weight), so micro-batches after the
-    first and the backward reuse one permuted copy instead of re-permuting per call."""
+    ``"crsk"`` = [cp][R][S][Cout] (data gradient), input channels zero-padded to ``cp``.  Both are
+    built by one native pass (tdl_conv_weight_layouts) the first time either is asked for in a weight
+    generation (every optimizer update / engine step bumps it, in-place torch writes bump the tensor
+    version: ops/layers.py fwd_weight) and cached on the parameter, so the forward, the backward and
+    later micro-batches share them."""
     from .layers import _WEIGHT_GEN
-    key = (_WEIGHT_GEN[0], weight._version, weight.data_ptr(), cp, kind)
-    cache = getattr(weight, "_tdl_conv_layouts", None)
-    if cache is None:
-        cache = {}
+    key = (_WEIGHT_GEN[0], weight._version, weight.data_ptr(), cp)
+    hit = getattr(weight, "_tdl_conv_layouts", None)
+    if hit is None or hit[0] != key:
+        Cout, C, R, S = weight.shape
+        if weight.is_cuda and weight.dtype == torch.bfloat16 and weight.is_contiguous():
+            krsc = torch.empty((Cout, R, S, cp), dtype=weight.dtype, device=weight.device)
+            crsk = torch.empty((cp, R, S, Cout), dtype=weight.dtype, device=weight.device)
+            _lib.call("tdl_conv_weight_layouts", ptr(weight), ptr(krsc), ptr(crsk), Cout, C, cp, R * S,
+                      stream_ptr(weight.device))
+        else:
+            wp = weight
+            if cp != C:
+                wp = torch.zeros((Cout, cp, R, S), dtype=weight.dtype, device=weight.device)
+                wp[:, :C].copy_(weight)
+            krsc, crsk = wp.permute(0, 2, 3, 1).contiguous(), wp.permute(1, 2, 3, 0).contiguous()
+        hit = (key, {"krsc": krsc, "crsk": crsk})
         try:
-            weight._tdl_conv_layouts = cache
+            weight._tdl_conv_layouts = hit
         except (AttributeError, RuntimeError):
             pass
-    hit = cache.get(kind)
-    if hit is not None and hit[0] == key:
-        return hit[1]
-    Cout, C, R, S = weight.shape
-    wp = weight
-    if cp != C:
-        wp = torch.zeros((Cout, cp, R, S), dtype=weight.dtype, device=weight.device)
-        wp[:, :C].copy_(weight)
-    out = wp.permute(0, 2, 3, 1).contiguous() if kind == "krsc" else wp.permute(1, 2, 3, 0).contiguous()
-    cache[kind] = (key, out)
-    return out
+    return hit[1][kind]
 
 
 def _pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
@@ -214,9 +217,9 @@ class _BNActConvNHWC(torch.autograd.Function):
         dev = y.device
         ys = y.contiguous(memory_format=torch.channels_last)
         M = N * H * W
-        mean = torch.empty(C, dtype=torch.float32, device=dev)
-        rstd = torch.empty_like(mean)
-        pro = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        # [scale | shift | mean | rstd] in one buffer: the backward's data-gradient epilogue reads all four
+        bnp = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        pro, mean, rstd = bnp[:2 * C], bnp[2 * C:3 * C], bnp[3 * C:]
         sums = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(C)), dtype=torch.float32, device=dev)
         upd = running_mean is not None
         _lib.call("tdl_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
@@ -232,7 +235,7 @@ class _BNActConvNHWC(torch.autograd.Function):
                              device=dev)
         _lib.call("tdl_conv_nt_pro", ptr(ys), ptr(wk), ptr(out), ptr(st), ptr(ws), N, H, W, C, P, Q, Cout, R, S,
                   stride, pad, ptr(pro), stream_ptr(dev))
-        ctx.save_for_backward(ys, mean, rstd, gamma, pro, weight)
+        ctx.save_for_backward(ys, bnp, gamma, weight)
         ctx.sums = sums
         ctx.beta = beta  # a parameter (leaf): only its identity / main_grad is needed
         ctx.geom = (N, C, H, W, Cout, R, S, P, Q, stride, pad)
@@ -243,7 +246,9 @@ class _BNActConvNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _dstats):
-        ys, mean, rstd, gamma, pro, weight = ctx.saved_tensors
+        ys, bnp, gamma, weight = ctx.saved_tensors
+        C_ = ys.shape[1]
+        pro, mean, rstd = bnp[:2 * C_], bnp[2 * C_:3 * C_], bnp[3 * C_:]
         N, C, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
         dev = dout.device
         dout = dout.contiguous(memory_format=torch.channels_last)
@@ -254,7 +259,6 @@ class _BNActConvNHWC(torch.autograd.Function):
         # backward below is the elementwise pass only
         wd = _weight_layout(weight, C, "crsk")  # [C][R][S][Cout]
         dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
-        bnp = torch.cat([pro, mean, rstd])
         ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * H * W, C)), dtype=torch.float32, device=dev)
         _lib.call("tdl_conv_dgrad_bnsums", ptr(dout), ptr(wd), ptr(dbn), ptr(ws), N, P, Q, Cout, H, W, C, R, S, stride,
                   pad, ptr(ys), ptr(bnp), ptr(ctx.sums), stream_ptr(dev))
