@@ -185,8 +185,6 @@ class PipelineEngine:
             self.device = torch.device(cfg.device)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
-            from ..runtime.gemm_tuning import enable_tuned_gemms
-            self.tuned_gemms = enable_tuned_gemms()   # measured hipBLASLt solutions for the library GEMMs
         # conv nets run bf16 on the native NHWC implicit-GEMM kernels (ops/conv.py), like GPT-2
         self.dtype = _resolve_dtype(cfg.compute_dtype, self.device)
         self.tracer = PhaseTracer(self.device, enabled=cfg.trace_phases)
