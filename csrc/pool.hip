@@ -90,6 +90,44 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
     }
 }
 
+// Global average pool (the ResNet / VGG classifier head): out[n][c] = mean over H*W of x[n][h][w][c].
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N, int HW,
+                                                      int C) {
+    const int C8 = C / 8;
+    const int64_t total = (int64_t)N * C8;
+    const float inv = 1.f / (float)HW;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int c8 = (int)(t % C8), n = (int)(t / C8);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const bf16_t* p = x + (size_t)n * HW * C + 8 * c8;
+        for (int i = 0; i < HW; ++i) {
+            float v[8];
+            unpack8(*(const uint4*)(p + (size_t)i * C), v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += v[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] *= inv;
+        *(uint4*)(y + (size_t)n * C + 8 * c8) = pack8(acc);
+    }
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx, int N, int HW,
+                                                      int C) {
+    const int C8 = C / 8;
+    const int64_t total = (int64_t)N * HW * C8;
+    const float inv = 1.f / (float)HW;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int c8 = (int)(t % C8);
+        const int n = (int)(t / ((int64_t)C8 * HW));
+        float g[8];
+        unpack8(*(const uint4*)(dy + (size_t)n * C + 8 * c8), g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] *= inv;
+        *(uint4*)(dx + (size_t)t * 8) = pack8(g);
+    }
+}
+
 int grid_for(int64_t work) {
     const int64_t g = (work + 255) / 256;
     return (int)(g < 8192 ? (g > 0 ? g : 1) : 8192);
@@ -110,5 +148,17 @@ TDL_API int tdl_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N,
     if (C % 8 || R * S > 255 || R <= 0 || S <= 0 || stride <= 0) return (int)hipErrorInvalidValue;
     maxpool_bwd_kernel<<<grid_for((int64_t)N * H * W * (C / 8)), 256, 0, s>>>((const bf16_t*)dy, arg, (bf16_t*)dx, N, H,
                                                                               W, C, P, Q, R, S, stride, pad);
+    TDL_LAUNCH_CHECK();
+}
+
+TDL_API int tdl_global_avgpool_fwd(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+    if (C % 8 || HW <= 0) return (int)hipErrorInvalidValue;
+    gap_fwd_kernel<<<grid_for((int64_t)N * (C / 8)), 256, 0, s>>>((const bf16_t*)x, (bf16_t*)y, N, HW, C);
+    TDL_LAUNCH_CHECK();
+}
+
+TDL_API int tdl_global_avgpool_bwd(const void* dy, void* dx, int N, int HW, int C, hipStream_t s) {
+    if (C % 8 || HW <= 0) return (int)hipErrorInvalidValue;
+    gap_bwd_kernel<<<grid_for((int64_t)N * HW * (C / 8)), 256, 0, s>>>((const bf16_t*)dy, (bf16_t*)dx, N, HW, C);
     TDL_LAUNCH_CHECK();
 }

@@ -266,3 +266,18 @@ def test_max_pool_nhwc_matches_torch(k, stride, pad, shape):
     yr.backward(g.float())
     assert torch.equal(y.float(), yr)
     assert float((x.grad.float() - xr.grad).abs().max()) <= 2e-2 * float(xr.grad.abs().max())
+
+
+@pytest.mark.parametrize("shape", [(4, 2048, 7, 7), (3, 64, 5, 3)])
+def test_global_avg_pool_nhwc_matches_torch(shape):
+    from trustworthy_dl.ops import global_avg_pool
+    torch.manual_seed(1)
+    x = torch.randn(shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = global_avg_pool(x)
+    g = torch.randn(y.shape, device="cuda").bfloat16()
+    y.backward(g)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.adaptive_avg_pool2d(xr, 1).flatten(1)
+    yr.backward(g.float())
+    assert _rel(y, yr) < 1e-2
+    assert _rel(x.grad, xr.grad) < 1e-2

@@ -38,9 +38,8 @@ class ClassifierHead(nn.Module):
         self.num_classes = num_classes
 
     def forward(self, x, labels=None):
-        if self.pool:
-            x = F.adaptive_avg_pool2d(x, 1)
-        logits = self.fc(torch.flatten(x, 1))
+        x = ops.global_avg_pool(x) if self.pool else torch.flatten(x, 1)
+        logits = self.fc(x)
         self._last_logits = logits
         if labels is None:
             return logits

@@ -349,6 +349,34 @@ class _MaxPoolNHWC(torch.autograd.Function):
         return dx, None, None, None
 
 
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """[N, C, H, W] (channels_last bf16) -> [N, C] mean over H*W (csrc/pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        xs = x.contiguous(memory_format=torch.channels_last)
+        y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+        _lib.call("tdl_global_avgpool_fwd", ptr(xs), ptr(y), N, H * W, C, stream_ptr(x.device))
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        _lib.call("tdl_global_avgpool_bwd", ptr(dy), ptr(dx), N, H * W, C, stream_ptr(dy.device))
+        return dx
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``F.adaptive_avg_pool2d(x, 1).flatten(1)``; native NHWC kernels for CUDA bf16 with C % 8 == 0."""
+    if native_conv_ok(x) and x.shape[1] % 8 == 0:
+        return _GlobalAvgPoolNHWC.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
 def max_pool2d(x: torch.Tensor, kernel_size: int, stride: Optional[int] = None, padding: int = 0) -> torch.Tensor:
     """``F.max_pool2d`` (square window, floor mode); native NHWC kernels for CUDA bf16 with C % 8 == 0."""
     stride = kernel_size if stride is None else stride
