@@ -288,11 +288,14 @@ def run(args):
                        "micro_batch": mbs, "micro_batches": M,
                        "parallelism": f"pp{stages}" + (f"xdp{dp}" if dp > 1 else ""),
                        "grad_verify": verify, "output_detection": verify, "trust_update": True,
+                       # deterministic stage cross-check (recompute audit; needs >= 2 stages)
+                       "stage_audit": bool(engine.cfg.audit and engine.plan.num_stages > 1),
                        "plan": engine.plan.describe(), "last_loss": engine.last_loss,
                        "detections": len(engine.attack_history),
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
-                       "native_gemm": "fc fwd+gelu, proj dgrad+dgelu, all weight gradients",
+                       "native_gemm": ("fc fwd+gelu, proj dgrad+dgelu, all weight gradients"
+                                       if os.environ.get("TDL_MLP_NATIVE", "1") != "0" else "all weight gradients"),
                        "native_wgrad": os.environ.get("TDL_WGRAD_KERNEL", "p4"),
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        # per-rank RCCL communicators / HIP streams (compute + verification + one per
