@@ -4,7 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out/prof_cnn
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_conv.log 2>&1 || { tail -30 gpurun_out/pytest_conv.log; exit 1; }
-tail -1 gpurun_out/pytest_conv.log
+true
 timeout -k 10 300 python -u bench_cnn.py --model resnet50 --image-size 224 --batch-per-gpu 64 --steps 5 --warmup 2 > gpurun_out/bench_r50.log 2>&1 || { tail -30 gpurun_out/bench_r50.log; exit 1; }
 grep metric gpurun_out/bench_r50.log
 timeout -k 10 300 python -u bench_cnn.py --model vgg16 --image-size 224 --batch-per-gpu 32 --steps 5 --warmup 2 > gpurun_out/bench_vgg16.log 2>&1 || { tail -30 gpurun_out/bench_vgg16.log; exit 1; }
