@@ -523,7 +523,30 @@ class PipelineEngine:
         """One optimizer step over the global batch.  Returns the most recent loss the host has
         read: step reports are consumed exactly ``REPORT_LAG`` steps later on every rank (so the
         host never stalls the device queue, and collective decisions such as a re-shard happen
-        at the same step everywhere); ``flush()`` drains the rest."""
+        at the same step everywhere); ``flush()`` drains the rest.
+
+        ``TDL_COMPUTE_PRIORITY=high`` (A/B): the step's compute runs on a high-priority HIP stream,
+        so the verification side stream's kernels take CUs only where the compute leaves them."""
+        hi = self._priority_stream()
+        if hi is None:
+            return self._train_step(batch)
+        cur = torch.cuda.current_stream(self.device)
+        hi.wait_stream(cur)
+        with torch.cuda.stream(hi):
+            out = self._train_step(batch)
+        cur.wait_stream(hi)
+        return out
+
+    def _priority_stream(self):
+        if self.device.type != "cuda" or os.environ.get("TDL_COMPUTE_PRIORITY", "") != "high":
+            return None
+        s = getattr(self, "_hi_stream", None)
+        if s is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            s = self._hi_stream = torch.cuda.Stream(self.device, priority=hi)
+        return s
+
+    def _train_step(self, batch: Dict[str, torch.Tensor]) -> Optional[float]:
         self.begin_step()
         progress.mark(f"step {self.global_step}: pipeline schedule")
         t0 = time.perf_counter()
