@@ -343,21 +343,48 @@ __device__ __forceinline__ void grad_partial_body(float* __restrict__ g, float* 
                                                   Moments* __restrict__ part, double* __restrict__ part_seg,
                                                   const float* __restrict__ slabs, int nsplit, int64_t seg_off,
                                                   int64_t seg_n) {
-    __shared__ Moments sh[16];
-    __shared__ float red[16];
+    __shared__ double red[12][4];
     const int64_t start = chunks[3 * c + 1], end = chunks[3 * c + 2];
     // the EMA reference (cosine feature) is kept on every REF_STRIDE-th chunk only: a 1/8 sample
     // of a stage's parameters estimates the cosine to well within its step-to-step noise at an
     // eighth of the reference traffic (read + write of an fp32 copy of the gradient)
     if (ref && (c % REF_STRIDE) != 0) ref = nullptr;
-    ThreadAcc acc;
-    acc.init();
+    // One shift for the whole chunk — the mean of the finite values among its first 64 elements
+    // (completed from the slabs in REDUCE mode), computed identically by every wave and read
+    // before any lane stores: every lane's shifted power sums are then about the same point and
+    // the block combines them by plain addition — no per-level Chan/Pebay merge of fp64 moment
+    // structs, which cost more than the 32 elements per lane themselves.
+    float shift;
+    {
+        const int64_t i0 = start + (threadIdx.x & 63);
+        float v0 = 0.f;
+        if (i0 < end) {
+            v0 = g[i0];
+            if constexpr (REDUCE) {
+                for (int s = 0; s < nsplit; ++s) v0 += slabs[(int64_t)s * seg_n + (i0 - seg_off)];
+            }
+        }
+        const bool ok = i0 < end && isfinite(v0);
+        const float num = wave_sum(ok ? v0 : 0.f), den = wave_sum(ok ? 1.f : 0.f);
+        shift = den > 0.f ? num / den : 0.f;
+    }
+    if constexpr (REDUCE) __syncthreads();
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, mn = INFINITY, mx = -INFINITY, abssum = 0.f;
+    int cnt = 0;
     float sq = 0.f, dot = 0.f, rsq = 0.f;
     int bad = 0;
     // per element: moments of the finite gradient values, the EMA reference update and the
     // gradient . reference dot product (returns the new reference value)
     auto proc = [&](float v, float r) -> float {
-        if (isfinite(v)) { acc.add(v); sq += v * v; } else ++bad;
+        if (isfinite(v)) {
+            const float d = v - shift, d2 = d * d;
+            s1 += d; s2 += d2; s3 += d2 * d; s4 += d2 * d2;
+            mn = fminf(mn, v); mx = fmaxf(mx, v); abssum += fabsf(v);
+            ++cnt;
+            sq += v * v;
+        } else {
+            ++bad;
+        }
         if (ref_valid) {
             dot += v * r;
             rsq += r * r;
@@ -434,18 +461,47 @@ __device__ __forceinline__ void grad_partial_body(float* __restrict__ g, float* 
         const float nr = proc(load1(i), ref ? ref[i] : 0.f);
         if (ref) ref[i] = nr;
     }
-    Moments r = block_merge(acc.to_moments(), sh);
-    sq = block_sum(sq, red);
-    dot = block_sum(dot, red);
-    rsq = block_sum(rsq, red);
-    const float nb = block_sum((float)bad, red);
+    // wave sums in fp64 (fixed shuffle tree), then the 4 waves in a fixed order: deterministic
+    double a[10] = {(double)cnt, (double)s1, (double)s2, (double)s3, (double)s4, (double)abssum,
+                    (double)sq, (double)dot, (double)rsq, (double)bad};
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        a[k] = wave_sum_d(a[k]);
+        if (lane == 0) red[k][wid] = a[k];
+    }
+    if (lane == 0) {
+        red[10][wid] = mn;
+        red[11][wid] = mx;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+        double t[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) t[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+        Moments r;
+        r.n = t[0];
+        r.mn = fmin(fmin(red[10][0], red[10][1]), fmin(red[10][2], red[10][3]));
+        r.mx = fmax(fmax(red[11][0], red[11][1]), fmax(red[11][2], red[11][3]));
+        r.abssum = t[5];
+        if (t[0] == 0.0) {
+            r.mean = r.m2 = r.m3 = r.m4 = 0.0;
+        } else {
+            const double N = t[0], S1 = t[1], S2 = t[2], S3 = t[3], S4 = t[4], mu = S1 / N;
+            r.mean = (double)shift + mu;
+            r.m2 = S2 - S1 * mu;
+            r.m3 = S3 - 3.0 * mu * S2 + 2.0 * S1 * mu * mu;
+            r.m4 = S4 - 4.0 * mu * S3 + 6.0 * mu * mu * S2 - 3.0 * S1 * mu * mu * mu;
+            if (r.m2 < 0.0) r.m2 = 0.0;
+        }
         part[c] = r;
-        part_seg[5 * c] = sq;
-        part_seg[5 * c + 1] = dot;
-        part_seg[5 * c + 2] = rsq;
-        part_seg[5 * c + 3] = nb;
-        part_seg[5 * c + 4] = ref ? sq : 0.0;   // |g|^2 over the reference-tracked chunks
+        part_seg[5 * c] = t[6];
+        part_seg[5 * c + 1] = t[7];
+        part_seg[5 * c + 2] = t[8];
+        part_seg[5 * c + 3] = t[9];
+        part_seg[5 * c + 4] = ref ? t[6] : 0.0;   // |g|^2 over the reference-tracked chunks
     }
 }
 
@@ -466,38 +522,38 @@ __global__ __launch_bounds__(256) void grad_reduce_partial_kernel(float* __restr
                             seg_n);
 }
 
-// One wave per segment (4 per block): lanes stride over the segment's chunks in a fixed order,
-// then a fixed-order shuffle tree.  Writes norms / cos and the segment's merged moments.
+// One workgroup per segment: each lane merges a fixed strided set of the segment's chunks (Chan /
+// Pebay, fixed order), then a fixed-order block merge — deterministic.  (One wave per segment left
+// the 6k-chunk embedding segment to 64 lanes and put an ~85 us serial merge on the step's tail.)
 __global__ __launch_bounds__(256) void grad_segment_kernel(const Moments* __restrict__ part,
                                                            const double* __restrict__ part_seg,
                                                            const int* __restrict__ seg_first, int S, int ref_valid,
                                                            float* __restrict__ out, Moments* __restrict__ seg,
                                                            float* __restrict__ nonfinite) {
-    const int sg = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (sg >= S) return;
+    __shared__ Moments sh[16];
+    __shared__ double red[5][4];
+    const int sg = blockIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     Moments m;
     m.n = 0.0; m.mean = m.m2 = m.m3 = m.m4 = 0.0; m.mn = INFINITY; m.mx = -INFINITY; m.abssum = 0.0;
-    double sq = 0.0, dot = 0.0, rsq = 0.0, bad = 0.0, sqt = 0.0;
-    for (int c = seg_first[sg] + lane; c < seg_first[sg + 1]; c += 64) {
+    double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // sq, dot, rsq, bad, sq over the reference-tracked chunks
+    for (int c = seg_first[sg] + threadIdx.x; c < seg_first[sg + 1]; c += blockDim.x) {
         merge(m, part[c]);
-        sq += part_seg[5 * c];
-        dot += part_seg[5 * c + 1];
-        rsq += part_seg[5 * c + 2];
-        bad += part_seg[5 * c + 3];
-        sqt += part_seg[5 * c + 4];
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        Moments other = shfl_xor_m(m, o);
-        if ((lane & o) == 0) merge(m, other); else { merge(other, m); m = other; }
+        for (int k = 0; k < 5; ++k) a[k] += part_seg[5 * c + k];
     }
-    sq = wave_sum_d(sq);
-    dot = wave_sum_d(dot);
-    rsq = wave_sum_d(rsq);
-    bad = wave_sum_d(bad);
-    sqt = wave_sum_d(sqt);
-    if (lane == 0) {
+    m = block_merge(m, sh);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        a[k] = wave_sum_d(a[k]);
+        if (lane == 0) red[k][wid] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) t[k] = ((red[k][0] + red[k][1]) + red[k][2]) + red[k][3];
+        const double sq = t[0], dot = t[1], rsq = t[2], bad = t[3], sqt = t[4];
         const double den = sqrt(sqt * rsq);
         out[18 + sg] = (float)sqrt(sq);
         // no tracked chunk in this segment (or no reference yet): no cosine (sentinel 2)
@@ -579,7 +635,7 @@ TDL_API int tdl_grad_stats_final(const float* g, const int64_t* table, int C, fl
     GradWs w = grad_ws(ws, C, S);
     const int* seg_first = (const int*)(table + 3 * (size_t)C);
     hipMemsetAsync(w.nonfinite, 0, sizeof(float) * 2, s);
-    grad_segment_kernel<<<(S + 3) / 4, 256, 0, s>>>(w.part, w.part_seg, seg_first, S, ref_valid, out, w.seg,
+    grad_segment_kernel<<<S, 256, 0, s>>>(w.part, w.part_seg, seg_first, S, ref_valid, out, w.seg,
                                                     w.nonfinite);
     grad_summary_kernel<<<1, 256, 0, s>>>(w.seg, S, out, w.range, w.hist, w.nonfinite);
     if (with_quantiles) {

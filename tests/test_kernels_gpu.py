@@ -264,6 +264,28 @@ def test_grad_stats_matches_cpu():
         assert torch.allclose(a[18:], b[18:], rtol=1e-3, atol=1e-4)
 
 
+def test_grad_stats_offset_and_outlier_match_cpu():
+    """The partial pass sums shifted powers about one per-chunk shift: a large common offset and a
+    huge outlier at a chunk's first element must not cost the moments their precision."""
+    from trustworthy_dl.ops.stats import CHUNK, FlatGradStats
+    sizes = [5 * CHUNK + 33, 4 * CHUNK]
+    n = sum(sizes)
+    torch.manual_seed(11)
+    for case in ("offset", "outlier"):
+        g = torch.randn(n, dtype=torch.float64) * 0.01
+        if case == "offset":
+            g += 3.0
+        else:
+            g[CHUNK] = 1e3
+            g[sizes[0]] = -5e2
+        g = g.float()
+        a = FlatGradStats(sizes, DEV).compute(g.to(DEV)).cpu()
+        b = FlatGradStats(sizes, "cpu").compute(g.clone())
+        for i in list(range(4)) + [5, 6, 9, 10, 11, 12, 13, 14, 15, 17]:
+            assert abs(float(a[i]) - float(b[i])) <= 2e-3 * max(1.0, abs(float(b[i]))), (case, i, a[i], b[i])
+        assert torch.allclose(a[18:18 + len(sizes)], b[18:18 + len(sizes)], rtol=1e-3, atol=1e-4)
+
+
 def test_grad_stats_in_pieces_match_one_pass():
     """Partial passes over arbitrary chunk ranges (the per-layer overlap path) + the final stages
     give the single pass's result; the bare clipping sum of squares matches torch."""

@@ -21,7 +21,9 @@ import torch
 
 _LIB_NAME = "libtdl_kernels.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "_native", _LIB_NAME))
+# TDL_NATIVE_LIB: another build of the same library (interleaved A/B runs of a kernel change on one
+# box, scripts/gpu_*_ab.sh); the in-tree build otherwise
+LIB_PATH = os.environ.get("TDL_NATIVE_LIB") or os.path.normpath(os.path.join(_HERE, "..", "_native", _LIB_NAME))
 
 _lib: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()

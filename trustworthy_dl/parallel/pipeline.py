@@ -997,6 +997,16 @@ class PipelineEngine:
                     dist.all_reduce(p.main_grad, group=self.tie_group)
                     break
 
+    def _index_tensor(self, nodes) -> torch.Tensor:
+        """Device index tensor of a node list, cached per list (building it is a blocking pageable
+        host-to-device copy; the present set only changes on a re-plan or an OFFLINE event)."""
+        key = tuple(nodes)
+        cache = self.__dict__.setdefault("_idx_cache", {})
+        t = cache.get(key)
+        if t is None:
+            t = cache[key] = torch.tensor(list(key), dtype=torch.long, device=self.device)
+        return t
+
     def _finish_step(self, loss, truth: Dict[int, bool]):
         tv = self.tracer.begin("verify")
         progress.mark(f"step {self.global_step}: tied-weight gradient all-reduce")
@@ -1019,7 +1029,8 @@ class PipelineEngine:
         if self.distributed:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
             if self.heartbeat is not None:
-                mine[SV.D_OFFLINE_MASK] = float(sum(1 << n for n in self.heartbeat.offline() if n < 24))
+                mine[SV.D_OFFLINE_MASK:SV.D_OFFLINE_MASK + 1].fill_(
+                    float(sum(1 << n for n in self.heartbeat.offline() if n < 24)))
             progress.mark(f"step {self.global_step}: digest all-gather")
             D = all_gather_rows(mine, self.world)
             if self.heartbeat is not None:
@@ -1046,7 +1057,7 @@ class PipelineEngine:
                 sq = sq * (1.0 - evidence)
             total_sumsq = sq.sum()
         present_nodes = self.all_ranks()
-        idx = torch.tensor(present_nodes, dtype=torch.long, device=self.device)
+        idx = self._index_tensor(present_nodes)
         raw = blame.to(torch.int32)
         # a single flag quarantines that step's update; k consecutive flags compromise the node;
         # a failed weight-integrity check (weights rewritten outside the optimizer) is definitive
@@ -1145,7 +1156,7 @@ class PipelineEngine:
                 flag, err = self._audit_verdict(rec[1], y_ref)
                 d = rows[aud]
                 d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag.to(d.device))
-                d[SV.D_AUDITED_PREV] = 1.0
+                d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
                 d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err.to(d.device))
             return
         st = self.my_stage()
@@ -1200,7 +1211,7 @@ class PipelineEngine:
             flag, err = self._audit_verdict(self._audit_inputs[m_mine], y_ref)
             d = rows[self.rank]
             d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag)
-            d[SV.D_AUDITED_PREV] = 1.0
+            d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
             d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err)
         self._audit_inputs = {}
 
@@ -1358,7 +1369,7 @@ class PipelineEngine:
         aggregated gradient (for clipping), from one extra scalar all-reduce."""
         st = self.my_stage()
         ranks = self._dp_group_ranks()
-        idx = torch.tensor(ranks, dtype=torch.long, device=self.device)
+        idx = self._index_tensor(ranks)
         rows = D[idx]
         bad = torch.maximum(rows[:, SV.D_GRAD_FLAG], (rows[:, SV.D_NONFINITE] > 0).float())
         bad = torch.maximum(bad, (self.t_status[idx] == STATUS_CODES[NodeStatus.COMPROMISED]).float())

@@ -94,7 +94,7 @@ class StageVerifier:
         self.clip_w = torch.ones(max(self.S, 1), dtype=torch.float32, device=self.device)
         self.norm_n = z(1)
         self.ctrl = z(2)
-        self.ctrl[0] = 1.0
+        self.ctrl[0:1].fill_(1.0)
         self.digest = z(DIGEST)
         self._have_out = False
         self._skip_grad_once = False
@@ -147,8 +147,11 @@ class StageVerifier:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
         d = self.digest
         d.zero_()
-        d[D_PRESENT] = 1.0
-        d[D_STAGE] = float(stage_id)
+        # scalar writes into device tensors go through fill_ (a kernel): `d[i] = 1.0` is a blocking
+        # pageable host-to-device copy that drained the whole backward before the step tail
+        # (HIP API trace: a 94 ms hipMemcpyWithStream per step, scripts/sync_probe.py)
+        d[D_PRESENT:D_PRESENT + 1].fill_(1.0)
+        d[D_STAGE:D_STAGE + 1].fill_(float(stage_id))
         if loss is not None:
             d[D_LOSS] = loss.detach().float().reshape(())
         # ---- output anomaly
@@ -178,7 +181,7 @@ class StageVerifier:
         if bare and self.grad_stats is not None and flat_grad is not None:
             # verification off: no statistics, quantiles or reference — only the clipping norm
             d[D_GRAD_SUMSQ] = self.sumsq.compute(flat_grad, self.clip_w)[0]
-            d[D_METRICS + 1] = 1.0
+            d[D_METRICS + 1:D_METRICS + 2].fill_(1.0)
         elif self.grad_stats is not None and flat_grad is not None:
             g = self.grad_stats.compute(flat_grad)
             Sn = self.S
@@ -215,19 +218,19 @@ class StageVerifier:
             self.norm_ema[:Sn].copy_(keep * (b * self.norm_ema[:Sn] + (1 - b) * norms) + (1 - keep) * self.norm_ema[:Sn])
             self.norm_n.add_(keep)
         else:
-            d[D_METRICS + 1] = 1.0
+            d[D_METRICS + 1:D_METRICS + 2].fill_(1.0)
         # ---- host-side runtime metrics (latency, utilization, error, uptime), one step lagged
         hm = torch.tensor(list(host_metrics), dtype=torch.float32).pin_memory() \
             if self.device.type == "cuda" else torch.tensor(list(host_metrics), dtype=torch.float32)
         d[D_METRICS + 2:D_METRICS + 6].copy_(hm, non_blocking=True)
         # error rate metric: any non-finite value this step counts as an error
         d[D_METRICS + 4] = torch.clamp(d[D_METRICS + 4] + (d[D_NONFINITE] > 0).float(), max=1.0)
-        d[D_ATTACK_TRUTH] = 1.0 if attack_truth else 0.0
+        d[D_ATTACK_TRUTH:D_ATTACK_TRUTH + 1].fill_(1.0 if attack_truth else 0.0)
         # ---- optimizer control block: quarantine flagged gradients on device
         if self.quarantine and gflag is not None:
             self.ctrl[1:2].copy_(torch.maximum(gflag, (d[D_NONFINITE:D_NONFINITE + 1] > 0).float()))
         else:
-            self.ctrl[1] = 0.0
+            self.ctrl[1:2].fill_(0.0)
         # clipping norm contribution: the gradient this stage will actually apply (a quarantined
         # update is skipped, so it must not shrink the honest stages' updates through the clip scale)
         if self.grad_stats is not None and flat_grad is not None and not bare:
@@ -259,7 +262,7 @@ class StageVerifier:
             tot = torch.sqrt(torch.clamp(total_sumsq, min=0.0))
             self.ctrl[0:1].copy_(torch.clamp(max_norm / (tot + 1e-6), max=1.0).reshape(1))
         else:
-            self.ctrl[0] = 1.0
+            self.ctrl[0:1].fill_(1.0)
 
     def adopt(self, other: "StageVerifier"):
         """Take over another verifier's detector state for the same parameters (a stage rebuilt
