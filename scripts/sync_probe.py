@@ -1,6 +1,7 @@
 """Where does the training step block the host on the GPU?  Runs bench.py's main with torch's CUDA
 sync debug mode on and prints every distinct Python stack that triggered a synchronising call
-(with its count).  Usage: python scripts/sync_probe.py --steps 3 --warmup 2 (bench.py arguments)."""
+(with its count).  Usage: python scripts/sync_probe.py --steps 3 --warmup 2 (bench.py arguments);
+PROBE_MODULE=bench_cnn probes the conv-net bench instead."""
 import collections
 import os
 import sys
@@ -10,7 +11,9 @@ import warnings
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-import bench  # noqa: E402
+import importlib  # noqa: E402
+
+bench = importlib.import_module(os.environ.get("PROBE_MODULE", "bench"))
 
 seen = collections.Counter()
 
