@@ -10,9 +10,16 @@
 
 namespace {
 
-// Backward reductions add into NREP replicas of the [2C] sums (replica = block % NREP): 16x less
-// same-address atomic contention than one copy; the dx kernel folds the replicas in LDS.
+// Backward sums live in NREP replicas of [2C] (the data-gradient convolutions' BN-sum epilogues
+// add into them, replica = block % NREP: 16x less same-address atomic contention than one copy);
+// bn_fold_kernel folds the replicas into the final row the dx pass reads.
 constexpr int NREP = 16;
+// Backward reduction: each row-chunk workgroup STORES its per-channel partial sums into its own
+// row of a [NB_MAX][2C] block (no atomics: the former per-block fp32 atomics into the replicas were
+// ~25 us per million on MI355X and dominated the pass for C >= 512, scripts/bench_bn.py), then
+// bn_partial_fold_kernel sums the rows in FOLD_G row groups (FOLD_G x 2C atomics in total).
+constexpr int NB_MAX = 1024;
+constexpr int FOLD_G = 16;
 
 // ---------------------------------------------------------------- forward
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ stats,
@@ -202,13 +209,30 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
                 sgx[e] += red[1][k * VPB + cvl][e];
             }
         }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float* rep = sums + (size_t)(blockIdx.x & (NREP - 1)) * 2 * C;
-            atomicAdd(rep + cv * 8 + e, sg[e]);
-            atomicAdd(rep + C + cv * 8 + e, sgx[e]);
-        }
+        float* row = sums + (size_t)(NREP + 1 + blockIdx.x) * 2 * C;
+        *(float4*)(row + cv * 8) = make_float4(sg[0], sg[1], sg[2], sg[3]);
+        *(float4*)(row + cv * 8 + 4) = make_float4(sg[4], sg[5], sg[6], sg[7]);
+        *(float4*)(row + C + cv * 8) = make_float4(sgx[0], sgx[1], sgx[2], sgx[3]);
+        *(float4*)(row + C + cv * 8 + 4) = make_float4(sgx[4], sgx[5], sgx[6], sgx[7]);
     }
+}
+
+// Sum of the nb partial rows -> replica 0 (zeroed by the forward): grid (2C / 256, FOLD_G), each
+// thread one column over the rows of its group (coalesced across the wave, 4 loads in flight).
+__global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, int nb, int C) {
+    const int col = blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= 2 * C) return;
+    const float* part = sums + (size_t)(NREP + 1) * 2 * C + col;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = blockIdx.y;
+    for (; r + 3 * FOLD_G < nb; r += 4 * FOLD_G) {
+        a0 += part[(size_t)r * 2 * C];
+        a1 += part[(size_t)(r + FOLD_G) * 2 * C];
+        a2 += part[(size_t)(r + 2 * FOLD_G) * 2 * C];
+        a3 += part[(size_t)(r + 3 * FOLD_G) * 2 * C];
+    }
+    for (; r < nb; r += FOLD_G) a0 += part[(size_t)r * 2 * C];
+    atomicAdd(sums + col, (a0 + a1) + (a2 + a3));
 }
 
 // ---------------------------------------------------------------- backward pass 2: elementwise
@@ -303,7 +327,7 @@ int grid_for(int64_t nvec) {
 }  // namespace
 
 // Floats of the replicated backward-reduction buffer for C channels (allocated with the forward).
-TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1) * 2 * C; }
+TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1 + NB_MAX) * 2 * C; }
 
 // stats: [2C] (sum, sumsq) in training mode, or null to normalise with run_mean/run_var (eval).
 // save_mean/save_rstd: [C] or null.  upd_mean/upd_var: running buffers to update (train) or null.
@@ -343,14 +367,17 @@ static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, con
     const int VPB = CV < 256 ? CV : 256;
     const int RPB = 256 / VPB;
     const int gy = (CV + VPB - 1) / VPB;
-    // ~16 blocks per CU in total (the stream needs many loads in flight), >= one 4-row unrolled
-    // iteration per thread
-    int64_t rows_per_block = (M * gy + 4095) / 4096;
+    // ~1024 workgroups in total (4 per CU, each thread >= one 4-row unrolled iteration: 12 loads
+    // in flight), at most NB_MAX row chunks (the partial rows of the workspace)
+    int64_t rows_per_block = (M * gy + 1023) / 1024;
     if (rows_per_block < 4 * RPB) rows_per_block = 4 * RPB;
+    if (rows_per_block < (M + NB_MAX - 1) / NB_MAX) rows_per_block = (M + NB_MAX - 1) / NB_MAX;
     rows_per_block = (rows_per_block + RPB - 1) / RPB * RPB;
-    const dim3 grid((unsigned)((M + rows_per_block - 1) / rows_per_block), gy);
+    const int nb = (int)((M + rows_per_block - 1) / rows_per_block);
+    const dim3 grid((unsigned)nb, gy);
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
                                                   sums, M, C, (int)rows_per_block, relu, pro);
+    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, nb, C);
     bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
     bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
         (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,
