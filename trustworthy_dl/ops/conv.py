@@ -107,6 +107,9 @@ class _Conv2dNHWC(torch.autograd.Function):
                   pad, 0, stream_ptr(x.device))
         ctx.save_for_backward(xs, weight)
         ctx.geom = (N, C, cp, H, W, Cout, R, S, P, Q, stride, pad)
+        # the statistics output never gets a gradient: without this autograd launches a zero fill
+        # for it in every backward (one per convolution per step)
+        ctx.set_materialize_grads(False)
         if stats is None:
             stats = torch.zeros(0, dtype=torch.float32, device=x.device)
         ctx.mark_non_differentiable(stats)
@@ -114,6 +117,8 @@ class _Conv2dNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None, None
         xs, weight = ctx.saved_tensors
         N, C, cp, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -239,6 +244,7 @@ class _BNActConvNHWC(torch.autograd.Function):
         ctx.sums = sums
         ctx.beta = beta  # a parameter (leaf): only its identity / main_grad is needed
         ctx.geom = (N, C, H, W, Cout, R, S, P, Q, stride, pad)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for the statistics output
         if st is None:
             st = torch.zeros(0, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(st)
@@ -246,6 +252,8 @@ class _BNActConvNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _dstats):
+        if dout is None:
+            return (None,) * 12
         ys, bnp, gamma, weight = ctx.saved_tensors
         C_ = ys.shape[1]
         pro, mean, rstd = bnp[:2 * C_], bnp[2 * C_:3 * C_], bnp[3 * C_:]
