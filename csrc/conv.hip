@@ -90,7 +90,12 @@ template <int BCO, bool TRANSPOSED, bool STATS, bool PRO = false, bool BNB = fal
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restrict__ act, const bf16_t* __restrict__ wk,
                                                          bf16_t* __restrict__ out, float* __restrict__ part,
                                                          ConvDims d, const float* __restrict__ pro,
-                                                         const bf16_t* __restrict__ bx = nullptr) {
+                                                         const bf16_t* __restrict__ bx = nullptr,
+                                                         float* __restrict__ zero_stats = nullptr) {
+    // the statistics finalize (next launch on the stream) accumulates into stats: zero it here
+    // instead of a separate memset launch per convolution
+    if (zero_stats != nullptr && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < 2 * d.Cout; i += blockDim.x) zero_stats[i] = 0.f;
     static_assert(!(PRO && TRANSPOSED), "the BN prologue applies to forward activations only");
     static_assert(!BNB || (TRANSPOSED && STATS), "BN-backward sums: data-gradient kernels with the STATS rows");
     constexpr int TCO = BCO / 64;   // 32-row cout tiles per wave (waves are 2 x 2)
@@ -501,8 +506,9 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     auto A = (const bf16_t*)act;
     auto W = (const bf16_t*)wk;
     auto O = (bf16_t*)out;
-#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr)
-#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro)
+    float* zs = (st && !stats_accumulate) ? stats : nullptr;
+#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr, nullptr, zs)
+#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, nullptr, zs)
 #define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, \
                                                                                     (const bf16_t*)bnb_x)
     if (bnb) {
@@ -522,10 +528,6 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
 #undef LAUNCHP
 #undef LAUNCHB
     if (st) {
-        if (!stats_accumulate) {
-            hipError_t e = hipMemsetAsync(stats, 0, sizeof(float) * 2 * Cout, s);
-            if (e != hipSuccess) return (int)e;
-        }
         const int rpb = 64;
         const dim3 g((2 * Cout + 63) / 64, (ntm + rpb - 1) / rpb);
         stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats);
