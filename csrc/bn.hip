@@ -62,7 +62,16 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
         // every thread of the grid-stride loop keeps the same 8 channels: fold BN into one
         // per-channel scale/shift computed once (the per-element rsqrt made this pass ALU-bound)
         const int64_t v0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
         const int c0 = (int)(v0 % CV) * 8;
+        // first activation (and residual) vector in flight before the per-channel fold below: most
+        // threads handle one or two vectors, so the fold's own loads would otherwise serialise
+        // with them (one more HBM round trip per thread)
+        uint4 xq = make_uint4(0, 0, 0, 0), rq = make_uint4(0, 0, 0, 0);
+        if (v0 < nvec) {
+            xq = ((const uint4*)x)[v0];
+            if (res) rq = ((const uint4*)res)[v0];
+        }
         float sc[8], sh[8];
         {
             float g[8], b[8];
@@ -83,12 +92,18 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
                 sh[e] = b[e] - mean * sc[e];
             }
         }
-        for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+        for (int64_t v = v0; v < nvec; v += stride) {
+            // next vector's loads issued before this one's math and store (software pipelining)
+            uint4 xn = make_uint4(0, 0, 0, 0), rn = make_uint4(0, 0, 0, 0);
+            if (v + stride < nvec) {
+                xn = ((const uint4*)x)[v + stride];
+                if (res) rn = ((const uint4*)res)[v + stride];
+            }
             float xv[8];
-            unpack8(((const uint4*)x)[v], xv);
+            unpack8(xq, xv);
             if (res) {
                 float rv[8];
-                unpack8(((const uint4*)res)[v], rv);
+                unpack8(rq, rv);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) xv[e] = fmaf(xv[e], sc[e], sh[e]) + rv[e];
             } else {
@@ -100,6 +115,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
                 for (int e = 0; e < 8; ++e) xv[e] = fmaxf(xv[e], 0.f);
             }
             ((uint4*)out)[v] = pack8(xv);
+            xq = xn;
+            rq = rn;
         }
         return;
     }

@@ -123,6 +123,44 @@ def test_conv_bn_act_train_matches_torch(relu, residual):
     assert _rel(bn.running_var, bn_r.running_var) < 2e-2
 
 
+@pytest.mark.parametrize("n,cin,cout,hw", [(64, 64, 2048, 7), (8, 64, 4096, 7), (16, 16, 64, 112)])
+def test_bn_act_production_shapes_match_fp32(n, cin, cout, hw):
+    """BN(+residual+ReLU) forward / backward at ResNet-50 stored-output BN shapes and beyond: C = 2048
+    (one channel-vector block), C = 4096 (two), and 200k rows at C = 64 (the most row chunks) —
+    the atomic-free backward reduction (partial rows + grouped fold) against an fp32 reference."""
+    from trustworthy_dl.ops.conv import conv_bn_act
+    torch.manual_seed(1)
+    conv = nn.Conv2d(cin, cout, 1, 1, 0, bias=False).cuda()
+    bn = nn.BatchNorm2d(cout).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    conv_r, bn_r = nn.Conv2d(cin, cout, 1, 1, 0, bias=False).cuda(), nn.BatchNorm2d(cout).cuda()
+    conv_r.load_state_dict(conv.state_dict())
+    bn_r.load_state_dict(bn.state_dict())
+    conv.to(torch.bfloat16)
+    bn.weight.data = bn.weight.data.to(torch.bfloat16)
+    bn.bias.data = bn.bias.data.to(torch.bfloat16)
+    conv_r.weight.data.copy_(conv.weight.data.float())
+    bn_r.weight.data.copy_(bn.weight.data.float())
+    bn_r.bias.data.copy_(bn.bias.data.float())
+    x = torch.randn(n, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(n, cout, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xn, rn = x.clone().requires_grad_(True), res.clone().requires_grad_(True)
+    out = conv_bn_act(xn, conv, bn, relu=True, residual=rn)
+    xr, rr = x.float().requires_grad_(True), res.float().requires_grad_(True)
+    ref = bn_r(conv_r(xr)) + rr
+    assert _rel(out, F.relu(ref)) < 2e-2
+    ref = ref * (out.detach() > 0).float()
+    gy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16)
+    out.backward(gy)
+    ref.backward(gy.float())
+    assert _rel(xn.grad, xr.grad) < 3e-2
+    assert _rel(rn.grad, rr.grad) < 2e-2
+    assert _rel(bn.weight.grad, bn_r.weight.grad) < 3e-2
+    assert _rel(bn.bias.grad, bn_r.bias.grad) < 3e-2
+
+
 def _chain_modules(cin, mid, cout, stride, seed):
     torch.manual_seed(seed)
     units = [(nn.Conv2d(cin, mid, 1, 1, 0, bias=False), nn.BatchNorm2d(mid)),
