@@ -605,6 +605,16 @@ class PipelineEngine:
         if self.attacker is not None and hasattr(self.attacker, "on_parameters"):
             if self.attacker.on_parameters(node, st.flat, self.global_step):
                 truth[node] = True
+        # the stage's weights are final for this step from here on: take the integrity checksum now,
+        # on the verifier's side stream, overlapped with the forward / backward instead of serially
+        # on the step's tail (_integrity_flag picks it up after finish_step joined the side stream)
+        side = getattr(st.verifier, "side", None)
+        if self.cfg.param_integrity and side is not None and st.flat.data.is_cuda:
+            cur = torch.cuda.current_stream(st.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                st._early_checksum = dstats.checksum(st.flat.data)
+            st._early_checksum.record_stream(cur)
 
     def _attack_output(self, node: int, y: torch.Tensor, truth: Dict[int, bool]) -> torch.Tensor:
         if self.attacker is not None and hasattr(self.attacker, "on_output"):
@@ -1242,7 +1252,9 @@ class PipelineEngine:
     def _integrity_flag(self, st: Stage) -> torch.Tensor:
         """1.0 when the stage's compute weights differ from the checksum taken right after its last
         optimizer step (a write outside the optimizer), else 0.0 — device-side, no sync."""
-        cur = dstats.checksum(st.flat.data)
+        cur = st.__dict__.pop("_early_checksum", None)
+        if cur is None:
+            cur = dstats.checksum(st.flat.data)
         ref = getattr(st, "param_checksum", None)
         if ref is None:  # first step / freshly (re)built or reloaded stage: nothing to compare yet
             st.param_checksum = cur

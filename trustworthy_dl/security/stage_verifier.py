@@ -84,6 +84,9 @@ class StageVerifier:
             self.out_det = S.DeviceZScore(3, self.device, z_decision=z_out, **kw)
             self.grad_det = S.DeviceZScore(3, self.device, z_decision=z_grad, **kw)
         self.sign_flip_cos = float(sign_flip_cos)
+        # the median / quartile histograms feed only the reference feature set (all 17 / 12
+        # statistics); the targeted detectors never read them, so they are not computed
+        self._quantiles = features == "reference"
         self.grad_stats = S.FlatGradStats(param_sizes, self.device) if len(param_sizes) else None
         self.sumsq = S.FlatSumSq(param_sizes, self.device)
         self.S = len(param_sizes)
@@ -113,10 +116,10 @@ class StageVerifier:
             cur = torch.cuda.current_stream(self.device)
             self.side.wait_stream(cur)
             with torch.cuda.stream(self.side):
-                S.tensor_stats(y.detach(), out=self.out_stats)
+                S.tensor_stats(y.detach(), with_quantiles=self._quantiles, out=self.out_stats)
             y.record_stream(self.side)
         else:
-            self.out_stats.copy_(S.tensor_stats(y.detach()))
+            self.out_stats.copy_(S.tensor_stats(y.detach(), with_quantiles=self._quantiles))
         self._have_out = True
 
     # ---------------------------------------------------------------- gradient path + digest
@@ -183,7 +186,7 @@ class StageVerifier:
             d[D_GRAD_SUMSQ] = self.sumsq.compute(flat_grad, self.clip_w)[0]
             d[D_METRICS + 1:D_METRICS + 2].fill_(1.0)
         elif self.grad_stats is not None and flat_grad is not None:
-            g = self.grad_stats.compute(flat_grad)
+            g = self.grad_stats.compute(flat_grad, with_quantiles=self._quantiles)
             Sn = self.S
             norms = g[18:18 + Sn]
             sumsq = (norms * norms * self.clip_w[:Sn]).sum()
