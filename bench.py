@@ -265,6 +265,7 @@ def run(args):
     el = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}" if use_cuda else "cpu")
     hwq_all = [hwq]
     inv = engine.comm_inventory()
+    inv["audit"] = engine.audit_summary()
     inv_all = [inv]
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -304,6 +305,9 @@ def run(args):
                        "hip_streams_per_rank": [i["hip_streams"] for i in inv_all],
                        "process_groups_created": inv["groups_created"],
                        "within_queue_budget": all(i["within_queue_budget"] for i in inv_all),
+                       # recompute audit (forward + backward) per rank and step: P2P bytes, host and
+                       # device time of the audit phase (inside the timed steps)
+                       "audit_per_rank": [i.get("audit", {}) for i in inv_all],
                        "reassignments": [{"step": r["step"], "from_nodes": r["from_nodes"],
                                           "migration_ms": round(1000 * r["migration_time"], 2),
                                           "plan": r["plan"]} for r in engine.reassignment_history]},

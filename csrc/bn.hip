@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16_t* __restric
 // per-channel scale / shift the convolution used (pro = [scale | shift]).
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
                                                                 const bf16_t* __restrict__ x, const float* __restrict__ mean,
-                                                                const float* __restrict__ rstd, float* __restrict__ sums,
+                                                                const float* __restrict__ rstd, float* __restrict__ part,
                                                                 int64_t M, int C, int rows_per_block, int relu,
                                                                 const float* __restrict__ pro) {
     __shared__ float red[2][256][8];
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
                 sgx[e] += red[1][k * VPB + cvl][e];
             }
         }
-        float* row = sums + (size_t)(NREP + 1 + blockIdx.x) * 2 * C;
+        float* row = part + (size_t)blockIdx.x * 2 * C;
         *(float4*)(row + cv * 8) = make_float4(sg[0], sg[1], sg[2], sg[3]);
         *(float4*)(row + cv * 8 + 4) = make_float4(sg[4], sg[5], sg[6], sg[7]);
         *(float4*)(row + C + cv * 8) = make_float4(sgx[0], sgx[1], sgx[2], sgx[3]);
@@ -236,10 +236,11 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
 
 // Sum of the nb partial rows -> replica 0 (zeroed by the forward): grid (2C / 256, FOLD_G), each
 // thread one column over the rows of its group (coalesced across the wave, 4 loads in flight).
-__global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, int nb, int C) {
+__global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, const float* __restrict__ partials,
+                                                              int nb, int C) {
     const int col = blockIdx.x * blockDim.x + threadIdx.x;
     if (col >= 2 * C) return;
-    const float* part = sums + (size_t)(NREP + 1) * 2 * C + col;
+    const float* part = partials + col;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int r = blockIdx.y;
     for (; r + 3 * FOLD_G < nb; r += 4 * FOLD_G) {
@@ -344,7 +345,10 @@ int grid_for(int64_t nvec) {
 }  // namespace
 
 // Floats of the replicated backward-reduction buffer for C channels (allocated with the forward).
-TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1 + NB_MAX) * 2 * C; }
+// (replicas + their sum; kept from the forward to the backward, so only (NREP + 1) x 2C)
+TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1) * 2 * C; }
+// Floats of the backward's per-block partial rows (scratch of ONE backward call, not kept).
+TDL_API int64_t tdl_bn_bwd_part_floats(int C) { return (int64_t)NB_MAX * 2 * C; }
 
 // stats: [2C] (sum, sumsq) in training mode, or null to normalise with run_mean/run_var (eval).
 // save_mean/save_rstd: [C] or null.  upd_mean/upd_var: running buffers to update (train) or null.
@@ -377,9 +381,9 @@ TDL_API int tdl_bn_finalize(const float* stats, const void* gamma, const void* b
 }
 
 static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
-                           const void* gamma, float* sums, void* dx, void* dres, float* dgamma, float* dbeta, int64_t M,
-                           int C, int relu, const float* pro, hipStream_t s) {
-    if (C % 8 != 0 || (relu && out == nullptr && pro == nullptr)) return (int)hipErrorInvalidValue;
+                           const void* gamma, float* sums, float* part, void* dx, void* dres, float* dgamma, float* dbeta,
+                           int64_t M, int C, int relu, const float* pro, hipStream_t s) {
+    if (C % 8 != 0 || (relu && out == nullptr && pro == nullptr) || part == nullptr) return (int)hipErrorInvalidValue;
     const int CV = C / 8;
     const int VPB = CV < 256 ? CV : 256;
     const int RPB = 256 / VPB;
@@ -393,8 +397,8 @@ static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, con
     const int nb = (int)((M + rows_per_block - 1) / rows_per_block);
     const dim3 grid((unsigned)nb, gy);
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
-                                                  sums, M, C, (int)rows_per_block, relu, pro);
-    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, nb, C);
+                                                  part, M, C, (int)rows_per_block, relu, pro);
+    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, part, nb, C);
     bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
     bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
         (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,
@@ -402,11 +406,12 @@ static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, con
     TDL_LAUNCH_CHECK();
 }
 
-// sums: the forward's bwd_ws (zeroed there).  dgamma/dbeta: fp32 accumulators (+=) or null.
+// sums: the forward's bwd_ws (zeroed there); part: tdl_bn_bwd_part_floats(C) floats of scratch.
+// dgamma/dbeta: fp32 accumulators (+=) or null.
 TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, const float* mean, const float* rstd,
-                           const void* gamma, float* sums, void* dx, void* dres, float* dgamma, float* dbeta, int64_t M,
-                           int C, int relu, hipStream_t s) {
-    return bn_act_bwd_impl(dout, out, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, M, C, relu, nullptr, s);
+                           const void* gamma, float* sums, float* part, void* dx, void* dres, float* dgamma, float* dbeta,
+                           int64_t M, int C, int relu, hipStream_t s) {
+    return bn_act_bwd_impl(dout, out, x, mean, rstd, gamma, sums, part, dx, dres, dgamma, dbeta, M, C, relu, nullptr, s);
 }
 
 // Backward of a folded BN (+ ReLU) whose two per-channel sums were already reduced (into the first
@@ -425,7 +430,7 @@ TDL_API int tdl_bn_act_bwd_pro_summed(const void* dout, const void* x, const flo
 
 // Backward of a folded BN (+ ReLU): no stored output, the mask is recomputed from x with pro.
 TDL_API int tdl_bn_act_bwd_pro(const void* dout, const void* x, const float* mean, const float* rstd, const void* gamma,
-                               const float* pro, float* sums, void* dx, float* dgamma, float* dbeta, int64_t M, int C,
-                               int relu, hipStream_t s) {
-    return bn_act_bwd_impl(dout, nullptr, x, mean, rstd, gamma, sums, dx, nullptr, dgamma, dbeta, M, C, relu, pro, s);
+                               const float* pro, float* sums, float* part, void* dx, float* dgamma, float* dbeta, int64_t M,
+                               int C, int relu, hipStream_t s) {
+    return bn_act_bwd_impl(dout, nullptr, x, mean, rstd, gamma, sums, part, dx, nullptr, dgamma, dbeta, M, C, relu, pro, s);
 }

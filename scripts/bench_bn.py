@@ -44,6 +44,7 @@ def main():
         mean = torch.empty(C, device=dev)
         rstd = torch.empty(C, device=dev)
         ws = torch.zeros(int(L.tdl_bn_bwd_ws_floats(C)), device=dev)
+        part = torch.empty(int(L.tdl_bn_bwd_part_floats(C)), device=dev)
         dx, dres = torch.empty_like(x), (torch.empty_like(x) if res else None)
         dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
         s = stream_ptr(dev)
@@ -54,7 +55,7 @@ def main():
 
         def bwd():
             ws.zero_()
-            _lib.call("tdl_bn_act_bwd", ptr(dout), ptr(out), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(ws),
+            _lib.call("tdl_bn_act_bwd", ptr(dout), ptr(out), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(ws), ptr(part),
                       ptr(dx), ptr(dres), ptr(dg), ptr(db), M, C, 1, s)
 
         def zero():

@@ -43,6 +43,21 @@ CONFIGS = {
 
 
 CONFIGS["clean"] = dict(model="gpt2-medium", attack=None, targets=[], lr=1e-4)
+# round 4 (backward audit): sign-flip gradient poisoning (reference F1 0.0), activation-gradient
+# (dX) tampering, the loss stage tampering its dX, single-micro-batch (one-of-M) adversaries, and a
+# model-poisoning rank that lies about its own integrity check
+CONFIGS["3s"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip"),
+                     targets=[3], lr=1e-4)
+CONFIGS["dx"] = dict(model="gpt2-medium", attack=dict(attack_types=["byzantine_backward"], intensity=0.5),
+                     targets=[4], lr=1e-4)
+CONFIGS["last"] = dict(model="gpt2-medium", attack=dict(attack_types=["byzantine_backward"], intensity=0.5),
+                       targets=[7], lr=1e-4)
+CONFIGS["3m"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip",
+                                                      micro_batches=1), targets=[3], lr=1e-4)
+CONFIGS["5m"] = dict(model="gpt2-medium", attack=dict(attack_types=["byzantine"], intensity=0.5, micro_batches=1),
+                     targets=[2, 5], lr=1e-4)
+CONFIGS["liar"] = dict(model="gpt2-medium", attack=dict(attack_types=["model_poisoning"], intensity=0.05,
+                                                        lie_integrity=True), targets=[6], lr=1e-4)
 
 
 def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_len: int, p_attack: float,
@@ -77,8 +92,11 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
     data = (MarkovLanguageModeling(batch, seq_len, 8192, num_batches=steps, seed=1) if gpt else
             SyntheticImages(batch, img, ncls, num_batches=steps, seed=1))
     t0 = time.perf_counter()
-    for b in data:
+    for i, b in enumerate(data):
         eng.train_step(b)
+        if i % 50 == 49:   # progress (a long run must not look hung)
+            print(f"[cfg {cfg_id} seed {seed}] step {i + 1}/{steps} {time.perf_counter() - t0:.0f}s",
+                  file=sys.stderr, flush=True)
     eng.flush()
     if device.startswith("cuda"):
         torch.cuda.synchronize()
@@ -88,6 +106,15 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
     rs = eng.reassignment_history
     first_attack = min(att.first_attack_step.values()) if att is not None and att.first_attack_step else None
     clean_blamed = sorted({r["node_id"] for r in eng.attack_history if not r.get("ground_truth")})
+    # per target: first tampered step, first detection, first re-shard away from it (reports late)
+    lag = {}
+    for n in c["targets"]:
+        inj = sorted(i["step"] for i in (att.injections if att is not None else []) if i["node"] == n)
+        det = sorted(r["step"] for r in eng.attack_history if r["node_id"] == n and r.get("ground_truth"))
+        rsh = sorted(r["step"] for r in rs if n in r["from_nodes"])
+        lag[str(n)] = {"first_tamper": inj[0] if inj else None, "first_detect": det[0] if det else None,
+                       "reshard": rsh[0] if rsh else None,
+                       "tampered_reports_before_reshard": (len([s for s in inj if s <= rsh[0]]) if inj and rsh else None)}
     compromised = [n for n in range(8) if eng.trust.get_node_status(n).value == "compromised"]
     rec = {
         "config": cfg_id, "seed": seed, "reassign": reassign, "audit": audit,
@@ -99,6 +126,8 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
         "detection": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in m.items()
                       if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
         "injections": len(att.injections) if att is not None else 0,
+        "tampered_steps": len({(i["node"], i["step"]) for i in att.injections}) if att is not None else 0,
+        "per_target": lag, "micro_batches": max(1, batch // mbs),
         "clean_nodes_blamed": clean_blamed,
         "clean_nodes_compromised": [n for n in compromised if n not in c["targets"]],
         "clean_nodes_resharded": sorted({n for r in rs for n in r["from_nodes"] if n not in c["targets"]}),
@@ -108,6 +137,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
                       "estimated_ms": round(1000 * r["estimated_migration_time"], 2),
                       "phases_ms": {k: round(1000 * v, 2) for k, v in r.get("phases", {}).items() if k.endswith("_s")},
                       "moved_params": r["moved_params"], "restored_from_shadow": r.get("restored_from_shadow"),
+                      "restored_from_initial": r.get("restored_from_initial"),
                       "plan": r["plan"]} for r in rs],
         "plan_before": plan0, "plan_after": eng.plan.describe(), "num_stages_after": eng.plan.num_stages,
         "final_trust": [round(eng.trust.get_trust_score(n), 3) for n in range(8)],
@@ -123,7 +153,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean")
+    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean, 3s, dx, last, 3m, 5m, liar")
     ap.add_argument("--seeds", default="3", help="comma list of attacker / monitor seeds")
     ap.add_argument("--no-reassign", action="store_true", help="detection only: the target keeps its layers, so "
                     "every injection is scored (a re-shard ends the attack after the first detections)")
@@ -139,7 +169,7 @@ def main():
     ap.add_argument("--small", action="store_true", help="tiny models (CPU smoke of the same flow)")
     ap.add_argument("--detector-warmup", type=int, default=50)
     args = ap.parse_args()
-    for cid in [x if x == "clean" else int(x) for x in args.configs.split(",")]:
+    for cid in [int(x) if x.isdigit() else x for x in args.configs.split(",")]:
         for seed in [int(x) for x in args.seeds.split(",")]:
             rec = run(cid, args.device, args.steps, args.start, args.batch, args.mbs, args.seq_len, args.p_attack,
                       args.small, args.detector_warmup, seed=seed, reassign=not args.no_reassign,

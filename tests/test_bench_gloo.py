@@ -61,8 +61,16 @@ def test_bench_multirank_json_line(n, mode):
             assert c == 1 + groups and streams[r] == c + 1, (r, comms, streams)
             continue
         i = ranks.index(r)
-        peers = (i > 0) + (i < len(ranks) - 1)
-        assert c == 1 + groups + (tie if i in (0, len(ranks) - 1) else 0) + per_peer * peers, (r, comms)
+        S = len(ranks)
+        nb = ({i - 1} if i > 0 else set()) | ({i + 1} if i < S - 1 else set())
+        # trusted weight snapshots (taken at build time and every shadow_interval steps) travel on
+        # the default group to the next min(2, S - 1) stages of the ring, and in from the previous ones
+        k = min(2, S - 1)
+        ring = {(i + dd) % S for dd in range(1, k + 1)} | {(i - dd) % S for dd in range(1, k + 1)}
+        default_peers = (ring | nb) if mode == "grouped" else ring
+        dir_peers = nb if mode == "async" else set()
+        expect = 1 + groups + (tie if i in (0, S - 1) else 0) + 2 * len(dir_peers) + len(default_peers)
+        assert c == expect, (r, comms, expect)
         assert streams[r] == c + 2                    # + compute stream + verification side stream
     assert max(streams) <= 32
 

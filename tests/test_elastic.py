@@ -145,3 +145,25 @@ def test_trust_follows_physical_node_after_losing_rank1(monkeypatch):
     _resize_trust(tr2, saved, 2)
     assert tr2.trust_manager.get_node_status(0) == NodeStatus.COMPROMISED
     assert tr2.engine.excluded == [0]
+
+
+def test_resume_plan_leaves_excluded_physical_node_out(monkeypatch):
+    """saved plan [0, 2] with node 1 excluded, then rank 0 is lost.  The survivors are
+    physical nodes 1, 2 (new ranks 0, 1): the saved stage of node 2 runs on new rank 1, node 0's
+    stage is gone, so the plan is re-planned — and never onto new rank 0 (compromised node 1)."""
+    import torch
+    from trustworthy_dl.utils.checkpoint import resume_plan_ranks
+    ck = {"node_ids": [0, 1, 2], "excluded": [1], "device_trust": {"values": torch.ones(3)}}
+    monkeypatch.setenv("TDL_ELASTIC_NODE_IDS", "1,2")
+    moved, live_ex = resume_plan_ranks(ck, [0, 2], live=2, pp=2)
+    assert moved is None and live_ex == [0]
+    live = [r for r in range(2) if r not in live_ex]
+    assert live == [1]
+    # losing node 1 (the excluded one) instead: the saved plan is hostable, its ranks translated
+    monkeypatch.setenv("TDL_ELASTIC_NODE_IDS", "0,2")
+    moved, live_ex = resume_plan_ranks(ck, [0, 2], live=2, pp=2)
+    assert moved == [0, 1] and live_ex == []
+    # a plan that put a stage on the excluded node is never adopted
+    monkeypatch.setenv("TDL_ELASTIC_NODE_IDS", "0,1,2")
+    moved, live_ex = resume_plan_ranks(ck, [0, 1], live=3, pp=3)
+    assert moved is None and live_ex == [1]

@@ -102,7 +102,9 @@ def test_byzantine_output_tamper_detected():
 
 
 def test_reshard_preserves_function_and_optimizer_state():
-    eng = _engine(nodes=3, reassign=False)
+    # a re-shard never takes a compromised node's layers from its own memory: they come from its
+    # last committed snapshot, which with a snapshot every step is the state of the last step
+    eng = _engine(nodes=3, reassign=False, shadow_interval=1)
     for b in _batches(5):
         eng.train_step(b)
     eng.flush()
@@ -266,7 +268,7 @@ def test_shadow_snapshot_restores_compromised_stage():
         eng.train_step(b)
     eng.flush()
     assert 1 in eng._shadow_meta and eng._shadow_meta[1][2] == 2   # node 1's copy lives on node 2
-    snap_step, (a, b), _ = eng._shadow_meta[1]
+    snap_step, (a, b), _, _ = eng._shadow_meta[1]
     st1 = eng.stages[1]
     assert st1.layer_range == (a, b)
     snap = torch.cat([eng._pack_layer(st1, li) for li in range(a, b)]).clone()

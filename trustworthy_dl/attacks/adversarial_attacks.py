@@ -15,7 +15,17 @@ of experiment_runner.py:439-451):
   zeroed before verification (``gradient_mode``);
 * ``model_poisoning`` (param perturbation) — the stage's weights are multiplicatively perturbed;
 * ``byzantine`` — the stage's output activations are tampered before they are sent downstream;
+* ``byzantine_backward`` — the activation gradient the stage sends UPSTREAM (its input gradient)
+  is tampered (sign flip + relative noise), the backward-pass counterpart of ``byzantine``;
 * ``data_poisoning`` — labels are flipped and inputs perturbed in the batch (consumed by stage 0).
+
+``micro_batches`` (k) restricts the per-micro-batch attacks to k of the step's M micro-batches
+(chosen by the attacker's own per-step hash): ``byzantine`` / ``byzantine_backward`` tamper only
+those, and ``gradient_poisoning`` then acts INSIDE the backward, on those micro-batches'
+weight-gradient contributions (sign-flipped / scaled / zeroed / noised as ``gradient_mode`` says)
+instead of on the step's accumulated gradient — the one-of-M adversary that a one-micro-batch
+audit catches with probability k / M per step.  ``lie_integrity``: the target's engine reports a
+passing weight-integrity check whatever it measured (a rank that lies about its own checksum).
 """
 from __future__ import annotations
 
@@ -33,7 +43,7 @@ from ..ops.attack import AttackMode, inject_
 
 logger = logging.getLogger(__name__)
 
-ATTACK_TYPES = ("gradient_poisoning", "model_poisoning", "byzantine", "data_poisoning",
+ATTACK_TYPES = ("gradient_poisoning", "model_poisoning", "byzantine", "byzantine_backward", "data_poisoning",
                 "backdoor", "adversarial_input")
 _GRAD_MODES = {"scale": AttackMode.SCALE, "noise": AttackMode.REL_NOISE, "sign_flip": AttackMode.SIGN_FLIP,
                "zero": AttackMode.ZERO, "additive_noise": AttackMode.NOISE}
@@ -52,6 +62,8 @@ class AttackConfig:
     param_noise: Optional[float] = None      # relative weight noise, default intensity
     activation_noise: Optional[float] = None  # relative activation noise, default 4 * intensity
     label_flip_fraction: Optional[float] = None  # default intensity
+    micro_batches: Optional[int] = None  # tamper only this many of the step's micro-batches (None: all)
+    lie_integrity: bool = False          # the target reports its weight-integrity check as passing
     seed: int = 1234
 
     def grad_factor(self) -> float:
@@ -95,6 +107,26 @@ class AdversarialAttacker:
         h = hashlib.blake2b(f"{c.seed}:{kind}:{node}:{step}".encode(), digest_size=8).digest()
         return int.from_bytes(h, "little") / 2.0 ** 64 < c.probability
 
+    def micro_fires(self, kind: str, node: int, step: int, micro: Optional[int], num_micro: Optional[int]) -> bool:
+        """Does ``kind`` hit micro-batch ``micro`` of ``num_micro`` at this step?  With
+        ``micro_batches = k`` the attacker tampers k micro-batches per step, picked by its own hash
+        of (seed, node, step) — independent of the auditor's private choice."""
+        if not self._fires(kind, node, step):
+            return False
+        k = self.config.micro_batches
+        if k is None or micro is None or not num_micro or k >= num_micro:
+            return True
+        h = hashlib.blake2b(f"{self.config.seed}:micro:{kind}:{node}:{step}".encode(), digest_size=8).digest()
+        rng = np.random.default_rng(int.from_bytes(h, "little"))
+        return int(micro) in set(rng.choice(int(num_micro), size=int(k), replace=False).tolist())
+
+    def per_micro_gradients(self) -> bool:
+        """Gradient poisoning acts inside the backward (on k micro-batches' contributions)."""
+        return self.config.micro_batches is not None and "gradient_poisoning" in self.config.attack_types
+
+    def lies_about_integrity(self, node: int, step: int) -> bool:
+        return self.config.lie_integrity and self.active and node in self.config.target_nodes
+
     def _log(self, kind: str, node: int, step: int, **info):
         self.injections.append({"type": kind, "node": node, "step": step, "timestamp": time.time(), **info})
         self.counts[kind] += 1
@@ -104,18 +136,54 @@ class AdversarialAttacker:
         return (self.config.seed * 1_000_003 + node * 7919 + step) & 0xFFFFFFFFFFFF
 
     # ---------------------------------------------------------------- engine hooks
-    def on_gradients(self, node: int, flat_grad: torch.Tensor, step: int) -> bool:
-        if not self._fires("gradient_poisoning", node, step):
-            return False
+    def _grad_magnitude(self, g: torch.Tensor):
         c = self.config
         mode = _GRAD_MODES[c.gradient_mode]
         a = {AttackMode.SCALE: c.grad_factor(), AttackMode.REL_NOISE: 10.0 * c.intensity,
              AttackMode.SIGN_FLIP: 1.0, AttackMode.ZERO: 0.0, AttackMode.NOISE: c.intensity}[mode]
         if mode == AttackMode.NOISE:  # absolute noise scaled to the gradient's RMS
-            a = float(c.intensity * 10.0 * flat_grad.float().pow(2).mean().sqrt().item() + 1e-12)
+            a = float(c.intensity * 10.0 * g.float().pow(2).mean().sqrt().item() + 1e-12)
+        return mode, a
+
+    def on_gradients(self, node: int, flat_grad: torch.Tensor, step: int) -> bool:
+        if self.per_micro_gradients() or not self._fires("gradient_poisoning", node, step):
+            return False
+        mode, a = self._grad_magnitude(flat_grad)
         inject_(flat_grad, mode, a, self._seed(node, step), 0)
-        self._log("gradient_poisoning", node, step, mode=c.gradient_mode, magnitude=a)
+        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a)
         return True
+
+    # gradient poisoning inside the backward (``micro_batches`` set): the engine calls
+    # before_micro_backward / after_micro_backward around each micro-batch's backward of the stage
+    # (its weight-gradient contribution d = G_after - G_before), and the attack rewrites d in place
+    def before_micro_backward(self, node: int, flat_grad: torch.Tensor, step: int, micro: int, num_micro: int):
+        if self.per_micro_gradients() and self.micro_fires("gradient_poisoning", node, step, micro, num_micro):
+            self._gsnap = (node, step, micro, flat_grad.detach().clone())
+
+    def after_micro_backward(self, node: int, flat_grad: torch.Tensor, step: int, micro: int, num_micro: int) -> bool:
+        snap = getattr(self, "_gsnap", None)
+        if snap is None or snap[:3] != (node, step, micro):
+            return False
+        self._gsnap = None
+        before = snap[3]
+        d = flat_grad - before
+        mode, a = self._grad_magnitude(d)
+        inject_(d, mode, a, self._seed(node, step) + micro, 0)
+        flat_grad.copy_(before + d)
+        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a, micro=micro)
+        return True
+
+    def on_input_grad(self, node: int, dx: torch.Tensor, step: int, micro: Optional[int] = None,
+                      num_micro: Optional[int] = None) -> Optional[torch.Tensor]:
+        """Byzantine backward: tamper the activation gradient the stage sends upstream."""
+        if not self.micro_fires("byzantine_backward", node, step, micro, num_micro):
+            return None
+        a = self.config.activation_noise if self.config.activation_noise is not None else 4.0 * self.config.intensity
+        out = dx.detach().clone().contiguous()
+        inject_(out, AttackMode.REL_NOISE, a, self._seed(node, step) + (micro or 0), 0)
+        inject_(out, AttackMode.SIGN_FLIP, 1.0)
+        self._log("byzantine_backward", node, step, magnitude=a, micro=micro)
+        return out
 
     def on_parameters(self, node: int, flat, step: int) -> bool:
         if not self._fires("model_poisoning", node, step):
@@ -127,17 +195,18 @@ class AdversarialAttacker:
         self._log("model_poisoning", node, step, magnitude=a)
         return True
 
-    def on_output(self, node: int, y: torch.Tensor, step: int) -> Optional[torch.Tensor]:
-        if not self._fires("byzantine", node, step):
+    def on_output(self, node: int, y: torch.Tensor, step: int, micro: Optional[int] = None,
+                  num_micro: Optional[int] = None) -> Optional[torch.Tensor]:
+        if not self.micro_fires("byzantine", node, step, micro, num_micro):
             return None
         a = self.config.activation_noise if self.config.activation_noise is not None else 4.0 * self.config.intensity
         yt = y.detach()
         if not yt.is_contiguous():
             return None
         # in place, before any consumer has read the activation (the producer saved none of it)
-        inject_(yt, AttackMode.REL_NOISE, a, self._seed(node, step), 0)
+        inject_(yt, AttackMode.REL_NOISE, a, self._seed(node, step) + (micro or 0), 0)
         inject_(yt, AttackMode.SIGN_FLIP, 1.0)
-        self._log("byzantine", node, step, magnitude=a)
+        self._log("byzantine", node, step, magnitude=a, micro=micro)
         return y
 
     def apply_attacks(self, batch: Dict[str, torch.Tensor], batch_idx: int) -> Dict[str, torch.Tensor]:

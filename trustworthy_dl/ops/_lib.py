@@ -131,9 +131,10 @@ _SIGNATURES = {
     "tdl_conv_wgrad": [_P] * 4 + [_I] * 12 + [_P],
     "tdl_bn_act_fwd": [_P] * 13 + [_L, _I, _F, _F, _I, _P],
     "tdl_bn_bwd_ws_floats": [_I],
-    "tdl_bn_act_bwd": [_P] * 11 + [_L, _I, _I, _P],
+    "tdl_bn_act_bwd": [_P] * 12 + [_L, _I, _I, _P],
+    "tdl_bn_bwd_part_floats": [_I],
     "tdl_bn_finalize": [_P] * 9 + [_L, _I, _F, _F, _P],
-    "tdl_bn_act_bwd_pro": [_P] * 10 + [_L, _I, _I, _P],
+    "tdl_bn_act_bwd_pro": [_P] * 11 + [_L, _I, _I, _P],
     "tdl_conv_nt_pro": [_P] * 5 + [_I] * 11 + [_P, _P],
     "tdl_conv_wgrad_pro": [_P] * 4 + [_I] * 12 + [_P, _P],
 }

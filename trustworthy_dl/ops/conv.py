@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import ptr, stream_ptr
+from .layers import _scratch
 
 _NUM_CU = {}
 
@@ -197,7 +198,9 @@ class _BatchNormActNHWC(torch.autograd.Function):
         mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
         dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
         db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
-        _lib.call("tdl_bn_act_bwd", ptr(dout), ptr(out), ptr(y), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums), ptr(dx),
+        # the per-block partial rows are scratch of this call only (not kept from the forward)
+        part = _scratch(int(_lib.lib().tdl_bn_bwd_part_floats(C)), dev)
+        _lib.call("tdl_bn_act_bwd", ptr(dout), ptr(out), ptr(y), ptr(mean), ptr(rstd), ptr(gamma), ptr(sums), ptr(part), ptr(dx),
                   ptr(dres), ptr(dg), ptr(db), M, C, int(relu), stream_ptr(dev))
         gg = None if mg_g is not None else dg.to(gamma.dtype)
         gb = None if mg_b is not None else db.to(beta.dtype)

@@ -93,6 +93,16 @@ class FlatParams:
             p.main_grad = self.grad[o:o + s].view(shp)
             p.grad = None
 
+    def set_grad_buffer(self, buf: torch.Tensor) -> torch.Tensor:
+        """Re-point every parameter's ``main_grad`` at ``buf`` (same layout as ``grad``) and return
+        the previous accumulator: the backward audit recomputes one micro-batch's gradient into a
+        scratch buffer without touching the step's accumulated gradient."""
+        old = self.grad
+        self.grad = buf
+        for p, o, s, shp in zip(self.params, self.offsets, self.sizes, self.shapes):
+            p.main_grad = buf[o:o + s].view(shp)
+        return old
+
     def view(self, buf: torch.Tensor, i: int) -> torch.Tensor:
         return buf[self.offsets[i]:self.offsets[i + 1]].view(self.shapes[i])
 

@@ -81,14 +81,27 @@ class EngineConfig:
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
-                                         # (0 = off); a compromised stage is restored from it, not from itself
+                                         # (0 = off); a compromised stage is restored from it, not from itself.
+                                         # A snapshot is also taken when the stages are (re)built
+    shadow_copies: int = 2               # holders per snapshot (the next 1-2 stages of the ring): a stage
+                                         # whose first holder is compromised too is still restorable
     audit: bool = True                   # deterministic stage cross-check: the next stage recomputes every
                                          # non-loss stage's monitored micro-batch from its input and weights and
                                          # compares the output it received; blame for a tampered forward comes
                                          # only from such a mismatch or a failed weight-integrity check, output
                                          # z-scores no longer blame (they stay in the trust metrics)
-    audit_prob: float = 1.0              # fraction of steps audited (drawn from the private monitor RNG)
+    audit_prob: float = 1.0              # fraction of steps audited (drawn privately by each auditor)
     audit_tol: float = 1e-2              # relative max error above which a recomputed output mismatches
+    audit_backward: bool = True          # the audit covers the backward too: the auditor recomputes the
+                                         # audited micro-batch's input gradient and the sketch of its
+                                         # weight-gradient contribution (security/grad_audit.py), the
+                                         # loss stage is audited by its predecessor, and every stage's
+                                         # applied gradient must equal the sum of its committed
+                                         # per-micro-batch contributions; gradient z-scores then no longer
+                                         # blame (they quarantine the update and feed the trust metrics)
+    audit_grad_tol: float = 0.05         # relative sketch error above which a gradient check fails
+    compromise_on_proof: bool = True     # a failed audit / integrity / gradient-consistency check (proof of
+                                         # tampering, not a statistic) compromises the node at once
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
     soft_output_z: float = 5.0           # with an output flag in a replica, an EARLIER stage whose output z
                                          # exceeds this (below its own decision threshold) is the source: a
@@ -205,6 +218,7 @@ class PipelineEngine:
             store = dist.distributed_c10d._get_default_store()
             self.heartbeat = HeartbeatMonitor(store, self.rank, self.world, cfg.heartbeat_interval,
                                               cfg.heartbeat_timeout, abort_on_offline=cfg.abort_on_offline).start()
+        self.refresh_shadows()   # a committed trusted copy of every stage from step 0 on
         logger.info("PipelineEngine[%s] plan: %s", "dist" if self.distributed else "local", self.plan.describe())
 
     # ================================================================== construction
@@ -360,7 +374,8 @@ class PipelineEngine:
             # early tied all-reduce only with hardware queues to spare (the p2p "async" mode): its
             # RCCL kernel waits on a stream of its own for the embedding stage, and on a queue
             # shared with the compute stream it would block the rest of this stage's backward
-            st.on_tied_ready = self._launch_tied_allreduce if self.distributed and self.p2p_mode == "async" else None
+            st.on_tied_ready = (self._launch_tied_allreduce
+                                if self.distributed and self.p2p_mode == "async" and len(self.ties) == 1 else None)
 
     def _set_clip_exclusions(self):
         """Count every tied weight once in the global clipping norm: the stage owning the first
@@ -551,6 +566,7 @@ class PipelineEngine:
         progress.mark(f"step {self.global_step}: pipeline schedule")
         t0 = time.perf_counter()
         truth: Dict[int, bool] = {}
+        self._truth_now = truth
         if self.attacker is not None and hasattr(self.attacker, "apply_attacks"):
             batch = self.attacker.apply_attacks(batch, self.global_step)
             truth.update(getattr(self.attacker, "last_batch_truth", {}) or {})
@@ -562,16 +578,21 @@ class PipelineEngine:
         targets = split_micro(tgt, M)
         oc = self.cfg.output_check
         self._mon_idx = -1 if oc == "none" else (self._mon_rng.randrange(M) if oc == "random" else 0)
-        # audited steps: the same decision on every rank (a hash of the step; every step at the
-        # default audit_prob = 1); WHICH micro-batch is audited is the auditor's private choice
-        self._audit_now = bool(self.cfg.audit and self.plan.num_stages > 1 and (
-            self.cfg.audit_prob >= 1.0 or
-            (hash((self.cfg.seed, self.global_step)) % 1_000_003) / 1_000_003 < self.cfg.audit_prob))
-        self._audit_rec: Dict[int, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
-        self._audit_inputs: Dict[int, torch.Tensor] = {}   # distributed: this stage's received inputs
-        self._audit_batch = inputs
-        if self._audit_now and not self.distributed and self._mon_idx < 0:
+        # audited steps: WHETHER a step is audited and WHICH micro-batch are the auditor's private
+        # choice (local: the engine's private RNG; distributed: each auditor's own RNG, revealed to
+        # the auditee through the c10d store only after its outputs were sent — a step-hash
+        # decision, as in round 3, was predictable by the auditee: ADVICE r3)
+        self._audit_now = bool(self.cfg.audit and self.plan.num_stages > 1)
+        if self._audit_now and not self.distributed and (
+                self._mon_idx < 0 or (self.cfg.audit_prob < 1.0 and self._mon_rng.random() >= self.cfg.audit_prob)):
             self._audit_now = False
+        self._audit_rec: Dict[int, Dict[str, Any]] = {}
+        self._audit_inputs: Dict[int, torch.Tensor] = {}   # distributed: this stage's received inputs
+        self._audit_sent_dx: Dict[int, torch.Tensor] = {}  # distributed: input gradients sent upstream
+        self._audit_recv_dy: Dict[int, torch.Tensor] = {}  # distributed: output gradients received
+        self._audit_batch = inputs
+        self._audit_targets = targets
+        self._begin_commitments(len(inputs))
         if self.distributed:
             loss = self._run_1f1b(inputs, targets, truth)
         else:
@@ -582,11 +603,103 @@ class PipelineEngine:
         self._step_time = time.perf_counter() - t0
         return self.last_loss
 
+    # ------------------------------------------------------------------ gradient commitments
+    def _sketch_for(self, st: Stage):
+        """The stage's gradient sketch (security/grad_audit.py), identical for the stage and any
+        mirror of it (same layer range -> same flat layout, signs and tied-weight mask)."""
+        from ..security.grad_audit import GradSketch, tied_ranges
+        key = (tuple(st.layer_range), st.flat.numel, str(st.device))
+        cache = self.__dict__.setdefault("_gsk_cache", {})
+        sk = cache.get(key)
+        if sk is None:
+            tied = []
+            for grp in self.ties:
+                for li, attr in grp:
+                    prm = st.local_param(li, attr)
+                    if prm is not None:
+                        tied.append(id(prm))
+            a, b = st.layer_range
+            sk = cache[key] = GradSketch(st.flat.numel, st.device, seed=self.cfg.seed * 1_000_003 + a * 7919 + b,
+                                         masked=tied_ranges(st.flat, tied))
+        return sk
+
+    def _tied_param(self, st: Stage) -> Optional[torch.Tensor]:
+        """This stage's member of the first tie group (GPT-2: wte / LM head), if any."""
+        if not self.ties:
+            return None
+        for li, attr in self.ties[0]:
+            prm = st.local_param(li, attr)
+            if prm is not None:
+                return prm
+        return None
+
+    def _tied_sketch(self, st: Stage, g: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """Sketch of the tied weight's gradient with a pattern shared by every member of the tie
+        group (parameter-local indexing), so the members' sketches add up across stages."""
+        from ..security.grad_audit import GradSketch
+        prm = self._tied_param(st)
+        if prm is None or getattr(prm, "main_grad", None) is None:
+            return None
+        cache = self.__dict__.setdefault("_tsk_cache", {})
+        key = (prm.numel(), str(st.device))
+        sk = cache.get(key)
+        if sk is None:
+            sk = cache[key] = GradSketch(prm.numel(), st.device, seed=self.cfg.seed * 7 + 424242)
+        return sk((prm.main_grad if g is None else g).reshape(-1), sk.offset(self.cfg.seed, self.global_step))
+
+    def _note_tied_pre(self, st: Stage):
+        """Right before the tied all-reduce: the stage's own tied-weight gradient contribution."""
+        if getattr(self, "_gsk_on", False):
+            t = self._tied_sketch(st)
+            if t is not None:
+                self._tsk_pre[st.stage_id] = t
+
+    def _begin_commitments(self, M: int):
+        """Per-step running gradient sketches of every local stage (index 0: before the first
+        micro-batch's backward, i + 1: after micro-batch i's weight gradients are accumulated)."""
+        self._gsk_on = bool(self.cfg.audit and self.cfg.audit_backward and self.plan.num_stages > 1 and self.dp == 1)
+        self._gsk_run: Dict[int, torch.Tensor] = {}
+        self._tsk_pre: Dict[int, torch.Tensor] = {}
+        if not self._gsk_on:
+            return
+        for node, st in self.stages.items():
+            sk = self._sketch_for(st)
+            r = torch.zeros(M + 1, 2, dtype=torch.float32, device=st.device)
+            r[0].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
+            self._gsk_run[node] = r
+
+    def _commit_micro(self, node: int, st: Stage, i: int):
+        """Micro-batch ``i``'s weight gradients of ``node`` are accumulated: (attack hook, then)
+        commit the running sketch."""
+        M = len(self._audit_batch)
+        if self.attacker is not None and hasattr(self.attacker, "after_micro_backward"):
+            if self.attacker.after_micro_backward(node, st.flat.grad, self.global_step, i, M):
+                self._truth_now[node] = True
+        r = self._gsk_run.get(node)
+        if r is not None:
+            sk = self._sketch_for(st)
+            r[i + 1].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
+
+    def _pre_micro(self, node: int, st: Stage, i: int):
+        if self.attacker is not None and hasattr(self.attacker, "before_micro_backward"):
+            self.attacker.before_micro_backward(node, st.flat.grad, self.global_step, i, len(self._audit_batch))
+
+    def _tamper_dx(self, node: int, dx: torch.Tensor, i: int) -> torch.Tensor:
+        """The input gradient ``node`` sends upstream for micro-batch ``i`` (Byzantine backward hook)."""
+        if self.attacker is not None and hasattr(self.attacker, "on_input_grad"):
+            d2 = self.attacker.on_input_grad(node, dx, self.global_step, i, len(self._audit_batch))
+            if d2 is not None:
+                self._truth_now[node] = True
+                return d2
+        return dx
+
     def begin_step(self) -> int:
         """Open an optimizer step (``train_step`` does this itself; the reference per-phase API —
         DistributedTrainer.forward_pass / backward_pass / optimizer_step — calls it explicitly)."""
         self._consume_reports(upto=self.global_step + 1 - self.REPORT_LAG)
         bump_weight_generation()   # weights may have changed since the last step (update, re-shard, restore, load)
+        self._gsk_on = False       # the per-phase API (external backward) commits no gradient sketches
+        self._truth_now = {}
         self.global_step += 1
         self.trust.advance_step(self.global_step)
         return self.global_step
@@ -616,9 +729,10 @@ class PipelineEngine:
                 st._early_checksum = dstats.checksum(st.flat.data)
             st._early_checksum.record_stream(cur)
 
-    def _attack_output(self, node: int, y: torch.Tensor, truth: Dict[int, bool]) -> torch.Tensor:
+    def _attack_output(self, node: int, y: torch.Tensor, truth: Dict[int, bool], micro: Optional[int] = None,
+                       num_micro: Optional[int] = None) -> torch.Tensor:
         if self.attacker is not None and hasattr(self.attacker, "on_output"):
-            y2 = self.attacker.on_output(node, y, self.global_step)
+            y2 = self.attacker.on_output(node, y, self.global_step, micro, num_micro)
             if y2 is not None:
                 truth[node] = True
                 return y2
@@ -636,32 +750,55 @@ class PipelineEngine:
         for node, _ in order:
             self._attack_params(node, self.stages[node], truth)
         total = None
+        bwd_audit = self._audit_now and self.cfg.audit_backward
         for i in range(M):
             x = inputs[i]
+            watch = i == self._mon_idx
             for sidx, (node, _) in enumerate(order):
                 st = self.stages[node]
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
-                watch = i == self._mon_idx
                 obs = st.output_observer() if watch else None
-                if watch and self._audit_now:
-                    x_in = x.detach().clone()
+                rec = self._audit_rec.setdefault(node, {}) if watch and self._audit_now else None
+                if rec is not None:
+                    rec["x"] = x.detach().clone()
+                    if st.computes_loss:
+                        rec["labels"] = labels
+                if sidx > 0 and x.requires_grad:
+                    # the input gradient this stage sends upstream (Byzantine-backward hook first, then
+                    # the audit's copy of what was sent); registered before the previous stage's
+                    # output-gradient capture below, so that capture sees the gradient as sent
+                    def _dx_hook(g, node=node, i=i, rec=rec):
+                        g2 = self._tamper_dx(node, g, i)
+                        if rec is not None and bwd_audit:
+                            rec["dx"] = g2.detach().clone()
+                        return g2 if g2 is not g else None
+                    x.register_hook(_dx_hook)
+                    prec = self._audit_rec.get(order[sidx - 1][0]) if rec is not None and bwd_audit else None
+                    if prec is not None:
+                        def _dy_hook(g, prec=prec):
+                            prec["dy"] = g.detach().clone()
+                        x.register_hook(_dy_hook)
                 with self.tracer.phase("fwd"):
                     y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1)
                 if not st.computes_loss:
-                    y = self._attack_output(node, y, truth)
+                    y = self._attack_output(node, y, truth, i, M)
                     if watch:
                         mon = y
-                        if self._audit_now:
-                            self._audit_rec[node] = (x_in, y.detach().clone())
+                        if rec is not None:
+                            rec["y"] = y.detach().clone()
                 if watch and mon is not None:
                     st.verifier.observe_output(mon)
                     if st.computes_loss and st.verifier.side is not None:
                         torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
                 x = y
             loss = x / M
+            for node, _ in order:
+                self._pre_micro(node, self.stages[node], i)
             with self.tracer.phase("bwd_input"):
                 loss.backward()
+            for node, _ in order:
+                self._commit_micro(node, self.stages[node], i)
             total = loss.detach() if total is None else total + loss.detach()
         return total
 
@@ -688,6 +825,8 @@ class PipelineEngine:
         out_q: deque = deque()
         total = [None]
         waited0 = comm.wait_seconds
+        keep_out = self._audit_now and self.cfg.audit_backward and s == S - 2
+        self._audit_outputs: Dict[int, torch.Tensor] = {}
 
         def get_input(i):
             if first:
@@ -711,9 +850,11 @@ class PipelineEngine:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()
             else:
-                y = self._attack_output(node, y, truth)
+                y = self._attack_output(node, y, truth, i, M)
                 if watch:
                     mon = y
+                if keep_out:
+                    self._audit_outputs[i] = y.detach()
             if watch and mon is not None:
                 st.verifier.observe_output(mon)
                 if last and st.verifier.side is not None:
@@ -721,26 +862,39 @@ class PipelineEngine:
                     torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
             return y
 
-        def bwd(x, y, dy):
+        def bwd(bi, x, y, dy):
             """Input-gradient backward; the weight-gradient GEMMs are queued (ops.layers
             .defer_weight_grads) and run by the caller AFTER dx has been posted upstream."""
+            self._pre_micro(node, st, bi)
+            if dy is not None and self._audit_now:
+                self._audit_recv_dy[bi] = dy
             with defer_weight_grads(defer_w) as dw:
                 if last:
                     y.backward()
                 else:
                     torch.autograd.backward(y, dy)
-            return (None if first else x.grad), dw
+            dx = None
+            if not first:
+                dx = self._tamper_dx(node, x.grad, bi)
+                if self._audit_now:
+                    self._audit_sent_dx[bi] = dx
+            dw.bi = bi
+            return dx, dw
+
+        def wgrad(dw):
+            dw.run()
+            self._commit_micro(node, st, dw.bi)
 
         def send_dx_then_w(dx, dw, recv_prev=None):
             h = comm.post(send_prev=dx, recv_prev=recv_prev)
-            dw.run()  # overlaps the transfer and the upstream stage's backward
+            wgrad(dw)  # overlaps the transfer and the upstream stage's backward
             return comm.wait(h)[0]
 
         for i in range(warm):
             x = get_input(i)
             y = fwd(i, x)
             comm.exchange(send_next=y)
-            in_q.append(x)
+            in_q.append((i, x))
             out_q.append(y)
         x = get_input(warm) if rem > 0 else None
         for j in range(rem):
@@ -750,29 +904,31 @@ class PipelineEngine:
                 dy = None
             else:
                 _, dy = comm.exchange(send_next=y, recv_next=(out_shape, act_dtype))
-            in_q.append(x)
+            in_q.append((i, x))
             out_q.append(y)
-            x0, y0 = in_q.popleft(), out_q.popleft()
-            dx, dw = bwd(x0, y0, dy)
+            (bi, x0), y0 = in_q.popleft(), out_q.popleft()
+            dx, dw = bwd(bi, x0, y0, dy)
             if j == rem - 1:
                 if not first:
                     send_dx_then_w(dx, dw)
-                dw.run()
+                else:
+                    wgrad(dw)
             else:
                 if first:
-                    dw.run()
+                    wgrad(dw)
                     x = get_input(i + 1)
                 else:
                     x = send_dx_then_w(dx, dw, recv_prev=(in_shape, act_dtype))
         for _ in range(warm):
-            x0, y0 = in_q.popleft(), out_q.popleft()
+            (bi, x0), y0 = in_q.popleft(), out_q.popleft()
             dy = None
             if not last:
                 _, dy = comm.exchange(recv_next=(out_shape, act_dtype))
-            dx, dw = bwd(x0, y0, dy)
+            dx, dw = bwd(bi, x0, y0, dy)
             if not first:
                 send_dx_then_w(dx, dw)
-            dw.run()
+            else:
+                wgrad(dw)
         self._comm_wait = comm.wait_seconds - waited0
         return total[0]
 
@@ -810,6 +966,9 @@ class PipelineEngine:
         total = [None]
         waited = [0.0]
         defer_w = self.cfg.defer_wgrad and not first
+        # the stage before the loss stage audits it and needs its own outputs (the loss stage's inputs)
+        keep_out = self._audit_now and self.cfg.audit_backward and s == S - 2
+        self._audit_outputs: Dict[int, torch.Tensor] = {}
 
         step = self.global_step
 
@@ -851,22 +1010,36 @@ class PipelineEngine:
                 y = y / M
                 total[0] = y.detach() if total[0] is None else total[0] + y.detach()
             else:
-                y = self._attack_output(node, y, truth)
+                y = self._attack_output(node, y, truth, i, M)
                 if watch:
                     mon = y
+                if keep_out:
+                    self._audit_outputs[i] = y.detach()
             if watch and mon is not None:
                 st.verifier.observe_output(mon)
                 if last and st.verifier.side is not None:
                     torch.cuda.current_stream(st.device).wait_stream(st.verifier.side)
             return y
 
-        def bwd(x, y, dy):
+        def bwd(bi, x, y, dy):
+            self._pre_micro(node, st, bi)
+            if dy is not None and self._audit_now:
+                self._audit_recv_dy[bi] = dy
             with defer_weight_grads(defer_w) as dw:
                 if last:
                     y.backward()
                 else:
                     torch.autograd.backward(y, dy)
-            return (None if first else x.grad), dw
+            dx = None
+            if not first:
+                dx = self._tamper_dx(node, x.grad, bi)
+                if self._audit_now:
+                    self._audit_sent_dx[bi] = dx
+            return dx, dw
+
+        def wgrad(bi, dw):
+            dw.run()
+            self._commit_micro(node, st, bi)
 
         def input_of(i, h):
             return self._stage_input(inputs[i], st) if first else take(h)
@@ -881,7 +1054,7 @@ class PipelineEngine:
             y = fwd(i, x)
             send(y, nxt, act_pg)
             x_h = post_x(i + 1)
-            in_q.append(x)
+            in_q.append((i, x))
             out_q.append(y)
         for j in range(rem):
             i = warm + j
@@ -891,26 +1064,26 @@ class PipelineEngine:
             if not last:
                 send(y, nxt, act_pg)
             x_h = post_x(i + 1)                    # arrives while the backward below runs
-            in_q.append(x)
+            in_q.append((i, x))
             out_q.append(y)
-            x0, y0 = in_q.popleft(), out_q.popleft()
+            (bi, x0), y0 = in_q.popleft(), out_q.popleft()
             dy = None if last else take(dy_h)
-            dx, dw = bwd(x0, y0, dy)
+            dx, dw = bwd(bi, x0, y0, dy)
             if not first:
                 send(dx, prev, grad_pg)
             with tr.phase("bwd_weight"):
-                dw.run()
+                wgrad(bi, dw)
         dy_h = post_dy(rem) if warm > 0 else None
         for c in range(warm):
             b = rem + c
             dy = take(dy_h)
-            x0, y0 = in_q.popleft(), out_q.popleft()
-            dx, dw = bwd(x0, y0, dy)
+            (bi, x0), y0 = in_q.popleft(), out_q.popleft()
+            dx, dw = bwd(bi, x0, y0, dy)
             if not first:
                 send(dx, prev, grad_pg)
             dy_h = post_dy(b + 1)                  # after the send: no send queues behind it
             with tr.phase("bwd_weight"):
-                dw.run()
+                wgrad(bi, dw)
         progress.mark(f"step {step}: stage {s} drains its P2P sends")
         t0 = time.perf_counter()
         for w in sends:
@@ -973,6 +1146,9 @@ class PipelineEngine:
             return
         g = self._tied_grad()
         if g is not None:
+            st = self.my_stage()
+            if st is not None:
+                self._note_tied_pre(st)
             self._tie_work = dist.all_reduce(g, group=self.tie_group, async_op=True)
 
     def _allreduce_tied(self):
@@ -993,6 +1169,8 @@ class PipelineEngine:
                     if all(p is not q for q in params):
                         params.append(p)
                 if len(params) > 1:
+                    for node, _, _ in owners:
+                        self._note_tied_pre(self.stages[node])
                     tot = sum(p.main_grad.to(params[0].device) for p in params)
                     for p in params:
                         p.main_grad.copy_(tot.to(p.device))
@@ -1000,10 +1178,14 @@ class PipelineEngine:
         if not self.tie_members or self.rank not in self.tie_members:
             return
         st = self.my_stage()
-        for grp in self.ties:
+        # one all-reduce per tie group, in the same order on every member (the early path handles
+        # only the first group: it is used only when there is exactly one)
+        for gi, grp in enumerate(self.ties):
             for li, attr in grp:
                 p = st.local_param(li, attr)
                 if p is not None:
+                    if gi == 0:
+                        self._note_tied_pre(st)
                     dist.all_reduce(p.main_grad, group=self.tie_group)
                     break
 
@@ -1028,13 +1210,33 @@ class PipelineEngine:
             hm = self._host_metric_row(node)
             d = st.verifier.finish_step(st.flat.grad, loss if st.computes_loss else None, hm,
                                         truth.get(node, False), st.stage_id)
+            # the weight commitment made after this stage's last update (before anything of this
+            # step could touch the weights): the auditor checks the weights it receives against it
+            pc = getattr(st, "param_checksum", None)
+            if pc is not None:
+                from ..security.grad_audit import fold_hash
+                d[SV.D_WHASH:SV.D_WHASH + 2].copy_(fold_hash(pc))
+            else:
+                d[SV.D_WHASH:SV.D_WHASH + 2].fill_(-1.0)
             if self.cfg.param_integrity:
                 d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].copy_(self._integrity_flag(st))
+                if self.attacker is not None and getattr(self.attacker, "lies_about_integrity", None) \
+                        and self.attacker.lies_about_integrity(node, self.global_step):
+                    d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].fill_(0.0)   # a rank lying about its own check
+            self._write_commitments(node, st, d)
             rows.append((node, d))
         if getattr(self, "_audit_now", False):
             ta = self.tracer.begin("audit")
             progress.mark(f"step {self.global_step}: recompute audit")
+            t_a = time.perf_counter()
+            ev = None
+            if self.device.type == "cuda":
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             self._audit(dict(rows))
+            if ev is not None:
+                ev[1].record()
+            self._note_audit_cost(time.perf_counter() - t_a, ev)
             self.tracer.end(ta)
         if self.distributed:
             mine = rows[0][1] if rows else torch.zeros(SV.DIGEST, dtype=torch.float32, device=self.device)
@@ -1073,8 +1275,9 @@ class PipelineEngine:
         # a failed weight-integrity check (weights rewritten outside the optimizer) is definitive
         # evidence and compromises at once
         self.t_flagrun.copy_((self.t_flagrun + 1) * raw)
+        proof = self._proof if self.cfg.compromise_on_proof else (D[:, SV.D_PARAM_FLAG] > 0).float()
         flags = torch.maximum((self.t_flagrun >= max(1, self.cfg.compromise_after)).to(torch.int32),
-                              (D[:, SV.D_PARAM_FLAG] > 0).to(torch.int32) * raw)
+                              (proof > 0).to(torch.int32) * raw)
         # every blamed step also costs trust through the metrics (worst output deviation, no
         # gradient consistency), so isolated detections accumulate instead of being forgotten
         metrics = D[:, SV.D_METRICS:SV.D_METRICS + 6].clone()
@@ -1097,6 +1300,10 @@ class PipelineEngine:
         to = self.tracer.begin("optimizer")
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
+            cur = getattr(st, "_cur_checksum", None)
+            if self.cfg.param_integrity and cur is not None:
+                # the weights must still be those checksummed at the start of the step
+                st._tail_flag = (dstats.checksum(st.flat.data) != cur).any().float().reshape(1)
             st.flat.adamw_step(self.cfg.adamw, ctrl=st.verifier.ctrl)
             if self.cfg.param_integrity:
                 st.param_checksum = dstats.checksum(st.flat.data, getattr(st, "param_checksum", None))
@@ -1107,10 +1314,11 @@ class PipelineEngine:
             self._audit_params()
         # queue the host report (pinned, non-blocking)
         if getattr(self, "_audit_now", False):
-            abad, adone = self._audit_vectors(D)
+            _, adone = self._audit_vectors(D)
         else:
-            abad = adone = torch.zeros(N, dtype=torch.float32, device=self.device)
-        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float(), blame.float(), abad, adone])
+            adone = torch.zeros(N, dtype=torch.float32, device=self.device)
+        akind = self._proof_kind
+        rep = torch.cat([D.reshape(-1), self.t_values, self.t_status.float(), blame.float(), akind, adone])
         if rep.is_cuda:
             host = torch.empty(rep.shape, dtype=rep.dtype, pin_memory=True)
             host.copy_(rep, non_blocking=True)
@@ -1120,19 +1328,62 @@ class PipelineEngine:
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
 
+    def _write_commitments(self, node: int, st: Stage, d: torch.Tensor):
+        """Digest slots of the gradient commitments: the sketch of the gradient about to be applied
+        (after the tied all-reduce and every hook) and the committed running sketch after the last
+        micro-batch's backward.  They differ when the gradient was rewritten in between."""
+        r = self._gsk_run.get(node) if getattr(self, "_gsk_on", False) else None
+        if r is None:
+            d[SV.D_GSK_ON:SV.D_GSK_ON + 1].fill_(0.0)
+            return
+        sk = self._sketch_for(st)
+        d[SV.D_GSK_APP:SV.D_GSK_APP + 2].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
+        d[SV.D_GSK_BWD:SV.D_GSK_BWD + 2].copy_(r[-1])
+        d[SV.D_GSK_ON:SV.D_GSK_ON + 1].fill_(1.0)
+        pre = self._tsk_pre.get(st.stage_id)
+        if pre is not None:
+            d[SV.D_TSK_PRE:SV.D_TSK_PRE + 2].copy_(pre)
+            d[SV.D_TSK_APP:SV.D_TSK_APP + 2].copy_(self._tied_sketch(st))
+            d[SV.D_TSK_ON:SV.D_TSK_ON + 1].fill_(1.0)
+        else:
+            d[SV.D_TSK_ON:SV.D_TSK_ON + 1].fill_(0.0)
+
     # ================================================================== deterministic stage cross-check
-    @torch.no_grad()
-    def _recompute(self, st: Stage, x: torch.Tensor) -> torch.Tensor:
-        """``st``'s forward of one micro-batch, as in training (BatchNorm in batch-statistics mode),
-        without leaving a trace: module buffers (running statistics) are restored afterwards."""
+    def _recompute(self, st: Stage, x: torch.Tensor, dy: Optional[torch.Tensor] = None,
+                   labels: Optional[torch.Tensor] = None, M: int = 1, backward: bool = False):
+        """``st``'s forward of one micro-batch as in training (BatchNorm in batch-statistics mode),
+        and with ``backward`` its backward from the output gradient ``dy`` (the loss stage: from
+        its loss / M, as the schedule runs it), without leaving a trace: module buffers (running
+        statistics) are restored and the weight gradients go to a scratch accumulator, whose
+        sketch is returned.  Returns (output, input gradient or None, weight-gradient sketch or None)."""
         bufs = [b.detach().clone() for b in st.module.buffers()]
         try:
-            with torch.no_grad():   # no autograd graph / saved activations for the recompute
-                y, _ = st.forward(x, None)
+            if not backward:
+                with torch.no_grad():   # no autograd graph / saved activations for the recompute
+                    y, _ = st.forward(x, labels)
+                return y, None, None
+            scratch = torch.zeros_like(st.flat.grad)
+            saved = st.flat.set_grad_buffer(scratch)
+            try:
+                xg = x.detach().clone()
+                if xg.is_floating_point():
+                    xg.requires_grad_(True)
+                with torch.enable_grad():
+                    y, _ = st.forward(xg, labels)
+                    if st.computes_loss:
+                        (y / M).backward()
+                    else:
+                        torch.autograd.backward(y, dy)
+                sk = self._sketch_for(st)
+                skv = sk(scratch, sk.offset(self.cfg.seed, self.global_step))
+                dx = xg.grad if xg.is_floating_point() else None
+                return y.detach(), dx, skv
+            finally:
+                st.flat.set_grad_buffer(saved)
         finally:
-            for b, v in zip(st.module.buffers(), bufs):
-                b.copy_(v)
-        return y
+            with torch.no_grad():
+                for b, v in zip(st.module.buffers(), bufs):
+                    b.copy_(v)
 
     def _audit_verdict(self, y_seen: torch.Tensor, y_ref: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(mismatch flag, relative max error) of a received output against its recomputation —
@@ -1142,110 +1393,339 @@ class PipelineEngine:
         err = torch.nan_to_num(err, nan=1e30, posinf=1e30)
         return (err > self.cfg.audit_tol).float().reshape(1), err.reshape(1)
 
-    def _audit(self, rows: Dict[int, torch.Tensor]):
-        """Recompute audit of every non-loss stage's monitored micro-batch (the private-RNG choice
-        of ``_mon_idx``): the output the next stage received must equal f(input; weights).
+    def _audit_one(self, st: Stage, x: torch.Tensor, m: int, M: int, y_seen=None, dy=None, labels=None,
+                   dx_seen=None, run=None, whash=None):
+        """All checks of one audited micro-batch ``m`` of stage ``st`` (its own modules in local mode,
+        a mirror holding its shipped weights in distributed mode).  Returns device tensors
+        (mismatch flag [1], failed-check bitmask [1], worst relative error [1]).
 
-        Local mode: the engine holds every stage, the verdict on stage p is computed right here.
-        Distributed: each stage sends its weights (bf16 compute copy) and its input for that
-        micro-batch to the next stage, which rebuilds the previous stage's layers once per plan (a
-        mirror on its own GPU), recomputes and compares with what it received; stage 0's input is
-        the token batch every rank has.  The verdict on stage p rides in its auditor's digest row
-        (``D_AUDIT_PREV``), so no collective is added.  A tampered activation (Byzantine output)
-        mismatches deterministically; a weight perturbation recomputes consistently but fails the
-        weight-integrity checksum; a clean stage always matches."""
-        order = [n for n in self.plan.ranks]
-        if not self.distributed:
-            for k in range(1, len(order)):
-                p, aud = order[k - 1], order[k]
-                rec = self._audit_rec.get(p)
-                if rec is None or rec[1] is None or aud not in rows:
-                    continue
-                st = self.stages[p]
-                y_ref = self._recompute(st, rec[0])
-                flag, err = self._audit_verdict(rec[1], y_ref)
-                d = rows[aud]
-                d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag.to(d.device))
-                d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
-                d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err.to(d.device))
+        * forward (AK_FWD): the output the next stage received == f(x; W);
+        * input gradient (AK_DX): the gradient sent upstream == the recomputed one for the output
+          gradient the audited stage received;
+        * weight gradient (AK_DW): the sketch of micro-batch m's committed contribution
+          (running sketches ``run[m+1] - run[m]``) == the sketch of the recomputed one;
+        * weights (AK_WHASH, local mode): the weights in use == the stage's post-update commitment."""
+        from ..security.grad_audit import sketch_mismatch
+        bwd = self.cfg.audit_backward and (st.computes_loss or dy is not None)
+        y_ref, dx_ref, sk_ref = self._recompute(st, x, dy, labels, M, backward=bwd)
+        z = torch.zeros(1, dtype=torch.float32, device=st.device)
+        kind, err = z.clone(), z.clone()
+        if y_seen is not None and not st.computes_loss:
+            f, e = self._audit_verdict(y_seen, y_ref)
+            kind += f * SV.AK_FWD
+            err = torch.maximum(err, e)
+        if bwd and dx_seen is not None and dx_ref is not None:
+            f, e = self._audit_verdict(dx_seen, dx_ref)
+            kind += f * SV.AK_DX
+            err = torch.maximum(err, e)
+        if bwd and run is not None and sk_ref is not None and 0 <= m < run.shape[0] - 1:
+            floor = 1e-3 * (run[1:] - run[:-1]).abs().amax()
+            f, e = sketch_mismatch(run[m + 1] - run[m], sk_ref, self.cfg.audit_grad_tol, floor)
+            kind += f * SV.AK_DW
+            err = torch.maximum(err, e)
+        if whash is not None:
+            kind += whash * SV.AK_WHASH
+        return (kind > 0).float(), kind, err
+
+    def _audit(self, rows: Dict[int, torch.Tensor]):
+        """Recompute audit of one privately chosen micro-batch per stage and step.
+
+        Every non-loss stage is audited by the NEXT stage (it received the output and sent back the
+        output gradient), the loss stage by its predecessor (which received its input gradient).
+        Forward (the output equals f(input; weights)) and, with ``audit_backward``, backward (the
+        input gradient sent upstream and the micro-batch's weight-gradient contribution equal their
+        recomputation) — see ``_audit_one``.  Local mode: the engine holds every stage and computes
+        each verdict right here.  Distributed: see ``_audit_dist``.  A verdict rides in its
+        auditor's digest row (``D_AUDIT_PREV`` / ``D_AUDIT_NEXT``), so no collective is added; a
+        tampered activation or gradient mismatches deterministically, a weight perturbation
+        recomputes consistently but fails the weight commitment, a clean stage always matches."""
+        if self.distributed:
+            self._audit_dist(rows)
             return
+        from ..security.grad_audit import fold_hash
+        order = list(self.plan.ranks)
+        S = len(order)
+        M = len(self._audit_batch)
+        m = self._mon_idx
+        for k in range(S):
+            p = order[k]
+            last = k == S - 1
+            if last and not self.cfg.audit_backward:
+                continue
+            aud = order[k + 1] if not last else order[k - 1]
+            rec = self._audit_rec.get(p)
+            if not rec or "x" not in rec or aud not in rows:
+                continue
+            st = self.stages[p]
+            dy = None if last else rec.get("dy")
+            wh = None
+            cur, ref = getattr(st, "_cur_checksum", None), getattr(st, "param_checksum", None)
+            if cur is not None and ref is not None and cur is not ref:
+                wh = (fold_hash(cur) != fold_hash(ref)).any().float().reshape(1)
+            flag, kind, err = self._audit_one(st, rec["x"], m, M, y_seen=rec.get("y"), dy=dy,
+                                              labels=rec.get("labels"), dx_seen=rec.get("dx"),
+                                              run=self._gsk_run.get(p), whash=wh)
+            d = rows[aud]
+            base = (SV.D_AUDIT_NEXT, SV.D_AUDITED_NEXT, SV.D_AUDIT_KIND_NEXT) if last else \
+                (SV.D_AUDIT_PREV, SV.D_AUDITED_PREV, SV.D_AUDIT_KIND_PREV)
+            d[base[0]:base[0] + 1].copy_(flag.to(d.device))
+            d[base[1]:base[1] + 1].fill_(1.0)
+            d[base[2]:base[2] + 1].copy_(kind.to(d.device))
+            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1],
+                                                                    err.to(d.device)))
+
+    def _audit_dist(self, rows: Dict[int, torch.Tensor]):
+        """Distributed audit protocol of one rank (stage s of S):
+
+        1. commit: every audited stage sends its running gradient sketches (one [M+1, 2] tensor) to
+           its auditor BEFORE any choice is revealed;
+        2. reveal: each auditor draws privately whether to audit and which micro-batch (-1 = no
+           audit) and posts it in the c10d store (host to host, no device sync); the auditee reads
+           it only now, after every output and gradient of the step reached its peers;
+        3. ship: the auditee sends its bf16 weights, and (non-first, non-loss stages) its input and
+           the input gradient it sent upstream for that micro-batch; the loss stage ships only its
+           weights (its auditor holds its input, the labels and the gradient it sent);
+        4. verify on a mirror of the audited stage (``_audit_one``); the hash of the weights
+           received (vs the auditee's post-update commitment ``D_WHASH``) and of the input gradient
+           shipped (vs what the upstream stage received, ``D_DXHASH_RECV``) go into the auditor's
+           row and are compared on every rank in ``_attribute`` — so a rank that lies about its own
+           integrity check, or ships a different gradient than it sent, is still caught."""
+        from ..security.grad_audit import hash2
         st = self.my_stage()
         if st is None:
             return
-        s = st.stage_id
+        s, S = st.stage_id, self.plan.num_stages
         prev, nxt = self.comm.prev, self.comm.next
-        group = self._dir_groups[0] if self.p2p_mode == "async" else None
+        bwd = self.cfg.audit_backward
+        act_g, grad_g = (self._dir_groups if self.p2p_mode == "async" else (None, None))
         M = len(self._audit_batch)
+        d = rows[self.rank]
         if not hasattr(self, "_audit_rng"):
             seed = self.cfg.monitor_seed
             self._audit_rng = __import__("random").Random(
                 int.from_bytes(os.urandom(8), "little") if seed is None else seed * 7919 + self.rank)
-        # The auditor's private choice of micro-batch and the auditee's input shape travel host to
-        # host through the c10d store (no device sync, no GPU collective): every output of this
-        # step already reached the auditor before it reveals its choice, so the auditee cannot
-        # tailor what it sent to it.
         store = dist.distributed_c10d._get_default_store()
         tag = f"tdl_audit/{self.plan.version}/{self.global_step}"
-        m_mine = self._audit_rng.randrange(M)
-        if prev is not None:
-            store.set(f"{tag}/req/{prev}", str(m_mine))
-        x_send = None
-        if nxt is not None and s > 0:           # I am audited by the next stage: which input?
+        # my auditees: prev (I am its next stage), and nxt when it is the loss stage
+        audit_prev = prev is not None
+        audit_next = bwd and nxt is not None and s + 1 == S - 1
+        # my auditor: nxt, or prev when I am the loss stage
+        my_auditor = nxt if nxt is not None else (prev if bwd and s == S - 1 and prev is not None else None)
+        # ---- 1. commitments: running sketches to my auditor before any reveal
+        runs_in: Dict[int, torch.Tensor] = {}
+        mine = self._gsk_run.get(self.rank) if getattr(self, "_gsk_on", False) else None
+        if bwd and mine is not None:
+            c_send = [(mine, my_auditor)] if my_auditor is not None else []
+            c_recv = []
+            for peer, on in ((prev, audit_prev), (nxt, audit_next)):
+                if on:
+                    runs_in[peer] = torch.empty(M + 1, 2, dtype=torch.float32, device=self.device)
+                    c_recv.append((runs_in[peer], peer))
+            self._audit_transfer(c_send, c_recv, prev, nxt, act_g, grad_g)
+
+        # ---- 2. reveal: private choices (whether + which micro-batch)
+        def choose():
+            if self.cfg.audit_prob < 1.0 and self._audit_rng.random() >= self.cfg.audit_prob:
+                return -1
+            return self._audit_rng.randrange(M)
+        m_prev = choose() if audit_prev else -1
+        m_next = choose() if audit_next else -1
+        if audit_prev:
+            store.set(f"{tag}/req/{prev}", str(m_prev))
+            if s - 1 > 0 and bwd:
+                store.set(f"{tag}/reqh/{prev}", str(m_prev))   # for the stage before prev: dx hash
+        if audit_next:
+            store.set(f"{tag}/req/{nxt}", str(m_next))
+        m_req = -1
+        if my_auditor is not None:
             k = f"{tag}/req/{self.rank}"
             m_req = int(store.get(k))
             store.delete_key(k)
+        # as the upstream recipient of nxt's input gradient: hash what I received for nxt's audited micro-batch
+        if bwd and nxt is not None and s + 1 < S - 1:
+            k = f"{tag}/reqh/{nxt}"
+            mh = int(store.get(k))
+            store.delete_key(k)
+            if mh >= 0 and mh in self._audit_recv_dy:
+                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].copy_(hash2(self._audit_recv_dy[mh]))
+            else:
+                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
+        else:
+            d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
+        x_send = dx_send = None
+        if m_req >= 0 and s > 0 and s < S - 1:
             x_send = self._audit_inputs[m_req].contiguous()
+            if bwd and m_req in self._audit_sent_dx:
+                dx_send = self._audit_sent_dx[m_req].contiguous()
             store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send.shape))
-        # weights (bf16 compute copy) and the requested input
+        # ---- 3. ship
         sends, recvs = [], []
-        if nxt is not None:
-            sends.append((st.flat.data, nxt))
+        if m_req >= 0:
+            sends.append((st.flat.data, my_auditor))
             if x_send is not None:
-                sends.append((x_send, nxt))
-        mirror, x_prev = None, None
-        if prev is not None:                     # I audit the previous stage
-            mirror = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
-            recvs.append((mirror.flat.data, prev))
+                sends.append((x_send, my_auditor))
+            if dx_send is not None:
+                sends.append((dx_send, my_auditor))
+        mir_p = mir_n = x_prev = dx_prev = None
+        if audit_prev and m_prev >= 0:
+            mir_p = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
+            recvs.append((mir_p.flat.data, prev))
             if s - 1 > 0:
                 k = f"{tag}/shape/{prev}"
                 shape = torch.Size([int(v) for v in store.get(k).decode().split(",")])
                 store.delete_key(k)
                 x_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
                 recvs.append((x_prev, prev))
-        self._note_peers(sends, recvs, "dir" if group is not None else "default")
-        batched_transfer(sends, recvs, group=group)
-        if mirror is not None:
+                if bwd:
+                    dx_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
+                    recvs.append((dx_prev, prev))
+        if audit_next and m_next >= 0:
+            mir_n = self._audit_mirror(tuple(self.plan.ranges[s + 1]), s + 1)
+            recvs.append((mir_n.flat.data, nxt))
+        self._audit_transfer(sends, recvs, prev, nxt, act_g, grad_g)
+        # ---- 4. verify
+        if mir_p is not None:
             if x_prev is None:
-                x_prev = self._stage_input(self._audit_batch[m_mine], mirror)
-            y_ref = self._recompute(mirror, x_prev)
-            flag, err = self._audit_verdict(self._audit_inputs[m_mine], y_ref)
-            d = rows[self.rank]
+                x_prev = self._stage_input(self._audit_batch[m_prev], mir_p)
+            dy = self._audit_sent_dx.get(m_prev) if bwd else None
+            flag, kind, err = self._audit_one(mir_p, x_prev, m_prev, M, y_seen=self._audit_inputs[m_prev], dy=dy,
+                                              dx_seen=dx_prev, run=runs_in.get(prev))
             d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag)
             d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
+            d[SV.D_AUDIT_KIND_PREV:SV.D_AUDIT_KIND_PREV + 1].copy_(kind)
             d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err)
+            d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].copy_(hash2(mir_p.flat.data))
+            if dx_prev is not None:
+                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].copy_(hash2(dx_prev))
+            else:
+                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
+        else:
+            d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].fill_(-1.0)
+            d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
+        if mir_n is not None:
+            x_n = self._audit_outputs.get(m_next)
+            labels = self._audit_targets[m_next].to(self.device, non_blocking=True)
+            flag, kind, err = self._audit_one(mir_n, x_n, m_next, M, labels=labels,
+                                              dx_seen=self._audit_recv_dy.get(m_next), run=runs_in.get(nxt))
+            d[SV.D_AUDIT_NEXT:SV.D_AUDIT_NEXT + 1].copy_(flag)
+            d[SV.D_AUDITED_NEXT:SV.D_AUDITED_NEXT + 1].fill_(1.0)
+            d[SV.D_AUDIT_KIND_NEXT:SV.D_AUDIT_KIND_NEXT + 1].copy_(kind)
+            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1], err))
+            d[SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2].copy_(hash2(mir_n.flat.data))
+        else:
+            d[SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2].fill_(-1.0)
         self._audit_inputs = {}
+        self._audit_sent_dx = {}
+        self._audit_recv_dy = {}
+        self._audit_outputs = {}
+
+    def _note_audit_cost(self, host_s: float, ev):
+        a = self.__dict__.setdefault("_audit_cost", {"steps": 0, "host_s": 0.0, "bytes": 0, "events": []})
+        a["steps"] += 1
+        a["host_s"] += host_s
+        if ev is not None:
+            a["events"].append(ev)
+            if len(a["events"]) > 512:
+                del a["events"][:256]
+
+    def audit_summary(self) -> Dict[str, float]:
+        """Per-step cost of the recompute audit on this rank (call after a device sync): P2P bytes
+        it sent + received (commitments, weights, inputs, gradients), host wall time of the audit
+        phase, and device time between its first and last kernel (HIP events)."""
+        a = getattr(self, "_audit_cost", None)
+        if not a or not a["steps"]:
+            return {"steps": 0}
+        gpu = [e0.elapsed_time(e1) for e0, e1 in a["events"] if e1.query()]
+        return {"steps": a["steps"], "bytes_per_step": a["bytes"] / a["steps"],
+                "host_ms_per_step": 1e3 * a["host_s"] / a["steps"],
+                "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None}
+
+    def _audit_transfer(self, sends, recvs, prev, nxt, act_g, grad_g):
+        """Audit traffic: toward the next stage on the activation communicator, toward the
+        previous one on the gradient communicator (async P2P mode; grouped mode: default group),
+        as two batched exchanges in the same order on every rank."""
+        fwd_s = [(t, r) for t, r in sends if r == nxt]
+        fwd_r = [(t, r) for t, r in recvs if r == prev]
+        bwd_s = [(t, r) for t, r in sends if r == prev]
+        bwd_r = [(t, r) for t, r in recvs if r == nxt]
+        a = self.__dict__.setdefault("_audit_cost", {"steps": 0, "host_s": 0.0, "bytes": 0, "events": []})
+        a["bytes"] += sum(t.numel() * t.element_size() for t, _ in list(sends) + list(recvs))
+        for ss, rr, g in ((fwd_s, fwd_r, act_g), (bwd_s, bwd_r, grad_g)):
+            self._note_peers(ss, rr, "dir" if g is not None else "default")
+            batched_transfer(ss, rr, group=g)
 
     def _audit_mirror(self, rng: Tuple[int, int], sid: int) -> Stage:
-        """The previous stage's layers on this GPU (weights overwritten by every audit)."""
-        key = (self.plan.version, rng)
-        if getattr(self, "_mirror_key", None) != key:
-            self._mirror = Stage(self.model, rng, sid, self.plan.num_stages, self.device, self.dtype,
-                                 {"output_detection": False, "gradient_verification": False,
-                                  "serialize_streams": True})
-            self._mirror.remove_hooks()
-            self._mirror_key = key
-        return self._mirror
+        """The audited stage's layers on this GPU (weights overwritten by every audit); one mirror
+        per audited layer range (the stage before the loss stage audits two stages)."""
+        key = (self.plan.version, tuple(rng))
+        cache = self.__dict__.setdefault("_mirrors", {})
+        if key not in cache:
+            for k in [k for k in cache if k[0] != self.plan.version]:
+                del cache[k]
+            # (its gradient-folding hooks stay: the backward audit recomputes weight gradients on it)
+            cache[key] = Stage(self.model, rng, sid, self.plan.num_stages, self.device, self.dtype,
+                               {"output_detection": False, "gradient_verification": False, "serialize_streams": True})
+        return cache[key]
 
     def _audit_vectors(self, D: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Per-node (audit mismatch, audited) from the digest: a stage's verdict sits in the row of
-        the next stage of its pipeline replica."""
-        bad = torch.zeros(D.shape[0], dtype=torch.float32, device=D.device)
-        done = torch.zeros_like(bad)
+        """Per-node (failed-check bitmask, audited) from the digest, identical on every rank: a
+        stage's verdict sits in the row of its auditor (the next stage of its pipeline replica; the
+        loss stage's in its predecessor's ``*_NEXT`` slots), plus the hash cross-checks — the
+        weights its auditor received vs its own post-update commitment, and the input gradient it
+        shipped to its auditor vs what the upstream stage received."""
+        N = D.shape[0]
+        kind = torch.zeros(N, dtype=torch.float32, device=D.device)
+        done = torch.zeros_like(kind)
+        bwd = self.cfg.audit_backward
         for idx in self._replica_orders():
-            if idx.numel() > 1:
-                bad[idx[:-1]] = D[idx[1:], SV.D_AUDIT_PREV]
-                done[idx[:-1]] = D[idx[1:], SV.D_AUDITED_PREV]
-        return bad, done
+            n = idx.numel()
+            if n < 2:
+                continue
+            a, p = idx[1:], idx[:-1]
+            kind[p] = D[a, SV.D_AUDIT_KIND_PREV] + (D[a, SV.D_AUDIT_PREV] > 0).float() * \
+                (D[a, SV.D_AUDIT_KIND_PREV] <= 0).float() * SV.AK_FWD
+            done[p] = D[a, SV.D_AUDITED_PREV]
+            if self.distributed:
+                wh_c, wh_s = D[p, SV.D_WHASH:SV.D_WHASH + 2], D[a, SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2]
+                both = ((wh_c[:, 0] >= 0) & (wh_s[:, 0] >= 0)).float()
+                kind[p] += both * (wh_c != wh_s).any(1).float() * SV.AK_WHASH
+                if n >= 3:
+                    # stage j (1 <= j <= n-2) shipped its dx to idx[j+1]; idx[j-1] received it
+                    q = idx[1:-1]
+                    recv, ship = D[idx[:-2], SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2], \
+                        D[idx[2:], SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2]
+                    both = ((recv[:, 0] >= 0) & (ship[:, 0] >= 0)).float()
+                    kind[q] += both * (recv != ship).any(1).float() * SV.AK_DXHASH
+            if bwd:
+                L, A = idx[-1], idx[-2]
+                kind[L] = D[A, SV.D_AUDIT_KIND_NEXT]
+                done[L] = D[A, SV.D_AUDITED_NEXT]
+                if self.distributed:
+                    wh_c, wh_s = D[L, SV.D_WHASH:SV.D_WHASH + 2], D[A, SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2]
+                    both = float(1.0) * ((wh_c[0] >= 0) & (wh_s[0] >= 0)).float()
+                    kind[L] += both * (wh_c != wh_s).any().float() * SV.AK_WHASH
+        return kind, done
+
+    def _gsk_mismatch(self, D: torch.Tensor) -> torch.Tensor:
+        """Per-node 1.0 where the applied gradient's sketch differs from the committed sum of the
+        stage's per-micro-batch contributions (a gradient rewritten after the backward)."""
+        from ..security.grad_audit import K_SKETCH
+        app = D[:, SV.D_GSK_APP:SV.D_GSK_APP + K_SKETCH]
+        com = D[:, SV.D_GSK_BWD:SV.D_GSK_BWD + K_SKETCH]
+        on = (D[:, SV.D_GSK_ON] > 0).float()
+        scale = torch.maximum(com.abs().amax(1), app.abs().amax(1)).clamp_min(1e-20)
+        err = torch.nan_to_num((app - com).abs().amax(1) / scale, nan=1e30, posinf=1e30)
+        bad = on * (err > 1e-3).float()
+        # the tied weight: every member must apply the sum of the members' own contributions
+        ton = (D[:, SV.D_TSK_ON] > 0).float()
+        pre, tapp = D[:, SV.D_TSK_PRE:SV.D_TSK_PRE + K_SKETCH], D[:, SV.D_TSK_APP:SV.D_TSK_APP + K_SKETCH]
+        for idx in self._replica_orders():
+            t = ton[idx]
+            exp = (pre[idx] * t[:, None]).sum(0, keepdim=True)
+            sc = torch.maximum(exp.abs().amax(), tapp[idx].abs().amax(1)).clamp_min(1e-20)
+            e = torch.nan_to_num((tapp[idx] - exp).abs().amax(1) / sc, nan=1e30, posinf=1e30)
+            bad[idx] = torch.maximum(bad[idx], t * (t.sum() >= 2).float() * (e > 1e-3).float())
+        return bad
 
     # ================================================================== integrity + attribution
     @torch.no_grad()
@@ -1255,11 +1735,16 @@ class PipelineEngine:
         cur = st.__dict__.pop("_early_checksum", None)
         if cur is None:
             cur = dstats.checksum(st.flat.data)
+        st._cur_checksum = cur
+        # a write between the start of the previous step and its update (during its forward /
+        # backward: ADVICE r3) was seen by that step's tail re-check and is reported now
+        tail = st.__dict__.pop("_tail_flag", None)
         ref = getattr(st, "param_checksum", None)
         if ref is None:  # first step / freshly (re)built or reloaded stage: nothing to compare yet
             st.param_checksum = cur
             return torch.zeros(1, dtype=torch.float32, device=st.device)
-        return (cur != ref).any().float().reshape(1)
+        flag = (cur != ref).any().float().reshape(1)
+        return flag if tail is None else torch.maximum(flag, tail)
 
     def _replica_orders(self) -> List[torch.Tensor]:
         key = (self.plan.version, self.dp)
@@ -1285,8 +1770,16 @@ class PipelineEngine:
         evidence = torch.zeros_like(of)
         self.t_taint.copy_(torch.maximum(self.t_taint, (pf > 0).float()))
         audited = getattr(self, "_audit_now", False)
+        akind = torch.zeros_like(of)
         if audited:
-            abad, _ = self._audit_vectors(D)
+            akind, _ = self._audit_vectors(D)
+        abad = (akind > 0).float()
+        # applied gradient != committed backward contributions: rewritten after the backward
+        gbad = self._gsk_mismatch(D) if self.cfg.audit and self.cfg.audit_backward else torch.zeros_like(of)
+        # proof of tampering (not a statistic): compromises at once (compromise_on_proof)
+        self._proof = torch.maximum(torch.maximum((pf > 0).float(), abad), gbad)
+        self._proof_kind = akind + gbad * 32.0
+        stat_blame = 0.0 if (audited and self.cfg.audit_backward) else 1.0
         for r, idx in enumerate(self._replica_orders()):
             o, g, p = of[idx], gf[idx], pf[idx]
             taint = self.t_taint[idx]
@@ -1296,9 +1789,12 @@ class PipelineEngine:
                 # mismatch (its own stage, never the downstream echoes) or a failed weight-integrity
                 # check; output z-scores do not blame.  Gradient anomalies count only in a replica
                 # without such evidence (gradient poisoning does not propagate, tampering does)
+                # with the backward audit, gradient z-scores no longer blame either: the
+                # deterministic gradient checks (recomputed contribution, applied-vs-committed
+                # sketch) do; the statistics still quarantine the update and feed the trust metrics
                 a = abad[idx]
                 ev = torch.maximum(p.max(), a.max())
-                b = torch.maximum(torch.maximum(p, a), g * (1.0 - ev))
+                b = torch.maximum(torch.maximum(p, a), g * (1.0 - ev) * stat_blame)
                 o = a   # "forward anomaly" below = a recompute mismatch
             elif self.cfg.attribute_flags:
                 # earliest anomalous stage; a stage with tampered (integrity-failed, not yet
@@ -1329,8 +1825,10 @@ class PipelineEngine:
                 quiet = torch.maximum(glob, (gr > 0).float())
                 b = torch.maximum(p, b * (1.0 - quiet))
                 ev = torch.maximum(torch.maximum(p.max(), o.max() * (1.0 - quiet)), glob)
-            blame[idx] = b
-            evidence[idx] = ev.expand(n)
+            gb = gbad[idx]
+            blame[idx] = torch.maximum(b, gb)
+            # a gradient rewritten after the backward skips that stage's update (it does not echo)
+            evidence[idx] = torch.maximum(ev.expand(n), gb)
         return blame, evidence
 
     # ================================================================== heartbeat -> OFFLINE
@@ -1502,7 +2000,8 @@ class PipelineEngine:
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
         statuses = [int(v) for v in host[N * SV.DIGEST + N:N * SV.DIGEST + 2 * N].tolist()]
         blamed = [v > 0 for v in host[N * SV.DIGEST + 2 * N:N * SV.DIGEST + 3 * N].tolist()]
-        audit_bad = [v > 0 for v in host[N * SV.DIGEST + 3 * N:N * SV.DIGEST + 4 * N].tolist()]
+        audit_kind = [int(v) for v in host[N * SV.DIGEST + 3 * N:N * SV.DIGEST + 4 * N].tolist()]
+        audit_bad = [k > 0 for k in audit_kind]
         present = set(self.all_ranks())
         lasts = [n for n in self.last_ranks() if D[n][SV.D_PRESENT] > 0]
         self.last_loss = sum(D[n][SV.D_LOSS] for n in lasts) / len(lasts) if lasts else None
@@ -1516,8 +2015,7 @@ class PipelineEngine:
             param_flag = row[SV.D_PARAM_FLAG] > 0
             flagged = blamed[n]
             if flagged:
-                kind = "model_poisoning" if param_flag else ("output_tampering" if audit_bad[n] else (
-                    "output_anomaly" if out_flag and not self.cfg.audit else "gradient_poisoning"))
+                kind = self._evidence_kind(param_flag, audit_kind[n], out_flag)
                 rec = {"node_id": n, "timestamp": time.time(), "step": step, "attack_type": kind,
                        "output_stats": {"mean": row[SV.D_OUT_MEAN], "std": row[SV.D_OUT_STD],
                                         "z": row[SV.D_OUT_Z]},
@@ -1533,8 +2031,9 @@ class PipelineEngine:
                 ds = self.detector.detection_stats
                 if flagged:
                     ds["total_detections"] += 1
-                    k = "model_poisoning" if param_flag else ("byzantine" if audit_bad[n] or (out_flag and not self.cfg.audit)
-                                                              else "gradient_poisoning")
+                    k = self._evidence_kind(param_flag, audit_kind[n], out_flag)
+                    k = {"output_tampering": "byzantine", "output_anomaly": "byzantine",
+                         "gradient_tampering": "byzantine"}.get(k, k)
                     ds["attack_types"][k] = ds["attack_types"].get(k, 0) + 1
                 key = ("true_positives" if gt else "false_positives") if flagged else \
                       ("false_negatives" if gt else "true_negatives")
@@ -1569,6 +2068,19 @@ class PipelineEngine:
         util = 1.0 - (self._comm_wait / self._step_time) if self._step_time > 0 else 0.0
         for n in range(N):
             self._host_metrics[n] = [self._comm_wait, max(0.0, min(1.0, util)), 0.0, 1.0]
+
+    def _evidence_kind(self, param_flag: bool, kind: int, out_flag: bool) -> str:
+        """Attack record type from the evidence behind a blame (audit bitmask AK_*, 32 = applied
+        gradient differs from the committed backward)."""
+        if param_flag or kind & SV.AK_WHASH:
+            return "model_poisoning"
+        if kind & SV.AK_FWD:
+            return "output_tampering"
+        if kind & (SV.AK_DX | SV.AK_DXHASH):
+            return "gradient_tampering"
+        if kind & (SV.AK_DW | 32):
+            return "gradient_poisoning"
+        return "output_anomaly" if out_flag and not self.cfg.audit else "gradient_poisoning"
 
     # ================================================================== re-sharding (task reassignment)
     def estimate_migration_time(self, layer_numel: int, links: int = 1, plan: Optional[PlacementPlan] = None) -> float:
@@ -1642,13 +2154,20 @@ class PipelineEngine:
             # same all-gathered report, but floats / trust state must not be able to split the job)
             new_plan = PlacementPlan.from_list(broadcast_ints(new_plan.to_list() if self.rank == 0 else None, 0,
                                                               self.device))
-        restored = {c: self._shadow_meta[c][0] for c in compromised if self._shadow_usable(c)}
+        # a compromised stage's layers never come from its own memory: from a committed shadow held by
+        # a trusted holder whose copy verifies, else from the initial weights
+        verified = self._verify_shadows() if self._shadow_meta else {}
+        sources = {c: self._shadow_source(c, compromised, verified) for c in compromised}
+        restored = {c: self._shadow_meta[c][0] for c in compromised if sources[c] is not None}
+        fresh = [c for c in compromised if sources[c] is None]
+        if fresh:
+            logger.warning("no verified shadow for %s: their layers restart from the initial weights", fresh)
         to_move = sum(self._layer_numel(li) for li in range(self.num_layers)
                       if self.plan.owner_of_layer(li) != new_plan.owner_of_layer(li) or
-                      any(self.plan.owner_of_layer(li) == c for c in restored))
+                      any(self.plan.owner_of_layer(li) == c for c in compromised))
         predicted = self.estimate_migration_time(to_move, plan=new_plan)   # before the move: a prediction
         t0 = time.perf_counter()
-        moved = self._migrate(new_plan, restore=list(restored))
+        moved = self._migrate(new_plan, restore={c: sources[c] for c in restored}, fresh=fresh)
         dt = time.perf_counter() - t0
         self.excluded = sorted(set(self.excluded) | set(compromised))
         for c in compromised:     # the tampered weights now live nowhere (restored or re-placed)
@@ -1662,6 +2181,8 @@ class PipelineEngine:
                "phases": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in self._migrate_phases.items()},
                "moved_params": moved, "step": step if step is not None else self.global_step,
                "restored_from_shadow": restored,
+               "restored_from_initial": fresh,
+               "shadow_holders": {c: sources[c] for c in restored},
                "plan": new_plan.describe()}
         self.reassignment_history.append(rec)
         logger.warning("Reassigned tasks from %s -> %s in %.3fs; new plan %s", compromised, to_nodes, dt,
@@ -1682,6 +2203,17 @@ class PipelineEngine:
         for name, b in mod.named_buffers():
             parts.append(b.detach().reshape(-1).float())
         return torch.cat(parts) if parts else torch.zeros(0, device=st.device)
+
+    def _pack_initial(self, li: int, device) -> torch.Tensor:
+        """Layer ``li`` in the migration format from the host model (initial weights, zero AdamW
+        moments): the source of last resort for a compromised stage with no verified shadow."""
+        parts = []
+        for name, p in self.layers[li].named_parameters(remove_duplicate=False):
+            v = p.detach().reshape(-1).float()
+            parts += [v, torch.zeros_like(v), torch.zeros_like(v)]
+        for name, b in self.layers[li].named_buffers():
+            parts.append(b.detach().reshape(-1).float())
+        return torch.cat(parts).to(device) if parts else torch.zeros(0, device=device)
 
     def _packed_numel(self, li: int) -> int:
         layer = self.layers[li]
@@ -1706,9 +2238,12 @@ class PipelineEngine:
             b.copy_(vec[off:off + n].view(b.shape).to(b.dtype))
             off += n
 
-    def _migrate(self, new_plan: PlacementPlan, restore: Sequence[int] = ()) -> int:
-        """Move every layer to its new owner.  Layers of the nodes in ``restore`` come from their
-        last committed shadow snapshot (held by a trusted neighbour), not from the node itself.
+    def _migrate(self, new_plan: PlacementPlan, restore: Optional[Dict[int, int]] = None,
+                 fresh: Sequence[int] = ()) -> int:
+        """Move every layer to its new owner.  Layers of the nodes in ``restore`` (owner -> serving
+        holder) come from their last committed shadow snapshot, those of the nodes in ``fresh``
+        from the initial weights (built by the new owner from the host model) — never from the
+        compromised node itself.
 
         Phases (timed into ``self._migrate_phases``, seconds, device-synchronised at each boundary):
         pack (fp32 master + moments + buffers of every layer leaving or staying, one device vector per
@@ -1718,10 +2253,11 @@ class PipelineEngine:
         old_plan = self.plan
         self._old_owner = {li: old_plan.owner_of_layer(li) for li in range(self.num_layers)}
         from_shadow: Dict[int, int] = {}     # layer -> holder rank serving it from a shadow
-        for c in restore:
+        for c, h in (restore or {}).items():
             a, b = self._shadow_meta[c][1]
             for li in range(a, b):
-                from_shadow[li] = self._shadow_meta[c][2]
+                from_shadow[li] = h
+        from_init = {li for c in fresh for li in range(self.num_layers) if old_plan.owner_of_layer(li) == c}
         step_count = next(iter(self.stages.values())).flat.step_count if self.stages else 0
         packed: Dict[int, torch.Tensor] = {}
         moved = 0
@@ -1735,6 +2271,11 @@ class PipelineEngine:
                 src, dst = old_plan.owner_of_layer(li), new_plan.owner_of_layer(li)
                 if li in from_shadow:
                     src = from_shadow[li]
+                if li in from_init:
+                    if dst == self.rank:
+                        packed[li] = self._pack_initial(li, self.device)
+                    moved += self._layer_numel(li)
+                    continue
                 if src == self.rank:
                     vec = (self._shadow_slice(li) if li in from_shadow
                            else self._pack_layer(self.stages[self.rank], li))
@@ -1760,8 +2301,11 @@ class PipelineEngine:
             # every stage is local: the packed vectors stay on the device (no host round trip)
             for li in range(self.num_layers):
                 src, dst = old_plan.owner_of_layer(li), new_plan.owner_of_layer(li)
-                packed[li] = (self._shadow_slice(li) if li in from_shadow
-                              else self._pack_layer(self.stages[src], li))
+                if li in from_init:
+                    packed[li] = self._pack_initial(li, self.stages[src].device)
+                else:
+                    packed[li] = (self._shadow_slice(li) if li in from_shadow
+                                  else self._pack_layer(self.stages[src], li))
                 if src != dst:
                     moved += self._layer_numel(li)
             self._sync_all()
@@ -1804,7 +2348,8 @@ class PipelineEngine:
         self._sync_all()
         ph["unpack_s"] = time.perf_counter() - t3
         self._shape_cache = {}
-        self._reset_shadows()                # the snapshot ring follows the plan: re-taken next interval
+        self._gsk_cache = {}
+        self.refresh_shadows()               # the snapshot ring follows the plan: a fresh committed copy now
         ph["transfer_bytes"] = xfer_bytes
         ph["local_bytes"] = sum(self._packed_numel(li) * 4 for li in range(self.num_layers)
                                 if not self.distributed or self.plan.owner_of_layer(li) == self.rank)
@@ -1816,34 +2361,81 @@ class PipelineEngine:
         return moved
 
     # ================================================================== trusted shadow snapshots
-    # SURVEY 5 ("shadow copies of each stage's weights on a neighbour GPU"): every
-    # ``shadow_interval`` steps each stage packs its layers (fp32 master + AdamW moments + buffers,
-    # the migration format) and sends them over xGMI to the next stage of the ring, which keeps the
-    # copy in HBM (~0.5 GB for a GPT-2-medium stage).  The copy is committed only when that step's
-    # report shows the stage unflagged; a stage later marked compromised is rebuilt from its last
-    # committed copy instead of from its own (possibly tampered) memory.  Metadata (step, layer
-    # range, holder) is tracked identically on every rank; only the holder keeps the data.
+    # SURVEY 5 ("shadow copies of each stage's weights on a neighbour GPU"): when the stages are
+    # (re)built and every ``shadow_interval`` steps each stage packs its layers (fp32 master + AdamW
+    # moments + buffers, the migration format) and sends them over xGMI to the next
+    # ``shadow_copies`` stages of the ring, which keep the copies in HBM (~0.5 GB per GPT-2-medium
+    # stage).  The owner's checksum of the packed vector is recorded on every rank.  A periodic
+    # copy is committed only when that step's report shows the stage unflagged (the build-time
+    # copy at once: the weights come from initialisation, a checkpoint or trusted sources).  A
+    # stage later marked compromised is rebuilt from a committed copy held by a trusted holder
+    # whose bytes still match the owner's checksum — never from its own (possibly tampered)
+    # memory; with no such copy its layers restart from their initial weights.  Metadata (step,
+    # layer range, holders, owner checksum) is identical on every rank; only holders keep data.
     def _reset_shadows(self):
-        self._shadow_meta: Dict[int, Tuple[int, Tuple[int, int], int]] = {}   # owner -> committed (step, range, holder)
-        self._shadow_pend_meta: Dict[int, Tuple[int, Tuple[int, int], int]] = {}
-        self._shadow_data: Dict[int, torch.Tensor] = {}      # owner -> committed vector (holder only)
+        # owner -> committed (step, layer range, primary holder, holders)
+        self._shadow_meta: Dict[int, Tuple[int, Tuple[int, int], int, List[int]]] = {}
+        self._shadow_pend_meta: Dict[int, Tuple[int, Tuple[int, int], int, List[int]]] = {}
+        self._shadow_data: Dict[int, torch.Tensor] = {}      # owner -> committed vector (holders only)
         self._shadow_pend: Dict[int, Tuple[int, torch.Tensor]] = {}
+        self._shadow_hash: Dict[int, torch.Tensor] = {}      # owner -> committed owner checksum (every rank)
+        self._shadow_pend_hash: Dict[int, torch.Tensor] = {}
 
     def _shadow_enabled(self) -> bool:
         return self.cfg.shadow_interval > 0 and self.dp == 1 and self.plan.num_stages > 1
 
-    def _shadow_holder(self, node: int) -> int:
+    def _shadow_holders(self, node: int) -> List[int]:
         ranks = self.plan.ranks
-        return ranks[(ranks.index(node) + 1) % len(ranks)]
+        i = ranks.index(node)
+        k = max(1, min(int(self.cfg.shadow_copies), len(ranks) - 1))
+        return [ranks[(i + d) % len(ranks)] for d in range(1, k + 1)]
 
-    def _shadow_usable(self, c: int) -> bool:
-        if c not in self._shadow_meta:
-            return False
-        holder = self._shadow_meta[c][2]
-        return holder not in self.excluded and self.trust.can_assign_task(holder)
+    def _shadow_holder(self, node: int) -> int:
+        return self._shadow_holders(node)[0]
+
+    def _shadow_usable(self, c: int, bad: Sequence[int] = ()) -> bool:
+        return self._shadow_source(c, bad) is not None
+
+    def _shadow_source(self, c: int, bad: Sequence[int] = (), verified: Optional[Dict] = None) -> Optional[int]:
+        """The holder that serves owner ``c``'s committed copy: the first of its holders that is
+        not excluded, not among ``bad`` (the nodes being compromised now), may take tasks and (when
+        ``verified`` is given) whose copy still matches the owner's checksum."""
+        meta = self._shadow_meta.get(c)
+        if meta is None:
+            return None
+        for h in meta[3]:
+            if h in self.excluded or h in bad or not self.trust.can_assign_task(h):
+                continue
+            if verified is not None and not verified.get((c, h), False):
+                continue
+            return h
+        return None
+
+    def _verify_shadows(self) -> Dict[Tuple[int, int], bool]:
+        """(owner, holder) -> the holder's committed copy matches the owner's checksum.  Each rank
+        checks the copies it holds; distributed: one all-gather so every rank decides alike."""
+        N = self.num_nodes
+        mine = torch.zeros(N, dtype=torch.float32, device=self.device)
+        for c, vec in self._shadow_data.items():
+            ref = self._shadow_hash.get(c)
+            if ref is not None:
+                ok = torch.equal(dstats.checksum(vec).to(ref.device), ref)
+                mine[c] = 1.0 if ok else 0.0
+        out: Dict[Tuple[int, int], bool] = {}
+        if self.distributed:
+            V = all_gather_rows(mine, self.world).cpu()
+            for c, meta in self._shadow_meta.items():
+                for h in meta[3]:
+                    out[(c, h)] = bool(V[h, c] > 0)
+        else:
+            for c, meta in self._shadow_meta.items():
+                for h in meta[3]:
+                    out[(c, h)] = bool(mine[c] > 0)
+        return out
 
     def _shadow_slice(self, li: int) -> torch.Tensor:
-        for c, (_, (a, b), holder) in self._shadow_meta.items():
+        for c, meta in self._shadow_meta.items():
+            a, b = meta[1]
             if a <= li < b:
                 off = sum(self._packed_numel(k) for k in range(a, li))
                 return self._shadow_data[c][off:off + self._packed_numel(li)]
@@ -1854,41 +2446,71 @@ class PipelineEngine:
         step = self.global_step
         owners = list(self.plan.ranks)
         for node, rng in zip(self.plan.ranks, self.plan.ranges):
-            self._shadow_pend_meta[node] = (step, tuple(rng), self._shadow_holder(node))
+            hs = self._shadow_holders(node)
+            self._shadow_pend_meta[node] = (step, tuple(rng), hs[0], hs)
         if self.distributed:
             st = self.my_stage()
+            vec = (torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)]) if st is not None
+                   else torch.zeros(0, device=self.device))
+            h = dstats.checksum(vec) if st is not None else torch.zeros(3, dtype=torch.float64, device=self.device)
+            H = all_gather_rows(h, self.world)
+            for node in owners:
+                self._shadow_pend_hash[node] = H[node].clone()
             if st is None:
                 return
-            i = owners.index(self.rank)
-            pred = owners[(i - 1) % len(owners)]
-            a, b = self.plan.ranges[(i - 1) % len(owners)]
-            vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
-            buf = torch.empty(sum(self._packed_numel(li) for li in range(a, b)), dtype=torch.float32,
-                              device=self.device)
-            self._note_peers([(vec, self._shadow_holder(self.rank))], [(buf, pred)])
-            batched_transfer([(vec, self._shadow_holder(self.rank))], [(buf, pred)], meter=self.link_meter)
-            self._shadow_pend[pred] = (step, buf)
+            sends = [(vec, hd) for hd in self._shadow_holders(self.rank)]
+            recvs = []
+            for o in owners:
+                if o != self.rank and self.rank in self._shadow_holders(o):
+                    a, b = self.plan.ranges[owners.index(o)]
+                    buf = torch.empty(sum(self._packed_numel(li) for li in range(a, b)), dtype=torch.float32,
+                                      device=self.device)
+                    recvs.append((buf, o))
+                    self._shadow_pend[o] = (step, buf)
+            self._note_peers(sends, recvs)
+            batched_transfer(sends, recvs, meter=self.link_meter)
         else:
             for node, st in self.stages.items():
                 dev = self.stages[self._shadow_holder(node)].device
                 vec = torch.cat([self._pack_layer(st, li) for li in range(*st.layer_range)])
+                self._shadow_pend_hash[node] = dstats.checksum(vec)
                 self._shadow_pend[node] = (step, vec.to(dev, copy=True))
+
+    def refresh_shadows(self):
+        """Take and commit a snapshot now (stages freshly built from trusted weights: at start-up,
+        after a re-shard, after a checkpoint load), so a committed copy exists from step 0 on."""
+        if not self._shadow_enabled():
+            return
+        self._reset_shadows()
+        self._take_shadow()
+        for owner in list(self._shadow_pend_meta):
+            self._commit_one(owner, self.global_step)
+
+    def _commit_one(self, owner: int, step: int) -> None:
+        meta = self._shadow_pend_meta.pop(owner)
+        data = self._shadow_pend.pop(owner, None)
+        if data is not None and data[0] != step:   # a newer snapshot replaced it: keep that one
+            self._shadow_pend[owner] = data
+            data = None
+        self._shadow_meta[owner] = meta
+        if owner in self._shadow_pend_hash:
+            self._shadow_hash[owner] = self._shadow_pend_hash.pop(owner)
+        if data is not None:
+            self._shadow_data[owner] = data[1]
 
     def _commit_shadows(self, step: int, blamed: Sequence[bool], statuses: Sequence[int]):
         bad = (STATUS_CODES[NodeStatus.COMPROMISED], STATUS_CODES[NodeStatus.SUSPICIOUS])
         for owner, meta in list(self._shadow_pend_meta.items()):
             if meta[0] != step:
                 continue
-            del self._shadow_pend_meta[owner]
-            data = self._shadow_pend.pop(owner, None)
-            if data is not None and data[0] != step:   # a newer snapshot replaced it: keep that one
-                self._shadow_pend[owner] = data
-                data = None
             if blamed[owner] or statuses[owner] in bad:
+                self._shadow_pend_meta.pop(owner)
+                data = self._shadow_pend.pop(owner, None)
+                if data is not None and data[0] != step:
+                    self._shadow_pend[owner] = data
+                self._shadow_pend_hash.pop(owner, None)
                 continue
-            self._shadow_meta[owner] = meta
-            if data is not None:
-                self._shadow_data[owner] = data[1]
+            self._commit_one(owner, step)
 
     # ================================================================== evaluation
     @torch.no_grad()
@@ -1995,6 +2617,7 @@ class PipelineEngine:
                 st.flat.data.copy_(st.flat.master)
             st.param_checksum = None
         bump_weight_generation()
+        self.refresh_shadows()    # the loaded weights are the new trusted copy
 
     def load_stage_states(self, model_sd: Dict[int, Dict], optim_sd: Dict[int, Dict],
                           verifier_sd: Optional[Dict[int, Dict]] = None):
@@ -2018,3 +2641,4 @@ class PipelineEngine:
             if verifier_sd and node in verifier_sd:
                 st.verifier.load_state_dict(verifier_sd[node])
             st.param_checksum = None  # weights legitimately replaced
+        self.refresh_shadows()        # the loaded weights are the new trusted copy

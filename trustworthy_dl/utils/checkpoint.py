@@ -161,6 +161,31 @@ def _node_map(saved_ids, live_ids) -> Dict[int, int]:
     return {i: where[int(p)] for i, p in enumerate(live_ids) if int(p) in where}
 
 
+def _saved_node_map(ck: Dict, live: int) -> Dict[int, int]:
+    """live rank -> saved node index of the same PHYSICAL node (see _resize_trust)."""
+    saved_n = int(ck["device_trust"]["values"].numel()) if "device_trust" in ck else \
+        int(ck.get("trust_manager", {}).get("num_nodes", live))
+    saved_ids = ck.get("node_ids") or list(range(saved_n))
+    return _node_map(saved_ids, node_ids_from_env(live))
+
+
+def resume_plan_ranks(ck: Dict, saved_ranks, live: int, pp: int):
+    """Where a saved plan's stages can run in a job of ``live`` ranks.
+
+    The saved plan names SAVED node indices; after an elastic restart on survivors those are
+    different ranks (or gone).  Returns ``(translated_ranks or None, excluded_live_ranks)``:
+    the saved ranks translated through the physical node ids, or None when a stage's node is gone,
+    out of the pipeline, or was excluded as compromised (then the caller re-plans over the live
+    ranks minus the excluded ones, so a compromised node never gets a stage back)."""
+    m = _saved_node_map(ck, live)
+    inv = {j: i for i, j in m.items()}
+    saved_ex = {int(n) for n in ck.get("excluded", [])}
+    live_ex = sorted(i for i, j in m.items() if j in saved_ex)
+    out = [inv.get(int(r)) for r in saved_ranks]
+    ok = len(out) <= pp and all(r is not None and r < pp and r not in live_ex for r in out)
+    return (out if ok else None), live_ex
+
+
 def _resize_trust(trainer, ck: Dict, live: int):
     """Trust state of a job resumed on ``live`` nodes.  Node records follow the PHYSICAL node: the
     checkpoint's ``node_ids`` and this job's (TDL_ELASTIC_NODE_IDS) map each live node to the saved
@@ -168,11 +193,7 @@ def _resize_trust(trainer, ck: Dict, live: int):
     COMPROMISED status to whichever survivor inherits its index.  Retired nodes' records stay in the
     attack / reassignment histories; nodes the saved job did not have start fresh."""
     tm = trainer.trust_manager
-    saved_n = int(ck["device_trust"]["values"].numel()) if "device_trust" in ck else \
-        int(ck.get("trust_manager", {}).get("num_nodes", live))
-    saved_ids = ck.get("node_ids") or list(range(saved_n))
-    live_ids = node_ids_from_env(live)
-    m = _node_map(saved_ids, live_ids)
+    m = _saved_node_map(ck, live)
     if "trust_manager" in ck:
         tm.load_state_dict(ck["trust_manager"])
         old_scores, old_status, old_metrics = tm.trust_scores, tm.node_status, tm.node_metrics
@@ -230,9 +251,12 @@ def load_checkpoint(trainer, path: str):
         e.set_granularity(g)  # layer indices of the saved plan refer to that unit size
         e._build()
     dp = getattr(e, "dp", 1)
+    # the saved plan's ranks are SAVED node indices: translate them to this job's ranks through the
+    # physical node ids first (after a rank shift an excluded node must not get a stage)
+    moved, live_ex = resume_plan_ranks(ck, saved_plan.ranks, e.num_nodes, e.pp)
     # with data-parallel replicas the manifest holds replica 0's plan; replicas share its layout
-    same = (saved_plan.ranks == e.plan.ranks or dp > 1) and saved_plan.ranges == e.plan.ranges
-    hostable = all(r < e.num_nodes for r in saved_plan.ranks) and len(saved_plan.ranks) <= e.pp
+    same = (moved == e.plan.ranks or dp > 1) and saved_plan.ranges == e.plan.ranges
+    hostable = moved is not None
     if same:
         # each rank reads its own shard (a DP replica's stage node is its own rank)
         full = consolidate(path, nodes=sorted(e.stages) if e.distributed else None)
@@ -241,9 +265,9 @@ def load_checkpoint(trainer, path: str):
         raise ValueError("resuming a data-parallel job under a different pipeline layout is not supported")
     else:
         if hostable:
-            new_plan = saved_plan
+            new_plan = PlacementPlan(list(moved), list(saved_plan.ranges), saved_plan.version)
         else:
-            live = list(range(e.pp))[: e.num_layers]
+            live = [r for r in range(e.pp) if r not in live_ex][: e.num_layers]
             new_plan = make_plan(e.costs, live, saved_plan.version + 1, e.cfg.balanced_partition)
         if e.distributed:
             new_plan = PlacementPlan.from_list(broadcast_ints(new_plan.to_list() if e.rank == 0 else None, 0,
