@@ -28,7 +28,11 @@
 // whole grid); TDL_ATTN_MAP=xcd -> one head's blocks back to back on one XCD (head_xcd_map).
 // dK/dV query-tile depth (32-row sub-tiles per barrier): TDL_ATTN_DKDV_NS=1|2 (default 1).  NS=2
 // measured slower on MI355X (B=32 H=16 T=1024 causal bwd: 306.6 vs 327.6 TFLOP/s; the second
-// staging register set and sub-tile loop cost more than the halved barrier count saves).
+// staging register set and sub-tile loop cost more than the halved barrier count saves).  A
+// software-pipelined form (two sub-tiles per barrier as straight-line S/dP(0), S/dP(1), [softmax |
+// dV/dK](0), [softmax | dV/dK](1), dP started from -delta) needs 389 VGPRs = one wave per SIMD and
+// measured 1220.7 vs 952.8 us for the whole backward at B=64 (profiles/r4_attn_dkdv_pipelined_ab.jsonl):
+// the second wave per SIMD hides more than the in-wave interleave does.
 static int dkdv_ns() {
     static int ns = [] {
         const char* e = std::getenv("TDL_ATTN_DKDV_NS");

@@ -148,8 +148,9 @@ def _colsum_into(acc, d):
 # (qkv / out / proj forward, qkv / out / fc dgrad) stay on the library GEMM, which the native kernel
 # reaches only 0.83-0.93x of on those shapes (profiles/r3_gemm_lab.jsonl).
 def _native_mlp(h2, wfc, bfc) -> bool:
-    # TDL_MLP_NATIVE=0: A/B only (library GEMM + the separate bias-GELU kernels for the MLP too)
-    if not h2.is_cuda or bfc.dtype != torch.bfloat16 or os.environ.get("TDL_MLP_NATIVE", "1") == "0":
+    # the separate bias-GELU kernels remain only for shapes the native GEMM does not take (and the
+    # CPU reference path)
+    if not h2.is_cuda or bfc.dtype != torch.bfloat16:
         return False
     from . import gemm
     return gemm.supported(h2, wfc)

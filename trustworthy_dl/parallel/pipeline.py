@@ -1213,7 +1213,7 @@ class PipelineEngine:
             # the weight commitment made after this stage's last update (before anything of this
             # step could touch the weights): the auditor checks the weights it receives against it
             pc = getattr(st, "param_checksum", None)
-            if pc is not None:
+            if pc is not None and self.cfg.audit and self.plan.num_stages > 1:
                 from ..security.grad_audit import fold_hash
                 d[SV.D_WHASH:SV.D_WHASH + 2].copy_(fold_hash(pc))
             else:
@@ -1823,8 +1823,14 @@ class PipelineEngine:
                 gr.copy_(torch.maximum(gr - 1.0, torch.zeros_like(gr)) * (1.0 - glob)
                          + glob * float(self.cfg.global_event_grace))
                 quiet = torch.maximum(glob, (gr > 0).float())
-                b = torch.maximum(p, b * (1.0 - quiet))
-                ev = torch.maximum(torch.maximum(p.max(), o.max() * (1.0 - quiet)), glob)
+                if audited:
+                    # a recompute mismatch is proof, not a statistic: never quieted (a grace window
+                    # opened by an earlier loss spike let tampered steps through in r4's first runs)
+                    b = torch.maximum(torch.maximum(p, o), b * (1.0 - quiet))
+                    ev = torch.maximum(torch.maximum(p.max(), o.max()), glob)
+                else:
+                    b = torch.maximum(p, b * (1.0 - quiet))
+                    ev = torch.maximum(torch.maximum(p.max(), o.max() * (1.0 - quiet)), glob)
             gb = gbad[idx]
             blame[idx] = torch.maximum(b, gb)
             # a gradient rewritten after the backward skips that stage's update (it does not echo)
