@@ -114,7 +114,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
         rsh = sorted(r["step"] for r in rs if n in r["from_nodes"])
         lag[str(n)] = {"first_tamper": inj[0] if inj else None, "first_detect": det[0] if det else None,
                        "reshard": rsh[0] if rsh else None,
-                       "tampered_reports_before_reshard": (len([s for s in inj if s <= rsh[0]]) if inj and rsh else None)}
+                       "tampered_steps_before_reshard": (len({s for s in inj if s <= rsh[0]}) if inj and rsh else None)}
     compromised = [n for n in range(8) if eng.trust.get_node_status(n).value == "compromised"]
     rec = {
         "config": cfg_id, "seed": seed, "reassign": reassign, "audit": audit,
