@@ -192,6 +192,10 @@ def run(args):
             rank, world, args.watchdog, store=dist.distributed_c10d._get_default_store(),
             on_failure=lambda kind, marks, errs: print(_failure_line(args, kind, marks, errs), flush=True)
             if rank == 0 else None).start()
+    # TDL_COMMCHECK=<dir>: record this rank's communication for the RCCL-model replay
+    # (trustworthy_dl/runtime/commcheck.py; the multi-rank CPU tests check the schedule with it)
+    from trustworthy_dl.runtime import commcheck
+    _rec = commcheck.maybe_install() if world > 1 else None
     hwq = effective_hw_queues()
     print(f"[bench] rank {rank} local_rank {local_rank} GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} "
           f"effective_hw_queues={hwq}", file=sys.stderr, flush=True)
@@ -230,6 +234,7 @@ def run(args):
     def sync():
         if world > 1:
             dist.barrier()
+        commcheck.note_host_sync(device=True)
         if use_cuda:
             torch.cuda.synchronize()
 
@@ -324,6 +329,8 @@ def run(args):
         _WATCHDOG.finish()
     if world > 1:
         dist.barrier()
+        if _rec is not None:
+            _rec.dump()
         dist.destroy_process_group()
 
 

@@ -155,8 +155,11 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ x, const float* __restrict__ mean,
                                                                 const float* __restrict__ rstd, float* __restrict__ part,
                                                                 int64_t M, int C, int rows_per_block, int relu,
-                                                                const float* __restrict__ pro) {
+                                                                const float* __restrict__ pro,
+                                                                unsigned* __restrict__ fold_cnt) {
     __shared__ float red[2][256][8];
+    // the fold (next launch on the stream) counts its arrivals here: zero the counters
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < (2 * C + 255) / 256) fold_cnt[threadIdx.x] = 0u;
     const int CV = C >> 3;
     const int VPB = CV < 256 ? CV : 256;
     const int RPB = 256 / VPB;
@@ -234,23 +237,45 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
     }
 }
 
-// Sum of the nb partial rows -> replica 0 (zeroed by the forward): grid (2C / 256, FOLD_G), each
-// thread one column over the rows of its group (coalesced across the wave, 4 loads in flight).
-__global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, const float* __restrict__ partials,
-                                                              int nb, int C) {
+// Sum of the nb partial rows -> replica 0 (zeroed by the forward), in a FIXED order (the recompute
+// audit evaluates a stage twice and compares; see conv.hip stats_finalize_kernel): grid (2C / 256,
+// FOLD_G), each thread one column over the rows r = y (mod FOLD_G) of its group (coalesced across
+// the wave, 4 loads in flight), the group total stored in row y (read by this group only); the LAST
+// group of the column block to arrive (agent-scope counter, release / acquire) adds the FOLD_G
+// totals in group order.  cnt: zeroed by bn_act_bwd_reduce_kernel.
+__global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, float* __restrict__ partials,
+                                                              int nb, int C, unsigned* __restrict__ cnt) {
+    __shared__ int is_last;
     const int col = blockIdx.x * blockDim.x + threadIdx.x;
-    if (col >= 2 * C) return;
-    const float* part = partials + col;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int r = blockIdx.y;
-    for (; r + 3 * FOLD_G < nb; r += 4 * FOLD_G) {
-        a0 += part[(size_t)r * 2 * C];
-        a1 += part[(size_t)(r + FOLD_G) * 2 * C];
-        a2 += part[(size_t)(r + 2 * FOLD_G) * 2 * C];
-        a3 += part[(size_t)(r + 3 * FOLD_G) * 2 * C];
+    float* part = partials + col;
+    if (col < 2 * C) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int r = blockIdx.y;
+        for (; r + 3 * FOLD_G < nb; r += 4 * FOLD_G) {
+            a0 += part[(size_t)r * 2 * C];
+            a1 += part[(size_t)(r + FOLD_G) * 2 * C];
+            a2 += part[(size_t)(r + 2 * FOLD_G) * 2 * C];
+            a3 += part[(size_t)(r + 3 * FOLD_G) * 2 * C];
+        }
+        for (; r < nb; r += FOLD_G) a0 += part[(size_t)r * 2 * C];
+        // row y < FOLD_G <= NB_MAX; agent-scope (sc1, write-through) store: see stats_finalize_kernel
+        __hip_atomic_store(part + (size_t)blockIdx.y * 2 * C, (a0 + a1) + (a2 + a3), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
-    for (; r < nb; r += FOLD_G) a0 += part[(size_t)r * 2 * C];
-    atomicAdd(sums + col, (a0 + a1) + (a2 + a3));
+    // every storing wave drains its stores (workgroup-scope release: s_waitcnt), then one lane counts in
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = prev == FOLD_G - 1;
+    }
+    __syncthreads();
+    if (!is_last || col >= 2 * C) return;
+    float a = 0.f;
+#pragma unroll
+    for (int g = 0; g < FOLD_G; ++g)
+        a += __hip_atomic_load(part + (size_t)g * 2 * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sums[col] += a;
 }
 
 // ---------------------------------------------------------------- backward pass 2: elementwise
@@ -348,7 +373,8 @@ int grid_for(int64_t nvec) {
 // (replicas + their sum; kept from the forward to the backward, so only (NREP + 1) x 2C)
 TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1) * 2 * C; }
 // Floats of the backward's per-block partial rows (scratch of ONE backward call, not kept).
-TDL_API int64_t tdl_bn_bwd_part_floats(int C) { return (int64_t)NB_MAX * 2 * C; }
+// + the fold's arrival counters (one per 256-column block)
+TDL_API int64_t tdl_bn_bwd_part_floats(int C) { return (int64_t)NB_MAX * 2 * C + (2 * C + 255) / 256; }
 
 // stats: [2C] (sum, sumsq) in training mode, or null to normalise with run_mean/run_var (eval).
 // save_mean/save_rstd: [C] or null.  upd_mean/upd_var: running buffers to update (train) or null.
@@ -397,8 +423,10 @@ static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, con
     const int nb = (int)((M + rows_per_block - 1) / rows_per_block);
     const dim3 grid((unsigned)nb, gy);
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
-                                                  part, M, C, (int)rows_per_block, relu, pro);
-    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, part, nb, C);
+                                                  part, M, C, (int)rows_per_block, relu, pro,
+                                                  (unsigned*)(part + (size_t)NB_MAX * 2 * C));
+    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, part, nb, C,
+                                                                            (unsigned*)(part + (size_t)NB_MAX * 2 * C));
     bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
     bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
         (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,

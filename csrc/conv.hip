@@ -60,6 +60,7 @@ struct ConvDims {
 };
 
 constexpr int BM = 128;  // m (pixels) per workgroup
+constexpr int FIN_CNT = 256;  // statistics-finalize arrival counters (column blocks of 64, 2 Cout <= 16384)
 constexpr int BK = 64;   // k per step
 
 // ============================================================================ conv_nt (fwd / dgrad)
@@ -91,11 +92,13 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                                                          bf16_t* __restrict__ out, float* __restrict__ part,
                                                          ConvDims d, const float* __restrict__ pro,
                                                          const bf16_t* __restrict__ bx = nullptr,
-                                                         float* __restrict__ zero_stats = nullptr) {
+                                                         float* __restrict__ zero_stats = nullptr,
+                                                         unsigned* __restrict__ fin_cnt = nullptr) {
     // the statistics finalize (next launch on the stream) accumulates into stats: zero it here
-    // instead of a separate memset launch per convolution
+    // instead of a separate memset launch per convolution; likewise its arrival counters
     if (zero_stats != nullptr && blockIdx.x == 0)
         for (int i = threadIdx.x; i < 2 * d.Cout; i += blockDim.x) zero_stats[i] = 0.f;
+    if (fin_cnt != nullptr && blockIdx.x == 0 && threadIdx.x < FIN_CNT) fin_cnt[threadIdx.x] = 0u;
     static_assert(!(PRO && TRANSPOSED), "the BN prologue applies to forward activations only");
     static_assert(!BNB || (TRANSPOSED && STATS), "BN-backward sums: data-gradient kernels with the STATS rows");
     constexpr int TCO = BCO / 64;   // 32-row cout tiles per wave (waves are 2 x 2)
@@ -307,10 +310,19 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
     }
 }
 
-// stats[c] = sum over the ntm partial rows of part[r][c], c < 2*Cout (stats zeroed by the caller)
-__global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __restrict__ part, int rows, int cols,
-                                                             int rows_per_block, float* __restrict__ stats) {
+// stats[c] += sum over the ntm partial rows of part[r][c], c < 2*Cout, in a FIXED order: the
+// recompute audit (parallel/pipeline.py) compares a stage's outputs and gradients with a second
+// evaluation, so BatchNorm statistics must not depend on the order fp32 atomics land in (a float-
+// atomic version differed by up to one bf16 ulp per call, which the BN backward amplified to 4-10 %
+// of the largest input gradient: scripts/audit_probe.py, profiles/r4_audit_probe_resnet50.txt).
+// Workgroup (x, y) sums rows [y rpb, (y + 1) rpb) of its 64 columns and stores the total in the
+// group's first row; the LAST workgroup of column block x to arrive (agent-scope counter, release /
+// acquire) adds the gridDim.y group totals in group order.  fin_cnt: zeroed by the conv kernel.
+__global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__ part, int rows, int cols,
+                                                             int rows_per_block, float* __restrict__ stats,
+                                                             unsigned* __restrict__ fin_cnt) {
     __shared__ float red[4][64];
+    __shared__ int is_last;
     const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
     const int r0 = blockIdx.y * rows_per_block;
     const int r1 = min(rows, r0 + rows_per_block);
@@ -319,8 +331,31 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(const float* __rest
         for (int r = r0 + rg; r < r1; r += 4) acc += part[(size_t)r * cols + c];
     red[rg][threadIdx.x & 63] = acc;
     __syncthreads();
-    if (rg == 0 && c < cols) atomicAdd(stats + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                      red[3][threadIdx.x]);
+    // wave 0 (rg == 0) stores the group total as an agent-scope (sc1, write-through) store and
+    // drains it before thread 0 of that same wave counts in; the last workgroup reads the totals
+    // with sc1 loads (no L2 write-back / invalidate fences: a wbl2 per workgroup wrote back the
+    // convolution's whole dirty output and cost ~1.4 % of a ResNet-50 step)
+    if (rg == 0 && c < cols)
+        __hip_atomic_store(part + (size_t)r0 * cols + c,
+                           ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores have landed
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(fin_cnt + blockIdx.x, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        is_last = prev == gridDim.y - 1;
+    }
+    __syncthreads();
+    if (!is_last) return;
+    float a = 0.f;
+    if (c < cols)
+        for (int g = rg; g < (int)gridDim.y; g += 4)
+            a += __hip_atomic_load(part + (size_t)g * rows_per_block * cols + c, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    red[rg][threadIdx.x & 63] = a;
+    __syncthreads();
+    if (rg == 0 && c < cols)
+        stats[c] += ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
 // ============================================================================ conv_wgrad
@@ -488,7 +523,9 @@ bool dims_ok(const ConvDims& d) {
 // transposed = 1 -> data-gradient mapping (act = dY, wk = W permuted to [Cin][R][S][Cout]).
 // stats: null, or fp32 [2 * Cout] = (per-channel sum, sum of squares) of out; then stats_ws must
 // hold tdl_conv_stats_ws_floats(...) floats (one partial row per 128-pixel tile).
-TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) { return (int64_t)((M + BM - 1) / BM) * 2 * Cout; }
+TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) {
+    return (int64_t)((M + BM - 1) / BM) * 2 * Cout + FIN_CNT;   // + the finalize's arrival counters
+}
 
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
                         int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
@@ -507,10 +544,13 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     auto W = (const bf16_t*)wk;
     auto O = (bf16_t*)out;
     float* zs = (st && !stats_accumulate) ? stats : nullptr;
-#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr, nullptr, zs)
-#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, nullptr, zs)
+    unsigned* cnt = st ? (unsigned*)(stats_ws + (size_t)ntm * 2 * Cout) : nullptr;
+    if (st && (2 * Cout + 63) / 64 > FIN_CNT) return (int)hipErrorInvalidValue;
+#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr, nullptr, zs, cnt)
+#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, nullptr, zs, \
+                                                                                  cnt)
 #define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, \
-                                                                                    (const bf16_t*)bnb_x)
+                                                                                    (const bf16_t*)bnb_x, nullptr, cnt)
     if (bnb) {
         if (big) LAUNCHB(128);
         else LAUNCHB(64);
@@ -530,7 +570,7 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     if (st) {
         const int rpb = 64;
         const dim3 g((2 * Cout + 63) / 64, (ntm + rpb - 1) / rpb);
-        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats);
+        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats, cnt);
     }
     TDL_LAUNCH_CHECK();
 }

@@ -56,6 +56,10 @@ CONFIGS["3m"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_po
                                                       micro_batches=1), targets=[3], lr=1e-4)
 CONFIGS["5m"] = dict(model="gpt2-medium", attack=dict(attack_types=["byzantine"], intensity=0.5, micro_batches=1),
                      targets=[2, 5], lr=1e-4)
+# one micro-batch's weight-gradient contribution scaled (its committed sketch norm stands out: the
+# targeted audit picks it)
+CONFIGS["3ms"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="scale",
+                                                       micro_batches=1), targets=[3], lr=1e-4)
 CONFIGS["liar"] = dict(model="gpt2-medium", attack=dict(attack_types=["model_poisoning"], intensity=0.05,
                                                         lie_integrity=True), targets=[6], lr=1e-4)
 
@@ -127,7 +131,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
                       if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
         "injections": len(att.injections) if att is not None else 0,
         "tampered_steps": len({(i["node"], i["step"]) for i in att.injections}) if att is not None else 0,
-        "per_target": lag, "micro_batches": max(1, batch // mbs),
+        "per_target": lag, "micro_batches": max(1, batch // mbs), "audit_summary": eng.audit_summary(),
         "clean_nodes_blamed": clean_blamed,
         "clean_nodes_compromised": [n for n in compromised if n not in c["targets"]],
         "clean_nodes_resharded": sorted({n for r in rs for n in r["from_nodes"] if n not in c["targets"]}),
@@ -153,7 +157,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean, 3s, dx, last, 3m, 5m, liar")
+    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean, 3s, dx, last, 3m, 3ms, 5m, liar")
     ap.add_argument("--seeds", default="3", help="comma list of attacker / monitor seeds")
     ap.add_argument("--no-reassign", action="store_true", help="detection only: the target keeps its layers, so "
                     "every injection is scored (a re-shard ends the attack after the first detections)")

@@ -109,6 +109,40 @@ def test_local_one_of_m_gradient_poisoning_caught_by_recompute():
     assert all(k == "gradient_poisoning" for _, _, k in got)
 
 
+@pytest.mark.parametrize("targeted", [None, False])
+def test_local_one_of_m_output_tamper_targeted(targeted):
+    """A Byzantine stage that tampers ONE micro-batch's output per step: the uniform private choice
+    alone recomputes it with probability 1/M; with the targeted audit (default in local mode) the
+    auditor also recomputes the micro-batch whose output statistics stand out, so every tampered
+    step is caught.  Never a clean stage."""
+    eng = _engine(3, "byzantine", targets=(1,), micro=4, atk_kw={"micro_batches": 1}, audit_targeted=targeted)
+    for b in _batches(26, bs=8):
+        eng.train_step(b)
+    eng.flush()
+    got = _blamed(eng)
+    assert {n for _, n, _ in got} == {1}, got
+    steps = {s for s, _, _ in got}
+    if targeted is None:
+        assert steps == set(range(6, 27)), steps
+        assert eng.audit_summary()["targeted_extra"] > 0
+    else:
+        assert 0 < len(steps) < 21, steps     # ~1/M of the tampered steps
+        assert eng.audit_summary()["targeted_extra"] == 0
+
+
+def test_local_one_of_m_gradient_scale_targeted():
+    """One micro-batch's weight-gradient contribution scaled inside the backward: its committed
+    sketch norm stands out, the targeted audit recomputes it on most tampered steps."""
+    eng = _engine(3, "gradient_poisoning", targets=(1,), micro=4,
+                  atk_kw={"gradient_mode": "scale", "micro_batches": 1})
+    for b in _batches(26, bs=8):
+        eng.train_step(b)
+    eng.flush()
+    got = _blamed(eng)
+    assert {n for _, n, _ in got} == {1}, got
+    assert len({s for s, _, _ in got}) >= 15, got      # of 21 tampered steps (uniform alone: ~5)
+
+
 def test_local_clean_run_no_blame_with_backward_audit():
     eng = _engine(4, micro=4)
     for b in _batches(10, bs=8):
@@ -155,17 +189,17 @@ def test_no_verified_shadow_restores_initial_weights_not_own():
     assert torch.equal(got, init)
 
 
-def _worker(rank, world, port, out_path, attack, targets, atk_kw, micro):
+def _worker(rank, world, port, out_path, attack, targets, atk_kw, micro, cfg=None, steps=9):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    eng = _engine(world, attack, targets=targets, atk_kw=atk_kw, micro=micro)
-    for b in _batches(9, bs=2 * micro):
+    eng = _engine(world, attack, targets=targets, atk_kw=atk_kw, micro=micro, **(cfg or {}))
+    for b in _batches(steps, bs=2 * micro):
         eng.train_step(b)
     eng.flush()
     with open(f"{out_path}.{rank}", "w") as f:
-        json.dump({"blamed": _blamed(eng)}, f)
+        json.dump({"blamed": _blamed(eng), "targeted": eng.audit_summary().get("targeted_extra", 0)}, f)
     eng.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -191,6 +225,23 @@ def test_distributed_backward_audit(attack, targets, atk_kw, kind):
     assert {n for _, n, _ in got} == set(targets), got
     assert all(k == kind for _, _, k in got), got
     assert {s for s, _, _ in got} == set(range(6, 10)), got
+
+
+def test_distributed_targeted_audit_one_of_m():
+    """Distributed opt-in targeted audit (audit_targeted=True): the auditor scores the M outputs it
+    received, reveals the uniform choice plus the outlier through the store, the auditee ships both
+    micro-batches; a one-of-M output tamper is caught at every tampered step, every rank agrees."""
+    world = 3
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "r")
+        mp.spawn(_worker, args=(world, _free_port(), out, "byzantine", (1,), {"micro_batches": 1}, 4,
+                                {"audit_targeted": True}, 14), nprocs=world, join=True)
+        res = [json.load(open(f"{out}.{r}")) for r in range(world)]
+    assert res[0]["blamed"] == res[1]["blamed"] == res[2]["blamed"]
+    got = res[0]["blamed"]
+    assert {n for _, n, _ in got} == {1}, got
+    assert {s for s, _, _ in got} == set(range(6, 15)), got
+    assert res[2]["targeted"] > 0            # rank 2 audits rank 1
 
 
 def _worker8(rank, world, port, out_path):

@@ -80,6 +80,16 @@ class P2PComm:
         return from_prev, from_next
 
 
+def isend(t: torch.Tensor, dst: int, group=None):
+    """One unbatched send (the async 1F1B schedule's direction communicators).  Called through this
+    module so the RCCL-model recorder (runtime/commcheck.py) sees it."""
+    return dist.isend(t, dst, group=group)
+
+
+def irecv(t: torch.Tensor, src: int, group=None):
+    return dist.irecv(t, src, group=group)
+
+
 def all_gather_rows(vec: torch.Tensor, world: int, group=None) -> torch.Tensor:
     """All-gather a fixed-size 1-D float tensor from every rank -> [world, K] (identical on all ranks)."""
     out = torch.empty(world * vec.numel(), dtype=vec.dtype, device=vec.device)
@@ -95,6 +105,8 @@ def broadcast_ints(values: Optional[Sequence[int]], src: int, device, max_len: i
         buf[0] = len(vals)
         buf[1:1 + len(vals)] = torch.tensor(vals, dtype=torch.int64)
     dist.broadcast(buf, src, group=group)
+    from ..runtime.commcheck import note_host_sync
+    note_host_sync()
     n = int(buf[0])
     return [int(v) for v in buf[1:1 + n].tolist()]
 

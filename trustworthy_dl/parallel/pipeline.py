@@ -37,7 +37,9 @@ from ..security import stage_verifier as SV
 from ..ops import stats as dstats
 from ..ops.layers import bump_weight_generation
 from ..ops.layers import defer_weight_grads
+from ..runtime.commcheck import note_host_sync
 from ..runtime.tracing import PhaseTracer
+from . import comm as p2p
 from .comm import LinkMeter, P2PComm, all_gather_rows, batched_transfer, broadcast_ints
 from .flat import AdamWConfig
 from .partition import PlacementPlan, make_plan
@@ -80,7 +82,7 @@ class EngineConfig:
                                          # this far below the median = outlier (sign flips)
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
-    shadow_interval: int = 100           # steps between trusted weight snapshots held by the next stage's GPU
+    shadow_interval: int = 25            # steps between trusted weight snapshots held by the next stage's GPU
                                          # (0 = off); a compromised stage is restored from it, not from itself.
                                          # A snapshot is also taken when the stages are (re)built
     shadow_copies: int = 2               # holders per snapshot (the next 1-2 stages of the ring): a stage
@@ -100,6 +102,14 @@ class EngineConfig:
                                          # per-micro-batch contributions; gradient z-scores then no longer
                                          # blame (they quarantine the update and feed the trust metrics)
     audit_grad_tol: float = 0.05         # relative sketch error above which a gradient check fails
+    audit_targeted: Optional[bool] = None  # besides the private uniform choice, also audit the micro-batch
+                                         # whose output statistics (log RMS, sign of the token-mean vector)
+                                         # or committed gradient-sketch norm stand out among the step's M
+                                         # (robust z > audit_target_z): a one-of-M tamper that moves them is
+                                         # then recomputed in the step it happens, not with probability 1/M.
+                                         # None = local mode only (distributed: one device->host read of the
+                                         # M scores per auditor and step, opt-in with True)
+    audit_target_z: float = 4.0
     compromise_on_proof: bool = True     # a failed audit / integrity / gradient-consistency check (proof of
                                          # tampering, not a statistic) compromises the node at once
     attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
@@ -187,6 +197,7 @@ class PipelineEngine:
             seed = int.from_bytes(os.urandom(8), "little")
         self._mon_rng = __import__("random").Random(seed)
         self._mon_idx = 0
+        self._targeted = False
 
         if cfg.device == "auto":
             if torch.cuda.is_available():
@@ -327,6 +338,7 @@ class PipelineEngine:
                              "flattened_params": total, "stages": len(built), "groups_s": t3 - t2}
 
     def _sync_all(self):
+        note_host_sync(device=True)
         if self.device.type == "cuda":
             torch.cuda.synchronize()
 
@@ -586,6 +598,8 @@ class PipelineEngine:
         if self._audit_now and not self.distributed and (
                 self._mon_idx < 0 or (self.cfg.audit_prob < 1.0 and self._mon_rng.random() >= self.cfg.audit_prob)):
             self._audit_now = False
+        tg = self.cfg.audit_targeted
+        self._targeted = self._audit_now and M > 1 and (not self.distributed if tg is None else bool(tg))
         self._audit_rec: Dict[int, Dict[str, Any]] = {}
         self._audit_inputs: Dict[int, torch.Tensor] = {}   # distributed: this stage's received inputs
         self._audit_sent_dx: Dict[int, torch.Tensor] = {}  # distributed: input gradients sent upstream
@@ -759,7 +773,8 @@ class PipelineEngine:
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
                 labels = targets[i].to(st.device, non_blocking=True) if st.computes_loss else None
                 obs = st.output_observer() if watch else None
-                rec = self._audit_rec.setdefault(node, {}) if watch and self._audit_now else None
+                rec = self._audit_rec.setdefault(node, {}).setdefault(i, {}) \
+                    if self._audit_now and (watch or self._targeted) else None
                 if rec is not None:
                     rec["x"] = x.detach().clone()
                     if st.computes_loss:
@@ -774,7 +789,7 @@ class PipelineEngine:
                             rec["dx"] = g2.detach().clone()
                         return g2 if g2 is not g else None
                     x.register_hook(_dx_hook)
-                    prec = self._audit_rec.get(order[sidx - 1][0]) if rec is not None and bwd_audit else None
+                    prec = self._audit_rec.get(order[sidx - 1][0], {}).get(i) if rec is not None and bwd_audit else None
                     if prec is not None:
                         def _dy_hook(g, prec=prec):
                             prec["dy"] = g.detach().clone()
@@ -785,8 +800,10 @@ class PipelineEngine:
                     y = self._attack_output(node, y, truth, i, M)
                     if watch:
                         mon = y
-                        if rec is not None:
-                            rec["y"] = y.detach().clone()
+                    if rec is not None:
+                        rec["y"] = y.detach().clone()
+                        if self._targeted:
+                            rec["ystat"] = self._output_stat(rec["y"])
                 if watch and mon is not None:
                     st.verifier.observe_output(mon)
                     if st.computes_loss and st.verifier.side is not None:
@@ -974,7 +991,7 @@ class PipelineEngine:
 
         def post_recv(shape, src, group):
             buf = torch.empty(shape, dtype=dt, device=st.device)
-            return dist.irecv(buf, src, group=group), buf, src
+            return p2p.irecv(buf, src, group=group), buf, src
 
         def take(h):
             progress.mark(f"step {step}: stage {s} waits for a P2P receive from rank {h[2]}")
@@ -991,7 +1008,7 @@ class PipelineEngine:
             return None if last or i >= M else post_recv(out_shape, nxt, grad_pg)
 
         def send(t, dst, group):
-            sends.append(dist.isend(t.contiguous(), dst, group=group))
+            sends.append(p2p.isend(t.contiguous(), dst, group=group))
             if len(sends) > 8:  # drop finished sends (their tensors are released)
                 sends[:] = [w for w in sends if not w.is_completed()]
 
@@ -1104,6 +1121,7 @@ class PipelineEngine:
         in_shape = None
         if s > 0:
             h, _ = self.comm.exchange(recv_prev=((8,), torch.int64))
+            note_host_sync()
             in_shape = torch.Size([int(v) for v in h[1:1 + int(h[0])].tolist()])
             probe = torch.zeros(in_shape, dtype=self.dtype, device=st.device)
         else:
@@ -1326,7 +1344,7 @@ class PipelineEngine:
             ev.record()
         else:
             host, ev = rep.clone(), None
-        self._pending.append((self.global_step, self.epoch, host, ev, dict(truth)))
+        self._pending.append((self.global_step, self.epoch, host, ev, dict(truth), list(self.last_ranks())))
 
     def _write_commitments(self, node: int, st: Stage, d: torch.Tensor):
         """Digest slots of the gradient commitments: the sketch of the gradient about to be applied
@@ -1384,6 +1402,66 @@ class PipelineEngine:
             with torch.no_grad():
                 for b, v in zip(st.module.buffers(), bufs):
                     b.copy_(v)
+
+    @staticmethod
+    @torch.no_grad()
+    def _output_stat(y: torch.Tensor):
+        """(log RMS, token-mean vector over the last dim) of one micro-batch's stage output, device."""
+        yf = y.float()
+        return (yf.square().mean().clamp_min(1e-30).log().reshape(1),
+                yf.reshape(-1, yf.shape[-1]).mean(0) if yf.dim() > 1 else yf.reshape(1, -1).mean(0))
+
+    @torch.no_grad()
+    def _target_scores(self, ystats, run) -> Optional[torch.Tensor]:
+        """Robust |z| per micro-batch (max over the statistics) of: the output's log RMS, the cosine of
+        its token-mean vector with the other micro-batches' (a sign flip or a large perturbation
+        drives it toward -1 / 0) and the norm of its committed weight-gradient sketch contribution."""
+        terms = []
+        if ystats:
+            lr = torch.cat([a for a, _ in ystats])
+            V = torch.stack([v for _, v in ystats])
+            ref = V.sum(0, keepdim=True) - V                      # the other micro-batches' sum
+            cos = torch.nn.functional.cosine_similarity(V, ref, dim=1)
+            terms += [(lr, 0.05), (cos, 0.05)]
+        if run is not None and run.shape[0] > 2:
+            dn = (run[1:] - run[:-1]).norm(dim=1).clamp_min(1e-30).log()
+            terms.append((dn, 0.1))
+        if not terms:
+            return None
+        zs = []
+        for t, floor in terms:
+            med = t.median()
+            mad = (t - med).abs().median()
+            zs.append((t - med).abs() / torch.clamp(1.4826 * mad, min=floor))
+        return torch.stack(zs).amax(0)
+
+    def _target_picks(self, order) -> Dict[int, int]:
+        """Local mode: per audited stage, the micro-batch with the largest anomaly score if it
+        exceeds ``audit_target_z`` (one device->host read for all stages)."""
+        M = len(self._audit_batch)
+        nodes, best = [], []
+        for k, p in enumerate(order):
+            recs = self._audit_rec.get(p, {})
+            last = k == len(order) - 1
+            ystats = None
+            if not last:
+                ystats = [recs.get(m, {}).get("ystat") for m in range(M)]
+                if any(v is None for v in ystats):
+                    ystats = None
+            run = self._gsk_run.get(p) if getattr(self, "_gsk_on", False) else None
+            z = self._target_scores(ystats, run)
+            if z is None:
+                continue
+            nodes.append(p)
+            best.append(torch.stack([z.max(), z.argmax().float()]).to(self.device))
+        if not best:
+            return {}
+        vals = torch.stack(best).tolist()
+        thr = self.cfg.audit_target_z
+        picks = {p: int(i) for p, (zm, i) in zip(nodes, vals) if zm > thr}
+        tl = self.__dict__.setdefault("_target_log", [])
+        tl.extend((self.global_step, p, m) for p, m in picks.items())
+        return picks
 
     def _audit_verdict(self, y_seen: torch.Tensor, y_ref: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(mismatch flag, relative max error) of a received output against its recomputation —
@@ -1446,25 +1524,33 @@ class PipelineEngine:
         order = list(self.plan.ranks)
         S = len(order)
         M = len(self._audit_batch)
-        m = self._mon_idx
+        picks = self._target_picks(order) if self._targeted else {}
         for k in range(S):
             p = order[k]
             last = k == S - 1
             if last and not self.cfg.audit_backward:
                 continue
             aud = order[k + 1] if not last else order[k - 1]
-            rec = self._audit_rec.get(p)
-            if not rec or "x" not in rec or aud not in rows:
+            recs = self._audit_rec.get(p, {})
+            chosen = [m for m in dict.fromkeys([self._mon_idx, picks.get(p, -1)]) if m >= 0 and "x" in recs.get(m, {})]
+            if not chosen or aud not in rows:
                 continue
             st = self.stages[p]
-            dy = None if last else rec.get("dy")
             wh = None
             cur, ref = getattr(st, "_cur_checksum", None), getattr(st, "param_checksum", None)
             if cur is not None and ref is not None and cur is not ref:
                 wh = (fold_hash(cur) != fold_hash(ref)).any().float().reshape(1)
-            flag, kind, err = self._audit_one(st, rec["x"], m, M, y_seen=rec.get("y"), dy=dy,
-                                              labels=rec.get("labels"), dx_seen=rec.get("dx"),
-                                              run=self._gsk_run.get(p), whash=wh)
+            flag = kind = err = None
+            for m in chosen:
+                rec = recs[m]
+                f1, k1, e1 = self._audit_one(st, rec["x"], m, M, y_seen=rec.get("y"),
+                                             dy=None if last else rec.get("dy"), labels=rec.get("labels"),
+                                             dx_seen=rec.get("dx"), run=self._gsk_run.get(p), whash=wh)
+                if flag is None:
+                    flag, kind, err = f1, k1, e1
+                else:   # failed-check bits of both audited micro-batches
+                    flag, err = torch.maximum(flag, f1), torch.maximum(err, e1)
+                    kind = torch.bitwise_or(kind.long(), k1.long()).float()
             d = rows[aud]
             base = (SV.D_AUDIT_NEXT, SV.D_AUDITED_NEXT, SV.D_AUDIT_KIND_NEXT) if last else \
                 (SV.D_AUDIT_PREV, SV.D_AUDITED_PREV, SV.D_AUDIT_KIND_PREV)
@@ -1523,90 +1609,135 @@ class PipelineEngine:
                     c_recv.append((runs_in[peer], peer))
             self._audit_transfer(c_send, c_recv, prev, nxt, act_g, grad_g)
 
-        # ---- 2. reveal: private choices (whether + which micro-batch)
-        def choose():
+        # ---- 2. reveal: private choices (whether + which micro-batches).  The uniform draw, plus
+        # with ``audit_targeted`` the micro-batch whose received output / committed sketch norm stands
+        # out (one host read of the scores: the choice needs them)
+        tgt_prev = tgt_next = -1
+        if self._targeted:
+            zs = []
+            if audit_prev:
+                ys = [self._output_stat(self._audit_inputs[m]) for m in range(M)] if s - 1 >= 0 else None
+                zs.append(self._target_scores(ys, runs_in.get(prev)))
+            if audit_next:
+                zs.append(self._target_scores(None, runs_in.get(nxt)))
+            got = [torch.stack([z.max(), z.argmax().float()]) if z is not None else
+                   torch.tensor([-1.0, -1.0], device=self.device) for z in zs]
+            note_host_sync()
+            vals = torch.stack(got).tolist() if got else []
+            thr = self.cfg.audit_target_z
+            picks = [int(i) if zm > thr else -1 for zm, i in vals]
+            if audit_prev:
+                tgt_prev = picks.pop(0)
+            if audit_next:
+                tgt_next = picks.pop(0)
+            tl = self.__dict__.setdefault("_target_log", [])
+            tl.extend((self.global_step, n, m) for n, m in ((prev, tgt_prev), (nxt, tgt_next)) if m >= 0)
+
+        def choose(extra):
             if self.cfg.audit_prob < 1.0 and self._audit_rng.random() >= self.cfg.audit_prob:
-                return -1
-            return self._audit_rng.randrange(M)
-        m_prev = choose() if audit_prev else -1
-        m_next = choose() if audit_next else -1
+                return [extra] if extra >= 0 else []
+            return list(dict.fromkeys([self._audit_rng.randrange(M)] + ([extra] if extra >= 0 else [])))
+        ms_prev = choose(tgt_prev) if audit_prev else []
+        ms_next = choose(tgt_next) if audit_next else []
+
+        def enc(ms):
+            return ",".join(str(m) for m in ms) if ms else "-1"
+
+        def dec(v):
+            return [int(t) for t in v.decode().split(",") if int(t) >= 0]
         if audit_prev:
-            store.set(f"{tag}/req/{prev}", str(m_prev))
+            store.set(f"{tag}/req/{prev}", enc(ms_prev))
             if s - 1 > 0 and bwd:
-                store.set(f"{tag}/reqh/{prev}", str(m_prev))   # for the stage before prev: dx hash
+                store.set(f"{tag}/reqh/{prev}", enc(ms_prev))   # for the stage before prev: dx hash
         if audit_next:
-            store.set(f"{tag}/req/{nxt}", str(m_next))
-        m_req = -1
+            store.set(f"{tag}/req/{nxt}", enc(ms_next))
+        ms_req: List[int] = []
         if my_auditor is not None:
             k = f"{tag}/req/{self.rank}"
-            m_req = int(store.get(k))
+            ms_req = dec(store.get(k))
             store.delete_key(k)
-        # as the upstream recipient of nxt's input gradient: hash what I received for nxt's audited micro-batch
+
+        def hsum(ts):
+            """Combined hash of several tensors (sum of the 16-bit halves mod 2^16, exact in fp32)."""
+            h = hash2(ts[0])
+            for t in ts[1:]:
+                h = torch.remainder(h + hash2(t), 65536.0)
+            return h
+        # as the upstream recipient of nxt's input gradient: hash what I received for nxt's audited micro-batches
         if bwd and nxt is not None and s + 1 < S - 1:
             k = f"{tag}/reqh/{nxt}"
-            mh = int(store.get(k))
+            mh = dec(store.get(k))
             store.delete_key(k)
-            if mh >= 0 and mh in self._audit_recv_dy:
-                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].copy_(hash2(self._audit_recv_dy[mh]))
+            if mh and all(m in self._audit_recv_dy for m in mh):
+                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].copy_(hsum([self._audit_recv_dy[m] for m in mh]))
             else:
                 d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
         else:
             d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
-        x_send = dx_send = None
-        if m_req >= 0 and s > 0 and s < S - 1:
-            x_send = self._audit_inputs[m_req].contiguous()
-            if bwd and m_req in self._audit_sent_dx:
-                dx_send = self._audit_sent_dx[m_req].contiguous()
-            store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send.shape))
+        x_send, dx_send = [], []
+        if ms_req and s > 0 and s < S - 1:
+            x_send = [self._audit_inputs[m].contiguous() for m in ms_req]
+            if bwd and all(m in self._audit_sent_dx for m in ms_req):
+                dx_send = [self._audit_sent_dx[m].contiguous() for m in ms_req]
+            store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send[0].shape))
         # ---- 3. ship
         sends, recvs = [], []
-        if m_req >= 0:
+        if ms_req:
             sends.append((st.flat.data, my_auditor))
-            if x_send is not None:
-                sends.append((x_send, my_auditor))
-            if dx_send is not None:
-                sends.append((dx_send, my_auditor))
-        mir_p = mir_n = x_prev = dx_prev = None
-        if audit_prev and m_prev >= 0:
+            sends += [(t, my_auditor) for t in x_send]
+            sends += [(t, my_auditor) for t in dx_send]
+        mir_p = mir_n = None
+        x_prev, dx_prev = [], []
+        if audit_prev and ms_prev:
             mir_p = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
             recvs.append((mir_p.flat.data, prev))
             if s - 1 > 0:
                 k = f"{tag}/shape/{prev}"
                 shape = torch.Size([int(v) for v in store.get(k).decode().split(",")])
                 store.delete_key(k)
-                x_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
-                recvs.append((x_prev, prev))
+                x_prev = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms_prev]
+                recvs += [(t, prev) for t in x_prev]
                 if bwd:
-                    dx_prev = torch.empty(shape, dtype=self.dtype, device=self.device)
-                    recvs.append((dx_prev, prev))
-        if audit_next and m_next >= 0:
+                    dx_prev = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms_prev]
+                    recvs += [(t, prev) for t in dx_prev]
+        if audit_next and ms_next:
             mir_n = self._audit_mirror(tuple(self.plan.ranges[s + 1]), s + 1)
             recvs.append((mir_n.flat.data, nxt))
         self._audit_transfer(sends, recvs, prev, nxt, act_g, grad_g)
+
+        def combine(acc, res):
+            if acc is None:
+                return res
+            (f0, k0, e0), (f1, k1, e1) = acc, res
+            return (torch.maximum(f0, f1), torch.bitwise_or(k0.long(), k1.long()).float(), torch.maximum(e0, e1))
         # ---- 4. verify
         if mir_p is not None:
-            if x_prev is None:
-                x_prev = self._stage_input(self._audit_batch[m_prev], mir_p)
-            dy = self._audit_sent_dx.get(m_prev) if bwd else None
-            flag, kind, err = self._audit_one(mir_p, x_prev, m_prev, M, y_seen=self._audit_inputs[m_prev], dy=dy,
-                                              dx_seen=dx_prev, run=runs_in.get(prev))
+            res = None
+            for j, m in enumerate(ms_prev):
+                xp = x_prev[j] if x_prev else self._stage_input(self._audit_batch[m], mir_p)
+                dy = self._audit_sent_dx.get(m) if bwd else None
+                res = combine(res, self._audit_one(mir_p, xp, m, M, y_seen=self._audit_inputs[m], dy=dy,
+                                                   dx_seen=dx_prev[j] if dx_prev else None, run=runs_in.get(prev)))
+            flag, kind, err = res
             d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag)
             d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
             d[SV.D_AUDIT_KIND_PREV:SV.D_AUDIT_KIND_PREV + 1].copy_(kind)
             d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err)
             d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].copy_(hash2(mir_p.flat.data))
-            if dx_prev is not None:
-                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].copy_(hash2(dx_prev))
+            if dx_prev:
+                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].copy_(hsum(dx_prev))
             else:
                 d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
         else:
             d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].fill_(-1.0)
             d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
         if mir_n is not None:
-            x_n = self._audit_outputs.get(m_next)
-            labels = self._audit_targets[m_next].to(self.device, non_blocking=True)
-            flag, kind, err = self._audit_one(mir_n, x_n, m_next, M, labels=labels,
-                                              dx_seen=self._audit_recv_dy.get(m_next), run=runs_in.get(nxt))
+            res = None
+            for m in ms_next:
+                labels = self._audit_targets[m].to(self.device, non_blocking=True)
+                res = combine(res, self._audit_one(mir_n, self._audit_outputs.get(m), m, M, labels=labels,
+                                                   dx_seen=self._audit_recv_dy.get(m), run=runs_in.get(nxt)))
+            flag, kind, err = res
             d[SV.D_AUDIT_NEXT:SV.D_AUDIT_NEXT + 1].copy_(flag)
             d[SV.D_AUDITED_NEXT:SV.D_AUDITED_NEXT + 1].fill_(1.0)
             d[SV.D_AUDIT_KIND_NEXT:SV.D_AUDIT_KIND_NEXT + 1].copy_(kind)
@@ -1633,12 +1764,14 @@ class PipelineEngine:
         it sent + received (commitments, weights, inputs, gradients), host wall time of the audit
         phase, and device time between its first and last kernel (HIP events)."""
         a = getattr(self, "_audit_cost", None)
+        tl = getattr(self, "_target_log", [])
         if not a or not a["steps"]:
-            return {"steps": 0}
+            return {"steps": 0, "targeted_extra": len(tl)}
         gpu = [e0.elapsed_time(e1) for e0, e1 in a["events"] if e1.query()]
         return {"steps": a["steps"], "bytes_per_step": a["bytes"] / a["steps"],
                 "host_ms_per_step": 1e3 * a["host_s"] / a["steps"],
-                "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None}
+                "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None,
+                "targeted_extra": len(tl)}
 
     def _audit_transfer(self, sends, recvs, prev, nxt, act_g, grad_g):
         """Audit traffic: toward the next stage on the activation communicator, toward the
@@ -1958,7 +2091,9 @@ class PipelineEngine:
             dg = torch.stack([m.sum(), (m * m).sum()])
         else:
             dg = torch.zeros(2, dtype=torch.float64, device=self.device)
-        G = all_gather_rows(dg, self.world).cpu()
+        G = all_gather_rows(dg, self.world)
+        note_host_sync()
+        G = G.cpu()
         my_pos = self.rank % self.pp
         for pos in range(self.pp):
             ranks = [d * self.pp + pos for d in range(self.dp)]
@@ -1995,12 +2130,14 @@ class PipelineEngine:
 
     def _consume_reports(self, upto: Optional[int]):
         while self._pending and (upto is None or self._pending[0][0] <= upto):
-            step, epoch, host, ev, truth = self._pending.popleft()
+            step, epoch, host, ev, truth, lasts = self._pending.popleft()
+            note_host_sync()
             if ev is not None:
                 ev.synchronize()
-            self._process_report(step, epoch, host, truth)
+            self._process_report(step, epoch, host, truth, lasts)
 
-    def _process_report(self, step: int, epoch: int, host: torch.Tensor, truth: Dict[int, bool]):
+    def _process_report(self, step: int, epoch: int, host: torch.Tensor, truth: Dict[int, bool],
+                        loss_ranks: Optional[List[int]] = None):
         N = self.num_nodes
         D = host[: N * SV.DIGEST].view(N, SV.DIGEST).tolist()
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
@@ -2009,7 +2146,9 @@ class PipelineEngine:
         audit_kind = [int(v) for v in host[N * SV.DIGEST + 3 * N:N * SV.DIGEST + 4 * N].tolist()]
         audit_bad = [k > 0 for k in audit_kind]
         present = set(self.all_ranks())
-        lasts = [n for n in self.last_ranks() if D[n][SV.D_PRESENT] > 0]
+        # the loss stages of the plan the step ran under (a re-shard decided by an earlier report
+        # may have moved the loss stage since)
+        lasts = [n for n in (loss_ranks if loss_ranks is not None else self.last_ranks()) if D[n][SV.D_PRESENT] > 0]
         self.last_loss = sum(D[n][SV.D_LOSS] for n in lasts) / len(lasts) if lasts else None
         detections = []
         for n in range(N):
@@ -2027,7 +2166,7 @@ class PipelineEngine:
                                         "z": row[SV.D_OUT_Z]},
                        "gradient_stats": {"norm_l2": row[SV.D_GRAD_L2], "z": row[SV.D_GRAD_Z],
                                           "cosine": row[SV.D_GRAD_COS]},
-                       "ground_truth": gt}
+                       "audit_kind": audit_kind[n], "ground_truth": gt}
                 self.attack_history.append(rec)
                 self.trust.attack_history[n].append({"timestamp": rec["timestamp"], "step": step,
                                                      "attack_type": kind,
@@ -2302,6 +2441,7 @@ class PipelineEngine:
             batched_transfer(sends, recvs, meter=self.link_meter)
             step_t = torch.tensor([float(step_count)], device=self.device)
             dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
+            note_host_sync()
             step_count = int(step_t.item())
         else:
             # every stage is local: the packed vectors stay on the device (no host round trip)
@@ -2429,7 +2569,9 @@ class PipelineEngine:
                 mine[c] = 1.0 if ok else 0.0
         out: Dict[Tuple[int, int], bool] = {}
         if self.distributed:
-            V = all_gather_rows(mine, self.world).cpu()
+            V = all_gather_rows(mine, self.world)
+            note_host_sync()
+            V = V.cpu()
             for c, meta in self._shadow_meta.items():
                 for h in meta[3]:
                     out[(c, h)] = bool(V[h, c] > 0)
