@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(ROOT, "csrc")
 OUT_DIR = os.path.join(ROOT, "trustworthy_dl", "_native")
 BUILD_DIR = os.path.join(ROOT, "build", "native")
+NO_NAN_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
 AGPR_FORM = {"gemm.hip"}
 
 
@@ -66,6 +67,9 @@ def build(arch: str = "gfx950", jobs: int = 8, debug: bool = False, verbose: boo
             # the persistent GEMM keeps its 256 accumulators per lane in AGPRs (one wave per SIMD,
             # 512 registers): it is built in the default AGPR form
             form = [] if os.path.basename(src) in AGPR_FORM else ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+            # attention softmax: scores are finite or -inf, never NaN; without NaN semantics fmax
+            # of an MFMA result needs no canonicalising v_max in front of it (csrc/attention.hip)
+            form += NO_NAN_FLAGS.get(os.path.basename(src), [])
             jobs_list.append([cc, f"--offload-arch={arch}", "-std=c++17", "-fPIC", *opt, "-munsafe-fp-atomics",
                               *form, "-I", CSRC, "-c", src, "-o", obj])
     for src in rt_srcs:
