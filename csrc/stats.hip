@@ -900,6 +900,185 @@ TDL_API int tdl_trust_update(float* values, int* counts, int* status, const floa
     TDL_LAUNCH_CHECK();
 }
 
+// ------------------------------------------------------------------ K6 stage-verifier step tail
+// security/stage_verifier.py StageVerifier.finish_step, fused: everything the verifier does after
+// the statistics and detector kernels — digest row, output-deviation and gradient-consistency trust
+// metrics, the two EMA baselines, the sign-flip rule, quarantine control and the clipping sum of
+// squares — in ONE launch.  The torch form (kept for CPU and as TDL_VERIFY_FUSED=0) issued ~110
+// element-sized kernels per stage and step, ~0.55 ms of the GPT-2-small step's 1.2 ms verification
+// overhead (bench --trace-phases: verify 1.06 vs 0.42 ms).  Host values (stage id, the four runtime
+// metrics, the ground-truth bit) travel as kernel arguments, so no host-to-device copy either.
+// Digest slots: security/stage_verifier.py (D_*).
+struct VerifyFinishArgs {
+    float* d;
+    const float* loss;          // [1] or null
+    int stage_id;
+    int out_on;                 // output statistics observed this step (and output detection on)
+    const float* out_res;       // output detector [flag, z, conf, ...]
+    const float* out_stats;     // [13]: 0 mean, 1 std, 12 non-finite count
+    float* out_mu;
+    float* out_sd;
+    float* out_n;
+    float warmup, deadzone, beta;
+    int grad_mode;              // 0: no gradient statistics, 1: bare (sum of squares only), 2: full
+    const float* sumsq_bare;    // mode 1: [1]
+    const float* g;             // mode 2: grad statistics [18 + 2 S]
+    int S;
+    const float* clip_w;        // [S]
+    int gdet;                   // gradient detector ran this step
+    const float* grad_res;      // its [flag, z, conf, ...]
+    int targeted;               // sign-flip rule on (targeted feature set)
+    float sign_flip_cos;
+    float* norm_ema;            // [S]
+    float* norm_n;
+    float tol;
+    int symmetric;
+    float hm0, hm1, hm2, hm3;   // latency, utilization, error, uptime (host, one step lagged)
+    int truth;
+    int quarantine;
+    float* ctrl;                // [2]: clip scale (not touched here), skip
+};
+
+enum {
+    VD_LOSS = 0, VD_OUT_FLAG = 1, VD_OUT_Z = 2, VD_GRAD_FLAG = 3, VD_GRAD_Z = 4, VD_METRICS = 5, VD_GRAD_SUMSQ = 11,
+    VD_OUT_MEAN = 12, VD_OUT_STD = 13, VD_GRAD_L2 = 14, VD_NONFINITE = 15, VD_GRAD_COS = 16, VD_ATTACK_TRUTH = 17,
+    VD_PRESENT = 18, VD_STAGE = 19, VD_OUT_CONF = 20, VD_GRAD_CONF = 21, VD_DIGEST = 51
+};
+
+__global__ __launch_bounds__(256) void verify_finish_kernel(VerifyFinishArgs a) {
+    __shared__ float red[16];
+    __shared__ float sh_keep_g, sh_b_g;
+    const int t = threadIdx.x;
+    float* d = a.d;
+    for (int i = t; i < VD_DIGEST; i += 256) d[i] = 0.f;
+    // gradient flag (needed by every thread for the EMA update): detector flag, sign-flip rule
+    float gflag = 0.f;
+    const bool full = a.grad_mode == 2;
+    if (full && a.gdet) {
+        gflag = a.grad_res[0];
+        if (a.targeted) {
+            const float warm = a.norm_n[0] >= a.warmup ? 1.f : 0.f;
+            gflag = fmaxf(gflag, (a.g[16] < a.sign_flip_cos ? 1.f : 0.f) * warm);
+        }
+    }
+    // per-parameter reductions over the pre-update EMA: clipping sum of squares, consistency
+    float sq = 0.f, cs = 0.f, nv = 0.f;
+    if (full) {
+        for (int i = t; i < a.S; i += 256) {
+            const float nrm = a.g[18 + i];
+            const float ema = a.norm_ema[i];
+            sq += nrm * nrm * a.clip_w[i];
+            const float r = nrm / fmaxf(ema, 1e-30f);
+            float sc = a.symmetric ? fminf(r, 1.f / fmaxf(r, 1e-30f)) : fminf(r, 1.f);
+            sc = fminf(sc * a.tol, 1.f);
+            const float valid = ema > 0.f ? 1.f : 0.f;
+            cs += sc * valid;
+            nv += valid;
+        }
+        sq = block_sum(sq, red);
+        cs = block_sum(cs, red);
+        nv = block_sum(nv, red);
+    }
+    __syncthreads();   // digest zeroed by every thread before thread 0 writes it
+    if (t == 0) {
+        d[VD_PRESENT] = 1.f;
+        d[VD_STAGE] = (float)a.stage_id;
+        if (a.loss) d[VD_LOSS] = a.loss[0];
+        float nonfin = 0.f;
+        if (a.out_on) {
+            const float flag = a.out_res[0];
+            d[VD_OUT_FLAG] = flag;
+            d[VD_OUT_Z] = a.out_res[1];
+            d[VD_OUT_CONF] = a.out_res[2];
+            const float mu = a.out_stats[0], sd = a.out_stats[1];
+            d[VD_OUT_MEAN] = mu;
+            d[VD_OUT_STD] = sd;
+            const float omu = a.out_mu[0], osd = a.out_sd[0], on = a.out_n[0];
+            const float ready = on >= a.warmup ? 1.f : 0.f;
+            float dev = fminf((fabsf(mu - omu) + fabsf(sd - osd)) / (2.f * fmaxf(osd, 1e-12f)), 1.f);
+            dev = fmaxf(dev - a.deadzone, 0.f) / (1.f - a.deadzone);
+            d[VD_METRICS + 0] = dev * ready;
+            const float keep = 1.f - flag;
+            const float first = on == 0.f ? 1.f : 0.f;
+            const float b = a.beta * (1.f - first);
+            a.out_mu[0] = keep * (b * omu + (1.f - b) * mu) + (1.f - keep) * omu;
+            a.out_sd[0] = keep * (b * osd + (1.f - b) * sd) + (1.f - keep) * osd;
+            a.out_n[0] = on + keep;
+            nonfin += a.out_stats[12];
+        }
+        if (a.grad_mode == 1) {
+            d[VD_GRAD_SUMSQ] = a.sumsq_bare[0];
+            d[VD_METRICS + 1] = 1.f;
+        } else if (full) {
+            d[VD_GRAD_L2] = a.g[10];
+            d[VD_GRAD_COS] = a.g[16];
+            nonfin += a.g[17];
+            if (a.gdet) {
+                d[VD_GRAD_FLAG] = gflag;
+                d[VD_GRAD_Z] = a.grad_res[1];
+                d[VD_GRAD_CONF] = a.grad_res[2];
+            }
+            const float ready = a.norm_n[0] >= a.warmup ? 1.f : 0.f;
+            const float cons = cs / fmaxf(nv, 1.f);
+            d[VD_METRICS + 1] = ready * cons + (1.f - ready) * 1.f;
+        } else {
+            d[VD_METRICS + 1] = 1.f;
+        }
+        d[VD_NONFINITE] = nonfin;
+        d[VD_METRICS + 2] = a.hm0;
+        d[VD_METRICS + 3] = a.hm1;
+        d[VD_METRICS + 4] = fminf(a.hm2 + (nonfin > 0.f ? 1.f : 0.f), 1.f);
+        d[VD_METRICS + 5] = a.hm3;
+        d[VD_ATTACK_TRUTH] = a.truth ? 1.f : 0.f;
+        float skip = 0.f;
+        if (a.quarantine && full && a.gdet) skip = fmaxf(gflag, nonfin > 0.f ? 1.f : 0.f);
+        a.ctrl[1] = skip;
+        if (full) d[VD_GRAD_SUMSQ] = sq * (1.f - skip);
+        const float keep = 1.f - gflag;
+        const float first = full ? (a.norm_n[0] == 0.f ? 1.f : 0.f) : 0.f;
+        sh_keep_g = keep;
+        sh_b_g = a.beta * (1.f - first);
+    }
+    __syncthreads();
+    if (full) {
+        const float keep = sh_keep_g, b = sh_b_g;
+        for (int i = t; i < a.S; i += 256) {
+            const float ema = a.norm_ema[i], nrm = a.g[18 + i];
+            a.norm_ema[i] = keep * (b * ema + (1.f - b) * nrm) + (1.f - keep) * ema;
+        }
+        if (t == 0) a.norm_n[0] += keep;
+    }
+}
+
+// targeted detector features (security/stage_verifier.py _out_features / _grad_features):
+// out: [mean, log std, log |max|], grad: [log ||g||, log max per-parameter norm, log element std]
+__global__ void verify_features_kernel(const float* __restrict__ o, const float* __restrict__ g, float* __restrict__ of,
+                                       float* __restrict__ gf) {
+    if (threadIdx.x != 0) return;
+    if (o) {
+        of[0] = o[0];
+        of[1] = logf(fmaxf(o[1], 1e-30f));
+        of[2] = logf(fmaxf(o[11], 1e-30f));
+    }
+    if (g) {
+        gf[0] = logf(fmaxf(g[10], 1e-30f));
+        gf[1] = logf(fmaxf(g[15], 1e-30f));
+        gf[2] = logf(fmaxf(g[1], 1e-30f));
+    }
+}
+
+TDL_API int tdl_verify_features(const float* o, const float* g, float* of, float* gf, hipStream_t s) {
+    verify_features_kernel<<<1, 64, 0, s>>>(o, g, of, gf);
+    TDL_LAUNCH_CHECK();
+}
+
+TDL_API int64_t tdl_verify_args_bytes() { return (int64_t)sizeof(VerifyFinishArgs); }
+
+TDL_API int tdl_verify_finish(const VerifyFinishArgs* args, hipStream_t s) {
+    verify_finish_kernel<<<1, 256, 0, s>>>(*args);
+    TDL_LAUNCH_CHECK();
+}
+
 // ------------------------------------------------------------------ K7 KL(softmax(b) || softmax(a)), batchmean
 // a, b: f32 [R, C]; out f32 [1] (accumulated with atomics; caller zeroes).  One block per row.
 __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ a, const float* __restrict__ b, int R, int C,

@@ -43,7 +43,7 @@ def wrap(owner, name):
     setattr(owner, name, w)
 
 
-for n in ("to", "copy_", "zero_", "fill_", "add_", "float", "contiguous", "clone"):
+for n in ("to", "copy_", "zero_", "fill_", "add_", "float", "contiguous", "clone", "__setitem__"):
     wrap(torch.Tensor, n)
 for n in ("zeros", "zeros_like", "cat"):
     wrap(torch, n)

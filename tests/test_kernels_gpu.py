@@ -687,3 +687,52 @@ def test_cosine_gram_native_matches_torch(n, dtype):
     ref = (X @ X.t()) / (X.norm(dim=1)[:, None] * X.norm(dim=1)[None, :])
     assert torch.allclose(g.double().cpu(), ref, atol=1e-5), (g, ref)
     assert torch.equal(cosine_gram(xs), g)   # deterministic
+
+
+@pytest.mark.parametrize("features", ["targeted", "reference"])
+def test_verifier_fused_tail_matches_torch_form(features, monkeypatch):
+    """csrc/stats.hip verify_finish_kernel (one launch for the verifier's step tail) against the
+    torch form it replaces, over 30 steps with clean, scaled, sign-flipped and non-finite
+    gradients and anomalous outputs: same digests (flags exactly), same EMA baselines and
+    quarantine control."""
+    from trustworthy_dl.security import stage_verifier as sv
+    sizes = [300, 1000, 64, 4096, 17]
+    mk = lambda: sv.StageVerifier(sizes, "cuda", warmup=5, features=features, serialize_streams=True)  # noqa: E731
+    A, B = mk(), mk()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    base = torch.randn(sum(sizes), device="cuda", generator=g)
+    for step in range(30):
+        flat = base + 0.3 * torch.randn(sum(sizes), device="cuda", generator=g)
+        if step in (12, 13):
+            flat = -flat                      # sign flip
+        if step == 17:
+            flat = flat * 50.0                # scaled
+        if step == 21:
+            flat[5] = float("nan")            # non-finite
+        y = torch.randn(4, 64, device="cuda", generator=g).bfloat16()
+        if step in (15, 25):
+            y = y * 20.0
+        loss = torch.tensor(3.0 - 0.01 * step, device="cuda")
+        hm = [0.1 * step, 0.5, 0.0, 1.0]
+        outs = []
+        for v, fused in ((A, True), (B, False)):
+            monkeypatch.setattr(sv, "VERIFY_FUSED", fused)
+            v.observe_output(y)
+            outs.append(v.finish_step(flat, loss, hm, step in (12, 13, 17), 2).clone())
+        da, db = outs
+        for k in (sv.D_OUT_FLAG, sv.D_GRAD_FLAG, sv.D_PRESENT, sv.D_STAGE, sv.D_ATTACK_TRUTH):
+            assert float(da[k]) == float(db[k]), (step, k, da.tolist(), db.tolist())
+        fin = torch.isfinite(db)
+        assert torch.equal(torch.isfinite(da), fin), step
+        # z-scores / confidences: the features' logs round differently (logf in the kernel vs
+        # torch.log), and a MAD-scaled z magnifies that; every other slot to fp32 rounding
+        zs = [sv.D_OUT_Z, sv.D_GRAD_Z, sv.D_OUT_CONF, sv.D_GRAD_CONF]
+        tight = fin.clone()
+        tight[zs] = False
+        assert torch.allclose(da[tight], db[tight], rtol=1e-4, atol=1e-5), (step, (da - db).abs().max())
+        assert torch.allclose(da[zs], db[zs], rtol=2e-2, atol=1e-3), (step, da[zs].tolist(), db[zs].tolist())
+        for x, y_ in ((A.out_mu, B.out_mu), (A.out_sd, B.out_sd), (A.out_n, B.out_n), (A.norm_n, B.norm_n),
+                      (A.ctrl, B.ctrl)):
+            assert torch.allclose(x, y_, rtol=1e-5, atol=1e-6), step
+        fe = torch.isfinite(B.norm_ema)
+        assert torch.allclose(A.norm_ema[fe], B.norm_ema[fe], rtol=1e-5, atol=1e-6), step

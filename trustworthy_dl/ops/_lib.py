@@ -118,6 +118,9 @@ _SIGNATURES = {
     "tdl_kl_div_softmax": [_P, _P, _I, _I, _P, _P],
     "tdl_stats_workspace_bytes": [],
     "tdl_checksum_bf16": [_P, _L, _P, _P, _P],
+    "tdl_verify_features": [_P, _P, _P, _P, _P],
+    "tdl_verify_finish": [_P, _P],
+    "tdl_verify_args_bytes": [],
     # attack.hip
     "tdl_attack_inject": [_P, _I, _L, _I, _F, ctypes.c_uint64, ctypes.c_uint64, _P],
     # attention.hip

@@ -17,11 +17,31 @@ step later through a pinned, non-blocking copy.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Optional, Sequence
 
 import torch
 
 from ..ops import stats as S
+
+# TDL_VERIFY_FUSED=0: the torch form of the step tail on the GPU too (A/B and cross-check)
+VERIFY_FUSED = os.environ.get("TDL_VERIFY_FUSED", "1") != "0"
+
+
+class _FinishArgs(ctypes.Structure):
+    """csrc/stats.hip VerifyFinishArgs (field order and types must match)."""
+    _fields_ = [("d", ctypes.c_void_p), ("loss", ctypes.c_void_p), ("stage_id", ctypes.c_int),
+                ("out_on", ctypes.c_int), ("out_res", ctypes.c_void_p), ("out_stats", ctypes.c_void_p),
+                ("out_mu", ctypes.c_void_p), ("out_sd", ctypes.c_void_p), ("out_n", ctypes.c_void_p),
+                ("warmup", ctypes.c_float), ("deadzone", ctypes.c_float), ("beta", ctypes.c_float),
+                ("grad_mode", ctypes.c_int), ("sumsq_bare", ctypes.c_void_p), ("g", ctypes.c_void_p),
+                ("S", ctypes.c_int), ("clip_w", ctypes.c_void_p), ("gdet", ctypes.c_int),
+                ("grad_res", ctypes.c_void_p), ("targeted", ctypes.c_int), ("sign_flip_cos", ctypes.c_float),
+                ("norm_ema", ctypes.c_void_p), ("norm_n", ctypes.c_void_p), ("tol", ctypes.c_float),
+                ("symmetric", ctypes.c_int), ("hm0", ctypes.c_float), ("hm1", ctypes.c_float),
+                ("hm2", ctypes.c_float), ("hm3", ctypes.c_float), ("truth", ctypes.c_int),
+                ("quarantine", ctypes.c_int), ("ctrl", ctypes.c_void_p)]
 
 # digest layout (floats)
 D_LOSS, D_OUT_FLAG, D_OUT_Z, D_GRAD_FLAG, D_GRAD_Z = 0, 1, 2, 3, 4
@@ -167,6 +187,8 @@ class StageVerifier:
         """Run detection on this step's signals and fill the digest row (device)."""
         if self.side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
+        if VERIFY_FUSED and self.device.type == "cuda":
+            return self._finish_fused(flat_grad, loss, host_metrics, attack_truth, stage_id)
         d = self.digest
         d.zero_()
         # scalar writes into device tensors go through fill_ (a kernel): `d[i] = 1.0` is a blocking
@@ -259,6 +281,68 @@ class StageVerifier:
             d[D_GRAD_SUMSQ] = sumsq * (1.0 - self.ctrl[1])
         self._have_out = False
         return d
+
+    def _finish_fused(self, flat_grad, loss, host_metrics, attack_truth: bool, stage_id: int) -> torch.Tensor:
+        """finish_step on the GPU in 2-5 launches: statistics final pass, detector features, the two
+        detectors, and csrc/stats.hip verify_finish_kernel for everything else (same arithmetic as
+        the torch form below; tests/test_kernels_gpu.py compares the two)."""
+        from ..ops import _lib
+        from ..ops._lib import ptr, stream_ptr
+        if not getattr(StageVerifier, "_args_checked", False):
+            n = int(_lib.lib().tdl_verify_args_bytes())
+            if n != ctypes.sizeof(_FinishArgs):
+                raise RuntimeError(f"VerifyFinishArgs layout mismatch: native {n} vs ctypes {ctypes.sizeof(_FinishArgs)}")
+            StageVerifier._args_checked = True
+        dev = self.device
+        out_on = bool(self.output_detection and self._have_out)
+        bare = not self.verify_on
+        g = None
+        grad_mode = 0
+        sumsq_bare = None
+        if bare and self.grad_stats is not None and flat_grad is not None:
+            grad_mode = 1
+            sumsq_bare = self.sumsq.compute(flat_grad, self.clip_w)
+        elif self.grad_stats is not None and flat_grad is not None:
+            grad_mode = 2
+            g = self.grad_stats.compute(flat_grad, with_quantiles=self._quantiles)
+        gdet = grad_mode == 2 and self.gradient_verification and not self._skip_grad_once
+        if grad_mode == 2 and self.gradient_verification and self._skip_grad_once:
+            self._skip_grad_once = False   # baselines restored without the EMA reference
+        targeted = self.features != "reference"
+        if out_on or gdet:
+            if targeted:
+                fb = getattr(self, "_feat_buf", None)
+                if fb is None:
+                    fb = self._feat_buf = torch.zeros(6, dtype=torch.float32, device=dev)
+                _lib.call("tdl_verify_features", ptr(self.out_stats if out_on else None), ptr(g if gdet else None),
+                          ptr(fb[0:3]), ptr(fb[3:6]), stream_ptr(dev))
+                of, gf = fb[0:3], fb[3:6]
+            else:
+                of, gf = self.out_stats[:12], (g[:17] if g is not None else None)
+        ores = self.out_det.observe(of) if out_on else None
+        gres = self.grad_det.observe(gf) if gdet else None
+        if loss is not None:
+            lf = getattr(self, "_loss_buf", None)
+            if lf is None:
+                lf = self._loss_buf = torch.zeros(1, dtype=torch.float32, device=dev)
+            lf.copy_(loss.detach().reshape(1))
+        hm = [float(v) for v in host_metrics][:4] + [0.0] * max(0, 4 - len(host_metrics))
+        a = _FinishArgs(
+            d=self.digest.data_ptr(), loss=lf.data_ptr() if loss is not None else 0, stage_id=int(stage_id),
+            out_on=int(out_on), out_res=ores.data_ptr() if ores is not None else 0,
+            out_stats=self.out_stats.data_ptr(), out_mu=self.out_mu.data_ptr(), out_sd=self.out_sd.data_ptr(),
+            out_n=self.out_n.data_ptr(), warmup=float(self.warmup), deadzone=float(self.deadzone),
+            beta=float(self.beta), grad_mode=grad_mode,
+            sumsq_bare=sumsq_bare.data_ptr() if sumsq_bare is not None else 0,
+            g=g.data_ptr() if g is not None else 0, S=int(self.S), clip_w=self.clip_w.data_ptr(), gdet=int(gdet),
+            grad_res=gres.data_ptr() if gres is not None else 0, targeted=int(targeted),
+            sign_flip_cos=float(self.sign_flip_cos), norm_ema=self.norm_ema.data_ptr(),
+            norm_n=self.norm_n.data_ptr(), tol=float(self.tol), symmetric=int(bool(self.symmetric)),
+            hm0=hm[0], hm1=hm[1], hm2=hm[2], hm3=hm[3], truth=int(bool(attack_truth)),
+            quarantine=int(bool(self.quarantine)), ctrl=self.ctrl.data_ptr())
+        _lib.call("tdl_verify_finish", ctypes.byref(a), stream_ptr(dev))
+        self._have_out = False
+        return self.digest
 
     def _grad_features(self, g: torch.Tensor) -> torch.Tensor:
         if self.features == "reference":
