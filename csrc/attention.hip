@@ -32,7 +32,9 @@
 // software-pipelined form (two sub-tiles per barrier as straight-line S/dP(0), S/dP(1), [softmax |
 // dV/dK](0), [softmax | dV/dK](1), dP started from -delta) needs 389 VGPRs = one wave per SIMD and
 // measured 1220.7 vs 952.8 us for the whole backward at B=64 (profiles/r4_attn_dkdv_pipelined_ab.jsonl):
-// the second wave per SIMD hides more than the in-wave interleave does.
+// the second wave per SIMD hides more than the in-wave interleave does.  Packing the score scaling
+// into v_pk_fma (as the forward does) measured no change either (profiles/r4_attn_bwd_pkfma_ab.txt):
+// the backward kernels wait on s_waitcnt / barriers, they are not VALU-bound.
 static int dkdv_ns() {
     static int ns = [] {
         const char* e = std::getenv("TDL_ATTN_DKDV_NS");
