@@ -53,7 +53,7 @@ def test_bench_multirank_json_line(n, mode):
     comms, streams = d["config"]["rccl_comms_per_rank"], d["config"]["hip_streams_per_rank"]
     assert len(comms) == n and len(streams) == n
     per_peer = 2 if mode == "async" else 1            # async: one activation + one gradient communicator per peer
-    groups = 2 if mode == "async" else 0              # the two direction groups
+    groups = (2 if mode == "async" else 0) + 1        # the two direction groups + the audit group
     tie = 1                                           # the tied embedding / LM head all-reduce group
     ranks = [int(x.split("@rank")[1].split(":")[0]) for x in d["config"]["plan"].split() if "@rank" in x]
     for r, c in enumerate(comms):
@@ -83,8 +83,8 @@ def test_bench_midrun_reassign():
     assert r["from_nodes"] == [3] and r["step"] == 2
     assert "@rank3" not in r["plan"] and r["plan"].count("stage") == 3
     assert d["config"]["last_loss"] is not None and d["value"] > 0
-    # the re-plan reused the direction groups and created ONE new tie group (ranks 0 and 2)
-    assert d["config"]["process_groups_created"] == 2 + 1 + 1
+    # the re-plan reused the direction and audit groups and created ONE new tie group (ranks 0 and 2)
+    assert d["config"]["process_groups_created"] == 2 + 1 + 1 + 1
 
 
 @pytest.mark.parametrize("fault", ["hang", "raise"])

@@ -224,9 +224,9 @@ def test_replans_reuse_process_groups():
         res = [json.load(open(f"{out}.{r}")) for r in range(world)]
     for r in res:
         created = [i["groups_created"] for i in r["inv"]]
-        assert created[0] == 3                   # act + grad direction groups + tie group (0, 3)
-        assert created[1] == 4                   # + tie group (0, 2) after the re-shard
-        assert created[2:] == [4, 4, 4]          # re-plans onto known member sets reuse them
+        assert created[0] == 4                   # act + grad direction groups + audit group + tie group (0, 3)
+        assert created[1] == 5                   # + tie group (0, 2) after the re-shard
+        assert created[2:] == [5, 5, 5]          # re-plans onto known member sets reuse them
         assert all(i["hip_streams"] <= 32 for i in r["inv"])
         assert r["inv"][-1]["rccl_comms"] == r["inv"][1]["rccl_comms"]
         assert r["loss"] is not None

@@ -438,6 +438,10 @@ class PipelineEngine:
             # (s+1 -> s): each carries one-way, in-order traffic per neighbour pair
             everyone = list(range(self.world))
             self._dir_groups = (self._group("act", everyone), self._group("grad", everyone))
+        if self.cfg.audit and getattr(self, "_audit_pg", None) is None:
+            # the audit's weight shipment runs on its own communicator, posted before the schedule
+            # and overlapped with it (``_audit_early_ship``)
+            self._audit_pg = self._group("audit", list(range(self.world)))
         # tied parameters living on different ranks need a gradient all-reduce group (one per
         # replica; new_group is collective over the whole world, so every rank creates them all)
         base = self.replica * self.pp
@@ -833,6 +837,7 @@ class PipelineEngine:
         s = st.stage_id
         first, last = s == 0, s == S - 1
         self._attack_params(node, st, truth)
+        self._audit_early_ship(st)
         in_shape, out_shape = self._boundary_shapes(st, inputs[0])
         act_dtype = self.dtype
         defer_w = self.cfg.defer_wgrad and not first
@@ -971,6 +976,7 @@ class PipelineEngine:
         s = st.stage_id
         first, last = s == 0, s == S - 1
         self._attack_params(node, st, truth)
+        self._audit_early_ship(st)
         in_shape, out_shape = self._boundary_shapes(st, inputs[0])
         act_pg, grad_pg = self._dir_groups
         prev, nxt = self.comm.prev, self.comm.next
@@ -1560,6 +1566,40 @@ class PipelineEngine:
             d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1],
                                                                     err.to(d.device)))
 
+    def _audit_early_ship(self, st: Stage):
+        """Distributed audit, weights part, posted BEFORE the 1F1B schedule on the audit
+        communicator so the transfer overlaps the step instead of sitting in its tail (a stage of
+        GPT-2-medium at 8 stages ships 75-180 MB of bf16 weights per step).  The weights sent are
+        those of the step (posted after the attacker's parameter hook, nothing writes them before
+        the optimizer, which runs after the audit waited for the transfer); shipping every step
+        reveals nothing about the private choice, so this runs only when every step is audited
+        (``audit_prob`` = 1).  ``_audit_dist`` waits for it and skips its own weight transfer."""
+        self._early_ship = None
+        if not (self.distributed and getattr(self, "_audit_now", False) and self.cfg.audit_prob >= 1.0
+                and getattr(self, "_audit_pg", None) is not None):
+            return
+        s, S = st.stage_id, self.plan.num_stages
+        prev, nxt = self.comm.prev, self.comm.next
+        bwd = self.cfg.audit_backward
+        my_auditor = nxt if nxt is not None else (prev if bwd and s == S - 1 and prev is not None else None)
+        mirrors: Dict[str, Stage] = {}
+        sends, recvs = [], []
+        if my_auditor is not None:
+            sends.append((st.flat.data, my_auditor))
+        if prev is not None:
+            mirrors["prev"] = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
+            recvs.append((mirrors["prev"].flat.data, prev))
+        if bwd and nxt is not None and s + 1 == S - 1:
+            mirrors["next"] = self._audit_mirror(tuple(self.plan.ranges[s + 1]), s + 1)
+            recvs.append((mirrors["next"].flat.data, nxt))
+        if not sends and not recvs:
+            return
+        g = self._audit_pg
+        ops = [dist.P2POp(dist.isend, t, r, g) for t, r in sends] + [dist.P2POp(dist.irecv, t, r, g) for t, r in recvs]
+        a = self.__dict__.setdefault("_audit_cost", {"steps": 0, "host_s": 0.0, "bytes": 0, "events": []})
+        a["bytes"] += sum(t.numel() * t.element_size() for t, _ in sends + recvs)
+        self._early_ship = (dist.batch_isend_irecv(ops), mirrors)
+
     def _audit_dist(self, rows: Dict[int, torch.Tensor]):
         """Distributed audit protocol of one rank (stage s of S):
 
@@ -1680,17 +1720,21 @@ class PipelineEngine:
             if bwd and all(m in self._audit_sent_dx for m in ms_req):
                 dx_send = [self._audit_sent_dx[m].contiguous() for m in ms_req]
             store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send[0].shape))
-        # ---- 3. ship
+        # ---- 3. ship (the weights went out before the schedule when ``_audit_early_ship`` ran)
+        early = getattr(self, "_early_ship", None)
+        self._early_ship = None
         sends, recvs = [], []
         if ms_req:
-            sends.append((st.flat.data, my_auditor))
+            if early is None:
+                sends.append((st.flat.data, my_auditor))
             sends += [(t, my_auditor) for t in x_send]
             sends += [(t, my_auditor) for t in dx_send]
         mir_p = mir_n = None
         x_prev, dx_prev = [], []
         if audit_prev and ms_prev:
             mir_p = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
-            recvs.append((mir_p.flat.data, prev))
+            if early is None:
+                recvs.append((mir_p.flat.data, prev))
             if s - 1 > 0:
                 k = f"{tag}/shape/{prev}"
                 shape = torch.Size([int(v) for v in store.get(k).decode().split(",")])
@@ -1702,8 +1746,12 @@ class PipelineEngine:
                     recvs += [(t, prev) for t in dx_prev]
         if audit_next and ms_next:
             mir_n = self._audit_mirror(tuple(self.plan.ranges[s + 1]), s + 1)
-            recvs.append((mir_n.flat.data, nxt))
+            if early is None:
+                recvs.append((mir_n.flat.data, nxt))
         self._audit_transfer(sends, recvs, prev, nxt, act_g, grad_g)
+        if early is not None:
+            for w in early[0]:
+                w.wait()
 
         def combine(acc, res):
             if acc is None:
