@@ -106,6 +106,9 @@ def main():
     ap.add_argument("--reassign-at", type=int, default=-1,
                     help="after this many steps (warmup included), exclude the last pipeline rank and "
                          "re-shard its layers over the others (exercises migration mid-run)")
+    ap.add_argument("--audit-targeted", action="store_true",
+                    help="audit the anomaly-picked micro-batch too (EngineConfig.audit_targeted; one host "
+                         "read per step on the auditors)")
     ap.add_argument("--debug-fault", default="", choices=["", "hang", "raise"])
     ap.add_argument("--debug-fault-rank", type=int, default=-1)
     ap.add_argument("--debug-fault-step", type=int, default=1)
@@ -219,7 +222,8 @@ def run(args):
                        adamw=AdamWConfig(lr=args.lr, weight_decay=0.01, max_grad_norm=1.0),
                        attack_detection=verify, gradient_verification=verify, quarantine=verify,
                        param_integrity=verify,
-                       reassign=False, trace_phases=bool(args.trace_phases))
+                       reassign=False, trace_phases=bool(args.trace_phases),
+                       audit_targeted=True if args.audit_targeted else None)
     engine = PipelineEngine(model, cfg)
     del model
 
