@@ -59,6 +59,16 @@ struct ConvDims {
     int R, S, stride, pad;  // filter geometry of the FORWARD convolution
 };
 
+// Output-parity class of a strided data gradient: dX pixel (h, w) with h = h0 + cs i, w = w0 + cs j
+// only receives the taps r = r0 + cs t (t < nr), s = s0 + cs u (u < ns), where r0 = (h0 + pad) mod cs
+// (every other tap lands between dY pixels).  One launch per class runs a GEMM over exactly those
+// taps instead of masking 3 of every 4 (stride 2) to zero inside the K loop.  The identity class
+// (cs = 1, Ps = P, nr = R, ...) is the plain convolution.  row_off: first statistics partial row of
+// the class (the classes of one call share one partial-row buffer and one finalize).
+struct ConvCls {
+    int Ps, Qs, h0, w0, r0, s0, nr, ns, cs, row_off;
+};
+
 constexpr int BM = 128;  // m (pixels) per workgroup
 constexpr int FIN_CNT = 256;  // statistics-finalize arrival counters (column blocks of 64, 2 Cout <= 16384)
 constexpr int BK = 64;   // k per step
@@ -90,7 +100,7 @@ __device__ __forceinline__ uint4 pro_apply(uint4 v, const float* sc, const float
 template <int BCO, bool TRANSPOSED, bool STATS, bool PRO = false, bool BNB = false>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restrict__ act, const bf16_t* __restrict__ wk,
                                                          bf16_t* __restrict__ out, float* __restrict__ part,
-                                                         ConvDims d, const float* __restrict__ pro,
+                                                         ConvDims d, ConvCls cl, const float* __restrict__ pro,
                                                          const bf16_t* __restrict__ bx = nullptr,
                                                          float* __restrict__ zero_stats = nullptr,
                                                          unsigned* __restrict__ fin_cnt = nullptr) {
@@ -108,8 +118,10 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, lr = lane & 31;
     const int wco = w >> 1, wm = w & 1;
-    const int M = d.N * d.P * d.Q;
-    const int K = d.R * d.S * d.Cin;
+    const int PQs = cl.Ps * cl.Qs;
+    const int M = d.N * PQs;                 // output pixels of this class
+    const int Kw = d.R * d.S * d.Cin;        // weight row length
+    const int K = cl.nr * cl.ns * d.Cin;     // reduction length of this class
     const int ntco = (d.Cout + BCO - 1) / BCO, ntm = (M + BM - 1) / BM;
     const int wg = xcd_remap(blockIdx.x, ntco * ntm);
     const int tco = wg % ntco, tm = wg / ntco;
@@ -117,13 +129,13 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
 
     // ---- per-thread staging geometry: rows srow + 32 i, 16-byte chunk sch of the 64-wide k step
     const int srow = tid >> 3, sch = tid & 7;
-    const int PQ = d.P * d.Q;
     int b_img[4], b_y[4], b_x[4];  // image offset, and spatial origin of each staged pixel row
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + srow + 32 * i;
         if (m < M) {
-            const int n = m / PQ, pq = m - n * PQ, p = pq / d.Q, q = pq - p * d.Q;
+            const int n = m / PQs, pq = m - n * PQs, ip = pq / cl.Qs, jq = pq - ip * cl.Qs;
+            const int p = cl.h0 + cl.cs * ip, q = cl.w0 + cl.cs * jq;
             b_img[i] = n;
             b_y[i] = TRANSPOSED ? p + d.pad : p * d.stride - d.pad;
             b_x[i] = TRANSPOSED ? q + d.pad : q * d.stride - d.pad;
@@ -145,13 +157,15 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
         if (kin) {
             const int rs = kk / d.Cin;
             c = kk - rs * d.Cin;
-            r = rs / d.S;
-            s = rs - r * d.S;
+            const int tr = rs / cl.ns;
+            r = cl.r0 + cl.cs * tr;
+            s = cl.s0 + cl.cs * (rs - tr * cl.ns);
         }
+        const int kw = (r * d.S + s) * d.Cin + c;   // == kk for the identity class
 #pragma unroll
         for (int i = 0; i < AROWS; ++i) {
             const int co = co0 + srow + 32 * i;
-            areg[i] = (kin && co < d.Cout) ? *(const uint4*)(wk + (size_t)co * K + kk) : make_uint4(0, 0, 0, 0);
+            areg[i] = (kin && co < d.Cout) ? *(const uint4*)(wk + (size_t)co * Kw + kw) : make_uint4(0, 0, 0, 0);
         }
         if (PRO && kin) pro_load(pro, d.Cin, c, psc, psh);
         bok = 0;
@@ -236,6 +250,13 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
     // two pixel tiles in registers, over its 32 lanes by shuffles and over the two pixel-waves in
     // LDS; each workgroup writes its own partial row part[tm][2 * Cout] (no atomics, no memset).
     float* red = reinterpret_cast<float*>(As[0]);  // [2 (wm)][BCO][2], free after the K loop
+    int mfull[2];   // the lane's two output pixels as indices of the full [N][P][Q] image
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int m = m0 + wm * 64 + 32 * j + lr;
+        const int n = m / PQs, pq = m - n * PQs, ip = pq / cl.Qs, jq = pq - ip * cl.Qs;
+        mfull[j] = (n * d.P + cl.h0 + cl.cs * ip) * d.Q + cl.w0 + cl.cs * jq;
+    }
 #pragma unroll
     for (int i = 0; i < TCO; ++i) {
         const int cl = wco * (BCO / 2) + 32 * i;  // tile-local first channel of this MFMA tile
@@ -254,17 +275,17 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
             }
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int m = m0 + wm * 64 + 32 * j + lr;
+                const int m = m0 + wm * 64 + 32 * j + lr, mf = mfull[j];
                 const bool mok = m < M;
                 float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
                 const uint2 pk = pack4(v);
-                if (mok && co < d.Cout) *(uint2*)(out + (size_t)m * d.Cout + co) = pk;
+                if (mok && co < d.Cout) *(uint2*)(out + (size_t)mf * d.Cout + co) = pk;
                 if (STATS && mok) {
                     float r[4];
                     unpack4(pk, r);
                     if constexpr (BNB) {
                         float xv[4] = {0.f, 0.f, 0.f, 0.f};
-                        if (co < d.Cout) unpack4(*(const uint2*)(bx + (size_t)m * d.Cout + co), xv);
+                        if (co < d.Cout) unpack4(*(const uint2*)(bx + (size_t)mf * d.Cout + co), xv);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const float dv = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? r[e] : 0.f;
@@ -303,8 +324,9 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
         for (int c = tid; c < BCO; c += 256) {
             const int co = co0 + c;
             if (co < d.Cout) {
-                part[(size_t)tm * 2 * d.Cout + co] = red[c * 2] + red[(BCO + c) * 2];
-                part[(size_t)tm * 2 * d.Cout + d.Cout + co] = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
+                const size_t row = (size_t)(cl.row_off + tm) * 2 * d.Cout;
+                part[row + co] = red[c * 2] + red[(BCO + c) * 2];
+                part[row + d.Cout + co] = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
             }
         }
     }
@@ -512,6 +534,15 @@ __global__ __launch_bounds__(256) void krsc_to_kcrs_add_kernel(const float* __re
     }
 }
 
+// TDL_CONV_PARITY=0: strided data gradients as one masked GEMM over all taps (A/B switch)
+bool conv_parity_on() {
+    static const bool v = [] {
+        const char* e = getenv("TDL_CONV_PARITY");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    return v;
+}
+
 bool dims_ok(const ConvDims& d) {
     return d.Cin % 8 == 0 && d.Cout % 8 == 0 && d.N > 0 && d.P > 0 && d.Q > 0 && d.R > 0 && d.S > 0 && d.stride > 0 &&
            (long long)d.N * d.Hin * d.Win * d.Cin < (1ll << 31) && (long long)d.N * d.P * d.Q * d.Cout < (1ll << 31);
@@ -523,8 +554,12 @@ bool dims_ok(const ConvDims& d) {
 // transposed = 1 -> data-gradient mapping (act = dY, wk = W permuted to [Cin][R][S][Cout]).
 // stats: null, or fp32 [2 * Cout] = (per-channel sum, sum of squares) of out; then stats_ws must
 // hold tdl_conv_stats_ws_floats(...) floats (one partial row per 128-pixel tile).
+// partial rows: one per 128-pixel tile, + 3 for the tile rounding of the 4 parity classes of a
+// stride-2 data gradient
+static int64_t stats_rows(int M) { return (M + BM - 1) / BM + 3; }
+
 TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) {
-    return (int64_t)((M + BM - 1) / BM) * 2 * Cout + FIN_CNT;   // + the finalize's arrival counters
+    return stats_rows(M) * 2 * Cout + FIN_CNT;   // + the finalize's arrival counters
 }
 
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
@@ -538,18 +573,36 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     const bool st = stats != nullptr;
     if (st && stats_ws == nullptr) return (int)hipErrorInvalidValue;
     const bool big = Cout > 64;
-    const int ntm = (M + BM - 1) / BM;
-    const int nblk = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
     auto A = (const bf16_t*)act;
     auto W = (const bf16_t*)wk;
     auto O = (bf16_t*)out;
     float* zs = (st && !stats_accumulate) ? stats : nullptr;
-    unsigned* cnt = st ? (unsigned*)(stats_ws + (size_t)ntm * 2 * Cout) : nullptr;
+    unsigned* cnt = st ? (unsigned*)(stats_ws + (size_t)stats_rows(M) * 2 * Cout) : nullptr;
     if (st && (2 * Cout + 63) / 64 > FIN_CNT) return (int)hipErrorInvalidValue;
-#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, nullptr, nullptr, zs, cnt)
-#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, nullptr, zs, \
-                                                                                  cnt)
-#define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, pro, \
+    // a stride-2 data gradient runs as its 4 output-parity classes (ConvCls), the rest as one class
+    const int cs = (transposed && stride == 2 && conv_parity_on()) ? 2 : 1;
+    int rows = 0;
+    for (int h0 = 0; h0 < cs; ++h0)
+        for (int w0 = 0; w0 < cs; ++w0) {
+            ConvCls cl{P, Q, 0, 0, 0, 0, R, S, 1, rows};
+            if (cs > 1) {
+                cl.Ps = (P - h0 + cs - 1) / cs;
+                cl.Qs = (Q - w0 + cs - 1) / cs;
+                cl.h0 = h0, cl.w0 = w0, cl.cs = cs;
+                cl.r0 = (h0 + pad) % cs, cl.s0 = (w0 + pad) % cs;
+                cl.nr = cl.r0 < R ? (R - cl.r0 + cs - 1) / cs : 0;
+                cl.ns = cl.s0 < S ? (S - cl.s0 + cs - 1) / cs : 0;
+            }
+            if (cl.Ps <= 0 || cl.Qs <= 0) continue;
+            const int ntm = (N * cl.Ps * cl.Qs + BM - 1) / BM;
+            rows += ntm;
+            const int nblk = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
+            // a class with no taps (1x1 stride 2: three of four) runs an empty K loop and stores zeros
+#define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, nullptr, nullptr, \
+                                                                             zs, cnt)
+#define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, nullptr, \
+                                                                                  zs, cnt)
+#define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, \
                                                                                     (const bf16_t*)bnb_x, nullptr, cnt)
     if (bnb) {
         if (big) LAUNCHB(128);
@@ -567,10 +620,11 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
 #undef LAUNCH
 #undef LAUNCHP
 #undef LAUNCHB
+        }
     if (st) {
         const int rpb = 64;
-        const dim3 g((2 * Cout + 63) / 64, (ntm + rpb - 1) / rpb);
-        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, ntm, 2 * Cout, rpb, stats, cnt);
+        const dim3 g((2 * Cout + 63) / 64, (rows + rpb - 1) / rpb);
+        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, rows, 2 * Cout, rpb, stats, cnt);
     }
     TDL_LAUNCH_CHECK();
 }

@@ -16,6 +16,9 @@ SHAPES = [
     (2, 3, 32, 32, 64, 7, 2, 3),     # image stem: channels padded to 8
     (1, 24, 9, 7, 40, 3, 1, 1),      # ragged everything
     (4, 64, 56, 56, 64, 3, 1, 1),    # many pixel tiles
+    # stride-2 data gradients run as 4 output-parity classes: odd extents give unequal classes
+    (1, 24, 9, 7, 40, 3, 2, 1),
+    (2, 16, 7, 7, 32, 1, 2, 0),      # 1x1 stride 2: three classes have no tap (zeros)
 ]
 
 
