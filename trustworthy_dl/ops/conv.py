@@ -37,6 +37,64 @@ def _num_cu(dev: torch.device) -> int:
     return n
 
 
+class _WgradSide:
+    """Weight gradients of the convolutions on a second HIP stream.
+
+    A convolution's data gradient and weight gradient both need only dY: the data gradient stays
+    on the compute stream (the backward's critical path) and the weight gradient runs beside it.
+    ResNet-50's 14 x 14 / 7 x 7 layers launch 196 / 100 data-gradient workgroups on 256 CUs, so the
+    weight gradient fills CUs that would idle.  Ordering: every consumer of a weight gradient
+    waits for this stream — the backward pass itself at its end (an autograd final callback makes
+    the compute stream wait) and the verifier's side stream before it takes per-layer gradient
+    statistics mid-backward (``wait_wgrad``).  ``TDL_CONV_WGRAD_SIDE=0``: weight gradients on the
+    compute stream."""
+    streams = {}
+    pending = {}
+
+    @classmethod
+    def on(cls) -> bool:
+        return os.environ.get("TDL_CONV_WGRAD_SIDE", "1") != "0"
+
+    @classmethod
+    def run(cls, dev: torch.device, fn, keep):
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        side = cls.streams.get(idx)
+        if side is None:
+            side = cls.streams[idx] = torch.cuda.Stream(device=dev)
+        cur = torch.cuda.current_stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            fn()
+        for t in keep:
+            if t is not None:
+                t.record_stream(side)
+        if not cls.pending.get(idx):
+            cls.pending[idx] = True
+
+            def _join(idx=idx, cur=cur, side=side):
+                cur.wait_stream(side)
+                cls.pending[idx] = False
+            torch.autograd.Variable._execution_engine.queue_callback(_join)
+
+    @classmethod
+    def wait(cls, stream: torch.cuda.Stream, dev: torch.device):
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        if cls.pending.get(idx):
+            stream.wait_stream(cls.streams[idx])
+
+
+def wait_wgrad(stream, dev: torch.device):
+    """Make ``stream`` wait for the convolution weight gradients issued so far (see _WgradSide)."""
+    _WgradSide.wait(stream, dev)
+
+
+def _wgrad(dev: torch.device, fn, keep):
+    if _WgradSide.on() and torch.is_grad_enabled() is False:
+        _WgradSide.run(dev, fn, keep)
+    else:
+        fn()
+
+
 def native_conv_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.bfloat16
 
@@ -137,13 +195,15 @@ class _Conv2dNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             mg = getattr(weight, "main_grad", None)
             if mg is not None and cp == C and mg.is_contiguous():
-                acc = mg
+                # into the fp32 main_grad: on the weight-gradient stream, beside the data gradient
+                ws = torch.empty(Cout * R * S * cp, dtype=torch.float32, device=dev) if R * S > 1 else None
+                _wgrad(dev, lambda: _lib.call("tdl_conv_wgrad", ptr(dy), ptr(xs), ptr(mg), ptr(ws), N, H, W, cp, P, Q,
+                                              Cout, R, S, stride, pad, _num_cu(dev), stream_ptr(dev)), (dy, xs, ws))
             else:
                 acc = torch.zeros((Cout, cp, R, S), dtype=torch.float32, device=dev)
-            ws = torch.empty(Cout * R * S * cp, dtype=torch.float32, device=dev) if R * S > 1 else None
-            _lib.call("tdl_conv_wgrad", ptr(dy), ptr(xs), ptr(acc), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
-                      pad, _num_cu(dev), stream_ptr(dev))
-            if acc is not mg:
+                ws = torch.empty(Cout * R * S * cp, dtype=torch.float32, device=dev) if R * S > 1 else None
+                _lib.call("tdl_conv_wgrad", ptr(dy), ptr(xs), ptr(acc), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
+                          pad, _num_cu(dev), stream_ptr(dev))
                 g = acc if cp == C else acc[:, :C]
                 if mg is not None:
                     mg.add_(g)
@@ -280,8 +340,14 @@ class _BNActConvNHWC(torch.autograd.Function):
             acc = mg if (mg is not None and mg.is_contiguous()) else torch.zeros((Cout, C, R, S), dtype=torch.float32,
                                                                                  device=dev)
             wsw = torch.empty(Cout * R * S * C, dtype=torch.float32, device=dev) if R * S > 1 else None
-            _lib.call("tdl_conv_wgrad_pro", ptr(dout), ptr(ys), ptr(acc), ptr(wsw), N, H, W, C, P, Q, Cout, R, S,
-                      stride, pad, _num_cu(dev), ptr(pro), stream_ptr(dev))
+
+            def _wg():
+                _lib.call("tdl_conv_wgrad_pro", ptr(dout), ptr(ys), ptr(acc), ptr(wsw), N, H, W, C, P, Q, Cout, R, S,
+                          stride, pad, _num_cu(dev), ptr(pro), stream_ptr(dev))
+            if acc is mg:
+                _wgrad(dev, _wg, (dout, ys, wsw, bnp))
+            else:
+                _wg()
             if acc is not mg:
                 if mg is not None:
                     mg.add_(acc)
