@@ -24,6 +24,7 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import ptr, stream_ptr
 from .layers import _scratch
+from .side_stream import WgradSide, wait_wgrad  # noqa: F401  (wait_wgrad: re-exported)
 
 _NUM_CU = {}
 
@@ -37,60 +38,9 @@ def _num_cu(dev: torch.device) -> int:
     return n
 
 
-class _WgradSide:
-    """Weight gradients of the convolutions on a second HIP stream.
-
-    A convolution's data gradient and weight gradient both need only dY: the data gradient stays
-    on the compute stream (the backward's critical path) and the weight gradient runs beside it.
-    ResNet-50's 14 x 14 / 7 x 7 layers launch 196 / 100 data-gradient workgroups on 256 CUs, so the
-    weight gradient fills CUs that would idle.  Ordering: every consumer of a weight gradient
-    waits for this stream — the backward pass itself at its end (an autograd final callback makes
-    the compute stream wait) and the verifier's side stream before it takes per-layer gradient
-    statistics mid-backward (``wait_wgrad``).  ``TDL_CONV_WGRAD_SIDE=0``: weight gradients on the
-    compute stream."""
-    streams = {}
-    pending = {}
-
-    @classmethod
-    def on(cls) -> bool:
-        return os.environ.get("TDL_CONV_WGRAD_SIDE", "1") != "0"
-
-    @classmethod
-    def run(cls, dev: torch.device, fn, keep):
-        idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        side = cls.streams.get(idx)
-        if side is None:
-            side = cls.streams[idx] = torch.cuda.Stream(device=dev)
-        cur = torch.cuda.current_stream(dev)
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            fn()
-        for t in keep:
-            if t is not None:
-                t.record_stream(side)
-        if not cls.pending.get(idx):
-            cls.pending[idx] = True
-
-            def _join(idx=idx, cur=cur, side=side):
-                cur.wait_stream(side)
-                cls.pending[idx] = False
-            torch.autograd.Variable._execution_engine.queue_callback(_join)
-
-    @classmethod
-    def wait(cls, stream: torch.cuda.Stream, dev: torch.device):
-        idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        if cls.pending.get(idx):
-            stream.wait_stream(cls.streams[idx])
-
-
-def wait_wgrad(stream, dev: torch.device):
-    """Make ``stream`` wait for the convolution weight gradients issued so far (see _WgradSide)."""
-    _WgradSide.wait(stream, dev)
-
-
 def _wgrad(dev: torch.device, fn, keep):
-    if _WgradSide.on() and torch.is_grad_enabled() is False:
-        _WgradSide.run(dev, fn, keep)
+    if WgradSide.on("TDL_CONV_WGRAD_SIDE", "1") and not torch.is_grad_enabled():
+        WgradSide.run(dev, fn, keep)
     else:
         fn()
 

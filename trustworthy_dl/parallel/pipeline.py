@@ -1173,6 +1173,9 @@ class PipelineEngine:
             st = self.my_stage()
             if st is not None:
                 self._note_tied_pre(st)
+            if g.is_cuda:   # a weight gradient still running on the side stream (ops/side_stream.py)
+                from ..ops.side_stream import wait_wgrad
+                wait_wgrad(torch.cuda.current_stream(g.device), g.device)
             self._tie_work = dist.all_reduce(g, group=self.tie_group, async_op=True)
 
     def _allreduce_tied(self):

@@ -177,7 +177,7 @@ class StageVerifier:
         stream = self.side if self.side is not None else cur
         if self.side is not None:
             self.side.wait_stream(cur)
-        from ..ops.conv import wait_wgrad   # convolution weight gradients run on their own stream
+        from ..ops.side_stream import wait_wgrad   # weight gradients may run on their own stream
         wait_wgrad(stream, self.device)
         for lo, hi in seg_runs:
             c0, c1 = self.grad_stats.chunk_range_of(lo, hi)
