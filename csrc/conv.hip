@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                                                          ConvDims d, ConvCls cl, const float* __restrict__ pro,
                                                          const bf16_t* __restrict__ bx = nullptr,
                                                          float* __restrict__ zero_stats = nullptr,
-                                                         unsigned* __restrict__ fin_cnt = nullptr) {
+                                                         unsigned* __restrict__ fin_cnt = nullptr,
+                                                         float* __restrict__ splitws = nullptr, int kps = 0) {
     // the statistics finalize (next launch on the stream) accumulates into stats: zero it here
     // instead of a separate memset launch per convolution; likewise its arrival counters
     if (zero_stats != nullptr && blockIdx.x == 0)
@@ -212,13 +213,17 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
 #pragma unroll
     for (int i = 0; i < TCO; ++i) acc[i][0] = acc[i][1] = f32x16{};
 
+    // split-K (splitws != null): workgroup (x, z) runs K steps [z kps, (z + 1) kps) and stores its
+    // fp32 partial tile; conv_split_epi_kernel sums the slices in order and runs the epilogue
     const int nk = (K + BK - 1) / BK;
-    gload(0);
+    const int kt0 = splitws != nullptr ? (int)blockIdx.y * kps : 0;
+    const int kt1 = splitws != nullptr ? min(nk, kt0 + kps) : nk;
+    gload(kt0 * BK);
     sstore(0);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        const bool has_next = kt + 1 < nk;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const int buf = (kt - kt0) & 1;
+        const bool has_next = kt + 1 < kt1;
         if (has_next) gload((kt + 1) * BK);
         const bf16_t* A_ = As[buf];
         const bf16_t* B_ = Bs[buf];
@@ -249,6 +254,23 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
     // STATS: per-channel sum / sumsq of the stored (bf16-rounded) values, reduced over the wave's
     // two pixel tiles in registers, over its 32 lanes by shuffles and over the two pixel-waves in
     // LDS; each workgroup writes its own partial row part[tm][2 * Cout] (no atomics, no memset).
+    if (splitws != nullptr) {
+        float* slab = splitws + (size_t)blockIdx.y * M * d.Cout;
+#pragma unroll
+        for (int i = 0; i < TCO; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = co0 + wco * (BCO / 2) + 32 * i + 8 * g + 4 * h;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int m = m0 + wm * 64 + 32 * j + lr;
+                    if (m < M && co < d.Cout)
+                        *(float4*)(slab + (size_t)m * d.Cout + co) =
+                            make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+                }
+            }
+        return;
+    }
     float* red = reinterpret_cast<float*>(As[0]);  // [2 (wm)][BCO][2], free after the K loop
     int mfull[2];   // the lane's two output pixels as indices of the full [N][P][Q] image
 #pragma unroll
@@ -329,6 +351,78 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                 part[row + d.Cout + co] = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
             }
         }
+    }
+}
+
+// Epilogue of a split-K convolution: out = bf16(sum of the split slices, in slice order) and, with
+// STATS, the per-channel partial rows of the 128-pixel tile exactly as conv_nt_kernel writes them
+// (BNB: the BatchNorm-backward sums of the folded BN).  Workgroup = 128 pixels x 64 channels;
+// thread = 4 channels x 8 pixels, 16 threads per 256-byte row segment.
+template <bool STATS, bool BNB>
+__global__ __launch_bounds__(256) void conv_split_epi_kernel(const float* __restrict__ ws, int split, int M, int Cout,
+                                                             bf16_t* __restrict__ out, float* __restrict__ part,
+                                                             const bf16_t* __restrict__ bx,
+                                                             const float* __restrict__ bnp) {
+    __shared__ float red[16][64][2];
+    const int tm = blockIdx.x, cb = blockIdx.y * 64;
+    const int cg = threadIdx.x & 15, rr = threadIdx.x >> 4;
+    const int co = cb + 4 * cg;
+    const bool cok = co < Cout;
+    float sv[4] = {0.f, 0.f, 0.f, 0.f}, sq[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsc[4] = {}, bsh[4] = {}, bmu[4] = {}, brs[4] = {};
+    if (BNB && cok) {
+        const float4 a = *(const float4*)(bnp + co), b = *(const float4*)(bnp + Cout + co);
+        const float4 c = *(const float4*)(bnp + 2 * Cout + co), e = *(const float4*)(bnp + 3 * Cout + co);
+        bsc[0] = a.x, bsc[1] = a.y, bsc[2] = a.z, bsc[3] = a.w;
+        bsh[0] = b.x, bsh[1] = b.y, bsh[2] = b.z, bsh[3] = b.w;
+        bmu[0] = c.x, bmu[1] = c.y, bmu[2] = c.z, bmu[3] = c.w;
+        brs[0] = e.x, brs[1] = e.y, brs[2] = e.z, brs[3] = e.w;
+    }
+#pragma unroll 2
+    for (int i = 0; i < 8; ++i) {
+        const int m = tm * BM + rr + 16 * i;
+        if (m >= M || !cok) continue;
+        float4 a = *(const float4*)(ws + (size_t)m * Cout + co);
+        for (int z = 1; z < split; ++z) {
+            const float4 b = *(const float4*)(ws + ((size_t)z * M + m) * Cout + co);
+            a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
+        }
+        float v[4] = {a.x, a.y, a.z, a.w};
+        const uint2 pk = pack4(v);
+        *(uint2*)(out + (size_t)m * Cout + co) = pk;
+        if (STATS) {
+            float r[4];
+            unpack4(pk, r);
+            if constexpr (BNB) {
+                float xv[4];
+                unpack4(*(const uint2*)(bx + (size_t)m * Cout + co), xv);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float dv = fmaf(xv[e], bsc[e], bsh[e]) > 0.f ? r[e] : 0.f;
+                    sv[e] += dv;
+                    sq[e] += dv * (xv[e] - bmu[e]) * brs[e];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    sv[e] += r[e];
+                    sq[e] += r[e] * r[e];
+                }
+            }
+        }
+    }
+    if (!STATS) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        red[rr][4 * cg + e][0] = sv[e];
+        red[rr][4 * cg + e][1] = sq[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+        const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+        float t = 0.f;
+        for (int k = 0; k < 16; ++k) t += red[k][c][q];
+        if (cb + c < Cout) part[(size_t)tm * 2 * Cout + q * Cout + cb + c] = t;
     }
 }
 
@@ -534,6 +628,15 @@ __global__ __launch_bounds__(256) void krsc_to_kcrs_add_kernel(const float* __re
     }
 }
 
+// TDL_CONV_SPLIT=0: no split-K for convolutions whose grid leaves the chip short (A/B switch)
+bool conv_split_on() {
+    static const bool v = [] {
+        const char* e = getenv("TDL_CONV_SPLIT");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    return v;
+}
+
 // TDL_CONV_PARITY=0: strided data gradients as one masked GEMM over all taps (A/B switch)
 bool conv_parity_on() {
     static const bool v = [] {
@@ -560,6 +663,29 @@ static int64_t stats_rows(int M) { return (M + BM - 1) / BM + 3; }
 
 TDL_API int64_t tdl_conv_stats_ws_floats(int M, int Cout) {
     return stats_rows(M) * 2 * Cout + FIN_CNT;   // + the finalize's arrival counters
+}
+
+// Split-K factor of a one-class convolution GEMM (M pixels x Cout channels, reduction K): the
+// 14 x 14 / 7 x 7 layers of ResNet-50 at batch 64 launch 196 / 100 workgroups of 128 x 128 on 256
+// CUs (2 fit per CU), so their long K loops (up to 72 steps) run on a fraction of the chip.  Split
+// until ~512 workgroups, each keeping >= 8 K steps.
+static int conv_split_of(int M, int Cout, int K) {
+    if (!conv_split_on()) return 1;
+    const int ntm = (M + BM - 1) / BM, ntco = Cout > 64 ? (Cout + 127) / 128 : (Cout + 63) / 64;
+    const int nblk = ntm * ntco, nk = (K + BK - 1) / BK;
+    if (nblk >= 256 || nk < 16) return 1;
+    int split = min(4, (512 + nblk - 1) / nblk);
+    while (split > 1 && nk / split < 8) --split;
+    if (split <= 1) return 1;
+    const int kps = (nk + split - 1) / split;
+    return (nk + kps - 1) / kps;
+}
+
+// Whole workspace of one tdl_conv_nt* call: statistics partial rows + finalize counters, then the
+// split-K slices (when conv_split_of splits; parity = 1 for a stride-2 data gradient: no split)
+TDL_API int64_t tdl_conv_ws_floats(int M, int Cout, int K, int parity) {
+    const int split = parity ? 1 : conv_split_of(M, Cout, K);
+    return tdl_conv_stats_ws_floats(M, Cout) + (split > 1 ? (int64_t)split * M * Cout : 0);
 }
 
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
@@ -596,14 +722,22 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
             if (cl.Ps <= 0 || cl.Qs <= 0) continue;
             const int ntm = (N * cl.Ps * cl.Qs + BM - 1) / BM;
             rows += ntm;
-            const int nblk = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
+            const int nblk0 = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
+            // split-K (one-class GEMMs, workspace given): slices after the statistics area
+            const int K = R * S * Cin, nk = (K + BK - 1) / BK;
+            // (never for a stride-2 data gradient, parity classes or not: tdl_conv_ws_floats(parity = 1)
+            // sized the caller's workspace without slices)
+            const int split = (!(transposed && stride == 2) && stats_ws != nullptr) ? conv_split_of(M, Cout, K) : 1;
+            const int kps = (nk + split - 1) / split;
+            float* sws = split > 1 ? stats_ws + tdl_conv_stats_ws_floats(M, Cout) : nullptr;
+            const dim3 nblk(nblk0, split);
             // a class with no taps (1x1 stride 2: three of four) runs an empty K loop and stores zeros
 #define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, nullptr, nullptr, \
-                                                                             zs, cnt)
+                                                                             zs, cnt, sws, kps)
 #define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, nullptr, \
-                                                                                  zs, cnt)
+                                                                                  zs, cnt, sws, kps)
 #define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, \
-                                                                                    (const bf16_t*)bnb_x, nullptr, cnt)
+                                                                                    (const bf16_t*)bnb_x, nullptr, cnt, sws, kps)
     if (bnb) {
         if (big) LAUNCHB(128);
         else LAUNCHB(64);
@@ -620,6 +754,18 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
 #undef LAUNCH
 #undef LAUNCHP
 #undef LAUNCHB
+            if (split > 1) {
+                const dim3 ge(ntm, (Cout + 63) / 64);
+                if (bnb)
+                    conv_split_epi_kernel<true, true><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, stats_ws,
+                                                                         (const bf16_t*)bnb_x, pro);
+                else if (st)
+                    conv_split_epi_kernel<true, false><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, stats_ws, nullptr,
+                                                                          nullptr);
+                else
+                    conv_split_epi_kernel<false, false><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, nullptr, nullptr,
+                                                                           nullptr);
+            }
         }
     if (st) {
         const int rpb = 64;

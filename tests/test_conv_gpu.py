@@ -19,6 +19,9 @@ SHAPES = [
     # stride-2 data gradients run as 4 output-parity classes: odd extents give unequal classes
     (1, 24, 9, 7, 40, 3, 2, 1),
     (2, 16, 7, 7, 32, 1, 2, 0),      # 1x1 stride 2: three classes have no tap (zeros)
+    # grids far below the CU count with long K loops run split-K (ordered slice sum + epilogue)
+    (2, 512, 7, 7, 512, 3, 1, 1),    # forward and data gradient split 4
+    (2, 1024, 7, 7, 256, 1, 1, 0),   # forward split 2
 ]
 
 
@@ -176,8 +179,9 @@ def _chain_modules(cin, mid, cout, stride, seed):
     return units
 
 
-@pytest.mark.parametrize("stride", [1, 2])
-def test_bn_fold_chain_matches_unfolded_and_fp32(stride, monkeypatch):
+@pytest.mark.parametrize("stride,widths,hw", [(1, (64, 32, 64), 16), (2, (64, 32, 64), 16),
+                                              (1, (256, 128, 256), 8)])   # last: conv2 fwd / dgrad split-K
+def test_bn_fold_chain_matches_unfolded_and_fp32(stride, widths, hw, monkeypatch):
     """Bottleneck chain conv1-BN1-ReLU-conv2-BN2-ReLU-conv3-BN3(+res)-ReLU with BN1/BN2 + ReLU folded
     into conv2 / conv3 (tdl_bn_finalize + tdl_conv_nt_pro / tdl_conv_wgrad_pro + tdl_bn_act_bwd_pro:
     the BN outputs are never written) against the unfolded native path and an fp32 torch reference:
@@ -187,10 +191,10 @@ def test_bn_fold_chain_matches_unfolded_and_fp32(stride, monkeypatch):
     folded = []
     orig = conv_mod._BNActConvNHWC.apply
     monkeypatch.setattr(conv_mod._BNActConvNHWC, "apply", lambda *a: folded.append(1) or orig(*a))
-    cin, mid, cout = 64, 32, 64
-    x = torch.randn(4, cin, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    res = torch.randn(4, cout, 16 // stride, 16 // stride, device="cuda").to(torch.bfloat16)
-    gy = torch.randn(4, cout, 16 // stride, 16 // stride, device="cuda").to(torch.bfloat16)
+    cin, mid, cout = widths
+    x = torch.randn(4, cin, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(4, cout, hw // stride, hw // stride, device="cuda").to(torch.bfloat16)
+    gy = torch.randn(4, cout, hw // stride, hw // stride, device="cuda").to(torch.bfloat16)
     runs = {}
     for fold in ("1", "0"):
         monkeypatch.setenv("TDL_BN_FOLD", fold)

@@ -131,6 +131,7 @@ _SIGNATURES = {
     # conv.hip / bn.hip
     "tdl_conv_nt": [_P] * 5 + [_I] * 12 + [_P],
     "tdl_conv_stats_ws_floats": [_I, _I],
+    "tdl_conv_ws_floats": [_I, _I, _I, _I],
     "tdl_conv_wgrad": [_P] * 4 + [_I] * 12 + [_P],
     "tdl_bn_act_fwd": [_P] * 13 + [_L, _I, _F, _F, _I, _P],
     "tdl_bn_bwd_ws_floats": [_I],

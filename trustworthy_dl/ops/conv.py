@@ -45,6 +45,12 @@ def _wgrad(dev: torch.device, fn, keep):
         fn()
 
 
+def _conv_ws(M: int, Cout: int, K: int, parity: bool, dev) -> torch.Tensor:
+    """Workspace of one tdl_conv_nt* call: statistics partial rows + finalize counters, and the
+    split-K slices when the kernel splits the reduction (csrc/conv.hip conv_split_of)."""
+    return torch.empty(int(_lib.lib().tdl_conv_ws_floats(M, Cout, K, int(parity))), dtype=torch.float32, device=dev)
+
+
 def native_conv_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.bfloat16
 
@@ -107,11 +113,10 @@ class _Conv2dNHWC(torch.autograd.Function):
         wk = _weight_layout(weight, cp, "krsc")
         P, Q = _out_hw(H, W, R, S, stride, pad)
         y = torch.empty((N, Cout, P, Q), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        stats = ws = None
+        stats = None
         if want_stats:
             stats = torch.empty(2 * Cout, dtype=torch.float32, device=x.device)
-            ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * P * Q, Cout)), dtype=torch.float32,
-                             device=x.device)
+        ws = _conv_ws(N * P * Q, Cout, R * S * cp, False, x.device)
         _lib.call("tdl_conv_nt", ptr(xs), ptr(wk), ptr(y), ptr(stats), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
                   pad, 0, stream_ptr(x.device))
         ctx.save_for_backward(xs, weight)
@@ -138,7 +143,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wd = _weight_layout(weight, cp, "crsk")  # [cp][R][S][Cout]
             dxp = torch.empty((N, cp, H, W), dtype=dy.dtype, device=dev, memory_format=torch.channels_last)
-            _lib.call("tdl_conv_nt", ptr(dy), ptr(wd), ptr(dxp), None, None, N, P, Q, Cout, H, W, cp, R, S, stride,
+            wsd = _conv_ws(N * H * W, cp, R * S * Cout, stride == 2, dev)
+            _lib.call("tdl_conv_nt", ptr(dy), ptr(wd), ptr(dxp), None, ptr(wsd), N, P, Q, Cout, H, W, cp, R, S, stride,
                       pad, 1, stream_ptr(dev))
             dx = dxp if cp == C else dxp[:, :C]
         gw = None
@@ -246,11 +252,10 @@ class _BNActConvNHWC(torch.autograd.Function):
         wk = _weight_layout(weight, C, "krsc")
         P, Q = _out_hw(H, W, R, S, stride, pad)
         out = torch.empty((N, Cout, P, Q), dtype=y.dtype, device=dev, memory_format=torch.channels_last)
-        st = ws = None
+        st = None
         if want_stats:
             st = torch.empty(2 * Cout, dtype=torch.float32, device=dev)
-            ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * P * Q, Cout)), dtype=torch.float32,
-                             device=dev)
+        ws = _conv_ws(N * P * Q, Cout, R * S * C, False, dev)
         _lib.call("tdl_conv_nt_pro", ptr(ys), ptr(wk), ptr(out), ptr(st), ptr(ws), N, H, W, C, P, Q, Cout, R, S,
                   stride, pad, ptr(pro), stream_ptr(dev))
         ctx.save_for_backward(ys, bnp, gamma, weight)
@@ -280,7 +285,7 @@ class _BNActConvNHWC(torch.autograd.Function):
         # backward below is the elementwise pass only
         wd = _weight_layout(weight, C, "crsk")  # [C][R][S][Cout]
         dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
-        ws = torch.empty(int(_lib.lib().tdl_conv_stats_ws_floats(N * H * W, C)), dtype=torch.float32, device=dev)
+        ws = _conv_ws(N * H * W, C, R * S * Cout, stride == 2, dev)
         _lib.call("tdl_conv_dgrad_bnsums", ptr(dout), ptr(wd), ptr(dbn), ptr(ws), N, P, Q, Cout, H, W, C, R, S, stride,
                   pad, ptr(ys), ptr(bnp), ptr(ctx.sums), stream_ptr(dev))
         # weight gradient against relu(BN(y)) recomputed on load
