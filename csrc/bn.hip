@@ -10,10 +10,10 @@
 
 namespace {
 
-// Backward sums live in NREP replicas of [2C] (the data-gradient convolutions' BN-sum epilogues
-// add into them, replica = block % NREP: 16x less same-address atomic contention than one copy);
-// bn_fold_kernel folds the replicas into the final row the dx pass reads.
-constexpr int NREP = 16;
+// Backward sums: one [2C] row (sum dv | sum dv * xhat) per BN, zeroed by the forward, completed in a
+// fixed order by the last workgroup of a reduction (bn_partial_fold_kernel here, or the data-gradient
+// convolution's statistics finalize, conv.hip), which also adds them into dbeta / dgamma: the dx
+// pass reads the row directly (the former replicated rows needed a separate fold launch per BN).
 // Backward reduction: each row-chunk workgroup STORES its per-channel partial sums into its own
 // row of a [NB_MAX][2C] block (no atomics: the former per-block fp32 atomics into the replicas were
 // ~25 us per million on MI355X and dominated the pass for C >= 512, scripts/bench_bn.py), then
@@ -244,7 +244,8 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
 // group of the column block to arrive (agent-scope counter, release / acquire) adds the FOLD_G
 // totals in group order.  cnt: zeroed by bn_act_bwd_reduce_kernel.
 __global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, float* __restrict__ partials,
-                                                              int nb, int C, unsigned* __restrict__ cnt) {
+                                                              int nb, int C, unsigned* __restrict__ cnt,
+                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
     __shared__ int is_last;
     const int col = blockIdx.x * blockDim.x + threadIdx.x;
     float* part = partials + col;
@@ -275,7 +276,12 @@ __global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict_
 #pragma unroll
     for (int g = 0; g < FOLD_G; ++g)
         a += __hip_atomic_load(part + (size_t)g * 2 * C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sums[col] += a;
+    const float tot = sums[col] + a;
+    sums[col] = tot;
+    if (dgamma != nullptr) {
+        if (col < C) dbeta[col] += tot;
+        else dgamma[col - C] += tot;
+    }
 }
 
 // ---------------------------------------------------------------- backward pass 2: elementwise
@@ -313,21 +319,6 @@ __global__ __launch_bounds__(256) void bn_act_bwd_dx_kernel(const bf16_t* __rest
             o[e] = g[e] * rs * (dv[e] - sums[c] * invM - xh * sums[C + c] * invM);
         }
         ((uint4*)dx)[v] = pack8(o);
-    }
-}
-
-// sums[c] = sum over the NREP replicas (stored after them), and dgamma/dbeta += (one tiny pass)
-__global__ __launch_bounds__(256) void bn_fold_kernel(float* __restrict__ rep, float* __restrict__ dgamma,
-                                                      float* __restrict__ dbeta, int C) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= 2 * C) return;
-    float a = 0.f;
-#pragma unroll
-    for (int r = 0; r < NREP; ++r) a += rep[(size_t)r * 2 * C + c];
-    rep[(size_t)NREP * 2 * C + c] = a;
-    if (dgamma) {
-        if (c < C) dbeta[c] += a;
-        else dgamma[c - C] += a;
     }
 }
 
@@ -369,9 +360,8 @@ int grid_for(int64_t nvec) {
 
 }  // namespace
 
-// Floats of the replicated backward-reduction buffer for C channels (allocated with the forward).
-// (replicas + their sum; kept from the forward to the backward, so only (NREP + 1) x 2C)
-TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)(NREP + 1) * 2 * C; }
+// Floats of the backward-sums row for C channels (allocated with the forward, kept to the backward).
+TDL_API int64_t tdl_bn_bwd_ws_floats(int C) { return (int64_t)2 * C; }
 // Floats of the backward's per-block partial rows (scratch of ONE backward call, not kept).
 // + the fold's arrival counters (one per 256-column block)
 TDL_API int64_t tdl_bn_bwd_part_floats(int C) { return (int64_t)NB_MAX * 2 * C + (2 * C + 255) / 256; }
@@ -386,7 +376,7 @@ TDL_API int tdl_bn_act_fwd(const void* x, const float* stats, const float* run_m
     if (C % 8 != 0) return (int)hipErrorInvalidValue;
     bn_act_fwd_kernel<<<grid_for(M * (C / 8)), 256, 0, s>>>(
         (const bf16_t*)x, stats, run_mean, run_var, (const bf16_t*)gamma, (const bf16_t*)beta, (const bf16_t*)res,
-        (bf16_t*)out, save_mean, save_rstd, upd_mean, upd_var, bwd_ws, bwd_ws ? (int64_t)NREP * 2 * C : 0, M, C, eps,
+        (bf16_t*)out, save_mean, save_rstd, upd_mean, upd_var, bwd_ws, bwd_ws ? (int64_t)2 * C : 0, M, C, eps,
         momentum, relu);
     TDL_LAUNCH_CHECK();
 }
@@ -397,7 +387,7 @@ TDL_API int tdl_bn_finalize(const float* stats, const void* gamma, const void* b
                             float* upd_mean, float* upd_var, float* pro, float* bwd_ws, int64_t M, int C, float eps,
                             float momentum, hipStream_t s) {
     if (C % 8 != 0 || stats == nullptr || pro == nullptr || bwd_ws == nullptr) return (int)hipErrorInvalidValue;
-    const int64_t zn = (int64_t)NREP * 2 * C;
+    const int64_t zn = (int64_t)2 * C;
     int g = (int)((zn + 255) / 256);
     const int gc = (C + 255) / 256;
     if (g < gc) g = gc;
@@ -425,12 +415,11 @@ static int bn_act_bwd_impl(const void* dout, const void* out, const void* x, con
     bn_act_bwd_reduce_kernel<<<grid, 256, 0, s>>>((const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd,
                                                   part, M, C, (int)rows_per_block, relu, pro,
                                                   (unsigned*)(part + (size_t)NB_MAX * 2 * C));
-    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(sums, part, nb, C,
-                                                                            (unsigned*)(part + (size_t)NB_MAX * 2 * C));
-    bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
+    bn_partial_fold_kernel<<<dim3((2 * C + 255) / 256, FOLD_G), 256, 0, s>>>(
+        sums, part, nb, C, (unsigned*)(part + (size_t)NB_MAX * 2 * C), dgamma, dbeta);
     bn_act_bwd_dx_kernel<<<grid_for(M * CV), 256, 0, s>>>(
         (const bf16_t*)dout, (const bf16_t*)out, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma,
-        sums + (size_t)NREP * 2 * C, (bf16_t*)dx, (bf16_t*)dres, M, C, relu, pro);
+        sums, (bf16_t*)dx, (bf16_t*)dres, M, C, relu, pro);
     TDL_LAUNCH_CHECK();
 }
 
@@ -442,16 +431,15 @@ TDL_API int tdl_bn_act_bwd(const void* dout, const void* out, const void* x, con
     return bn_act_bwd_impl(dout, out, x, mean, rstd, gamma, sums, part, dx, dres, dgamma, dbeta, M, C, relu, nullptr, s);
 }
 
-// Backward of a folded BN (+ ReLU) whose two per-channel sums were already reduced (into the first
-// replica row of sums) by the producing data-gradient convolution (tdl_conv_dgrad_bnsums): fold +
-// the elementwise pass only.
+// Backward of a folded BN (+ ReLU) whose two per-channel sums were already reduced (and added into
+// dbeta / dgamma) by the producing data-gradient convolution (tdl_conv_dgrad_bnsums): the
+// elementwise pass only.
 TDL_API int tdl_bn_act_bwd_pro_summed(const void* dout, const void* x, const float* mean, const float* rstd,
-                                      const void* gamma, const float* pro, float* sums, void* dx, float* dgamma,
-                                      float* dbeta, int64_t M, int C, hipStream_t s) {
+                                      const void* gamma, const float* pro, const float* sums, void* dx, int64_t M, int C,
+                                      hipStream_t s) {
     if (C % 8 != 0 || pro == nullptr) return (int)hipErrorInvalidValue;
-    bn_fold_kernel<<<(2 * C + 255) / 256, 256, 0, s>>>(sums, dgamma, dbeta, C);
     bn_act_bwd_dx_kernel<<<grid_for(M * (C / 8)), 256, 0, s>>>(
-        (const bf16_t*)dout, nullptr, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma, sums + (size_t)NREP * 2 * C,
+        (const bf16_t*)dout, nullptr, (const bf16_t*)x, mean, rstd, (const bf16_t*)gamma, sums,
         (bf16_t*)dx, nullptr, M, C, 1, pro);
     TDL_LAUNCH_CHECK();
 }

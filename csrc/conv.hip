@@ -434,9 +434,13 @@ __global__ __launch_bounds__(256) void conv_split_epi_kernel(const float* __rest
 // Workgroup (x, y) sums rows [y rpb, (y + 1) rpb) of its 64 columns and stores the total in the
 // group's first row; the LAST workgroup of column block x to arrive (agent-scope counter, release /
 // acquire) adds the gridDim.y group totals in group order.  fin_cnt: zeroed by the conv kernel.
+// acc_lo / acc_hi (nullable): the completed column c is also added into acc_lo[c] (c < cols / 2) or
+// acc_hi[c - cols / 2] (a folded BN's backward sums -> dbeta / dgamma).
 __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__ part, int rows, int cols,
                                                              int rows_per_block, float* __restrict__ stats,
-                                                             unsigned* __restrict__ fin_cnt) {
+                                                             unsigned* __restrict__ fin_cnt,
+                                                             float* __restrict__ acc_lo = nullptr,
+                                                             float* __restrict__ acc_hi = nullptr) {
     __shared__ float red[4][64];
     __shared__ int is_last;
     const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
@@ -470,8 +474,15 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
                                    __HIP_MEMORY_SCOPE_AGENT);
     red[rg][threadIdx.x & 63] = a;
     __syncthreads();
-    if (rg == 0 && c < cols)
-        stats[c] += ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    if (rg == 0 && c < cols) {
+        const float v = stats[c] + (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x]);
+        stats[c] = v;
+        if (acc_lo != nullptr) {
+            const int half = cols >> 1;
+            if (c < half) acc_lo[c] += v;
+            else acc_hi[c - half] += v;
+        }
+    }
 }
 
 // ============================================================================ conv_wgrad
@@ -690,7 +701,8 @@ TDL_API int64_t tdl_conv_ws_floats(int M, int Cout, int K, int parity) {
 
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
                         int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
-                        const float* pro, hipStream_t s, const void* bnb_x = nullptr, bool stats_accumulate = false) {
+                        const float* pro, hipStream_t s, const void* bnb_x = nullptr, bool stats_accumulate = false,
+                        float* acc_lo = nullptr, float* acc_hi = nullptr) {
     ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
     const bool bnb = bnb_x != nullptr;
     if (!dims_ok(d) || (pro != nullptr && transposed && !bnb)) return (int)hipErrorInvalidValue;
@@ -770,7 +782,7 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     if (st) {
         const int rpb = 64;
         const dim3 g((2 * Cout + 63) / 64, (rows + rpb - 1) / rpb);
-        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, rows, 2 * Cout, rpb, stats, cnt);
+        stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, rows, 2 * Cout, rpb, stats, cnt, acc_lo, acc_hi);
     }
     TDL_LAUNCH_CHECK();
 }
@@ -867,14 +879,17 @@ TDL_API int tdl_conv_weight_layouts(const void* w, void* krsc, void* crsk, int C
 }
 
 // Data gradient dbn of a convolution whose input relu(BN(y)) was folded into its operand load, with
-// the BN backward's per-channel sums reduced in its epilogue (see BNB): sums (fp32 [2 C], the first
-// replica row of the BN's zeroed backward buffer) += (sum dv, sum dv * xhat); bnp = [scale | shift |
-// mean | rstd] fp32 [4 C]; y = the BN input (NHWC, same shape as dbn).  Pair with tdl_bn_act_bwd_pro_summed.
+// the BN backward's per-channel sums reduced in its epilogue (see BNB): sums (fp32 [2 C], the BN's
+// backward row, zeroed by its forward) += (sum dv, sum dv * xhat), and the completed sums are added
+// into dbeta / dgamma (fp32 [C] each, or both null); bnp = [scale | shift | mean | rstd] fp32 [4 C];
+// y = the BN input (NHWC, same shape as dbn).  Pair with tdl_bn_act_bwd_pro_summed.
 TDL_API int tdl_conv_dgrad_bnsums(const void* dy, const void* wd, void* dbn, float* ws, int N, int Hin, int Win, int Cin,
                                   int P, int Q, int Cout, int R, int S, int stride, int pad, const void* y,
-                                  const float* bnp, float* sums, hipStream_t s) {
-    if (y == nullptr || bnp == nullptr || sums == nullptr || ws == nullptr) return (int)hipErrorInvalidValue;
-    return conv_nt_impl(dy, wd, dbn, sums, ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 1, bnp, s, y, true);
+                                  const float* bnp, float* sums, float* dgamma, float* dbeta, hipStream_t s) {
+    if (y == nullptr || bnp == nullptr || sums == nullptr || ws == nullptr || (dgamma == nullptr) != (dbeta == nullptr))
+        return (int)hipErrorInvalidValue;
+    return conv_nt_impl(dy, wd, dbn, sums, ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 1, bnp, s, y, true,
+                        dbeta, dgamma);
 }
 
 TDL_API int tdl_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int N, int Hin, int Win, int Cin, int P,

@@ -7,7 +7,10 @@ out=${OUT:-gpurun_out/cnn_env_ab.txt}
 : > $out
 for r in $(seq 1 ${ROUNDS:-3}); do
   for e in $ENVS; do
-    line=$(env $e timeout -k 10 200 python -u ${BENCH:-bench_cnn.py --model ${MODEL:-resnet50}} --steps ${STEPS:-30} --warmup 5 2>/dev/null | grep '^{') || exit 1
+    # AB_DIR=<dir>: run that tree (e.g. a build of the previous commit in ab_old/) instead
+    dir=.
+    case $e in AB_DIR=*) dir=${e#AB_DIR=} ;; esac
+    line=$(cd $dir && env $e timeout -k 10 200 python -u ${BENCH:-bench_cnn.py --model ${MODEL:-resnet50}} --steps ${STEPS:-30} --warmup 5 2>/dev/null | grep '^{') || exit 1
     echo "round $r $e $line" >> $out
     echo "round $r $e done"
   done

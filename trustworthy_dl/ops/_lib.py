@@ -85,8 +85,8 @@ _SIGNATURES = {
     "tdl_embedding_bwd": [_P, _P, _P, _P, _I, _I, _I, _I, _P],
     "tdl_add_into_f32": [_P, _P, _L, _I, _P],
     "tdl_conv_weight_layouts": [_P, _P, _P, _I, _I, _I, _I, _P],
-    "tdl_conv_dgrad_bnsums": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
-    "tdl_bn_act_bwd_pro_summed": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
+    "tdl_conv_dgrad_bnsums": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
+    "tdl_bn_act_bwd_pro_summed": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     "tdl_global_avgpool_fwd": [_P, _P, _I, _I, _I, _P],
     "tdl_global_avgpool_bwd": [_P, _P, _I, _I, _I, _P],
     "tdl_maxpool_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P],

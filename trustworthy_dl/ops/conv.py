@@ -283,11 +283,16 @@ class _BNActConvNHWC(torch.autograd.Function):
         # data gradient of the conv = gradient w.r.t. the (never stored) BN output; its epilogue also
         # reduces the BN backward's per-channel sums (ReLU mask recomputed from y), so the BN
         # backward below is the elementwise pass only
+        # (the completed sums are also the BN's bias / scale gradients: added into dbeta / dgamma there)
+        beta = ctx.beta
+        mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
+        dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
+        db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
         wd = _weight_layout(weight, C, "crsk")  # [C][R][S][Cout]
         dbn = torch.empty((N, C, H, W), dtype=dout.dtype, device=dev, memory_format=torch.channels_last)
         ws = _conv_ws(N * H * W, C, R * S * Cout, stride == 2, dev)
         _lib.call("tdl_conv_dgrad_bnsums", ptr(dout), ptr(wd), ptr(dbn), ptr(ws), N, P, Q, Cout, H, W, C, R, S, stride,
-                  pad, ptr(ys), ptr(bnp), ptr(ctx.sums), stream_ptr(dev))
+                  pad, ptr(ys), ptr(bnp), ptr(ctx.sums), ptr(dg), ptr(db), stream_ptr(dev))
         # weight gradient against relu(BN(y)) recomputed on load
         gw = None
         if ctx.needs_input_grad[8]:
@@ -310,12 +315,8 @@ class _BNActConvNHWC(torch.autograd.Function):
                     gw = acc.to(weight.dtype)
         # BN (+ ReLU) backward with the mask recomputed from y
         dy = torch.empty_like(ys, memory_format=torch.channels_last)
-        beta = ctx.beta
-        mg_g, mg_b = getattr(gamma, "main_grad", None), getattr(beta, "main_grad", None)
-        dg = mg_g if mg_g is not None else torch.zeros(C, dtype=torch.float32, device=dev)
-        db = mg_b if mg_b is not None else torch.zeros(C, dtype=torch.float32, device=dev)
         _lib.call("tdl_bn_act_bwd_pro_summed", ptr(dbn), ptr(ys), ptr(mean), ptr(rstd), ptr(gamma), ptr(pro),
-                  ptr(ctx.sums), ptr(dy), ptr(dg), ptr(db), N * H * W, C, stream_ptr(dev))
+                  ptr(ctx.sums), ptr(dy), N * H * W, C, stream_ptr(dev))
         gg = None if mg_g is not None else dg.to(gamma.dtype)
         gb = None if mg_b is not None else db.to(beta.dtype)
         return dy, None, gg, gb, None, None, None, None, gw, None, None, None
