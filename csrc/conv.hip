@@ -868,6 +868,46 @@ __global__ __launch_bounds__(256) void conv_weight_layouts_kernel(const bf16_t* 
     }
 }
 
+// Up to LAYOUT_MAX weights' layouts in ONE launch (kernel argument by value, no descriptor upload):
+// a stage's convolution weights change every optimizer step, and one launch per weight put ~50
+// dependent ~7 us launches at the head of each ResNet-50 forward.  Grid (blocks per weight, n).
+constexpr int LAYOUT_MAX = 32;
+struct LayoutBatch {
+    const bf16_t* w[LAYOUT_MAX];
+    bf16_t* krsc[LAYOUT_MAX];
+    bf16_t* crsk[LAYOUT_MAX];
+    int Cout[LAYOUT_MAX], C[LAYOUT_MAX], Cp[LAYOUT_MAX], RS[LAYOUT_MAX];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void conv_weight_layouts_batch_kernel(const LayoutBatch b) {
+    const int j = blockIdx.y;
+    const bf16_t* __restrict__ w = b.w[j];
+    bf16_t* __restrict__ krsc = b.krsc[j];
+    bf16_t* __restrict__ crsk = b.crsk[j];
+    const int Cout = b.Cout[j], C = b.C[j], Cp = b.Cp[j], RS = b.RS[j];
+    const int64_t n = (int64_t)Cout * Cp * RS;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % Cp);
+        const int64_t t = i / Cp;
+        const int rs = (int)(t % RS);
+        const int co = (int)(t / RS);
+        const bf16_t v = c < C ? w[((int64_t)co * C + c) * RS + rs] : (bf16_t)0;
+        krsc[i] = v;
+        crsk[((int64_t)c * RS + rs) * Cout + co] = v;
+    }
+}
+
+// Python packs the LayoutBatch (ctypes structure passed by value).
+TDL_API int tdl_conv_weight_layouts_batch(LayoutBatch b, hipStream_t s) {
+    if (b.n <= 0 || b.n > LAYOUT_MAX) return (int)hipErrorInvalidValue;
+    for (int j = 0; j < b.n; ++j)
+        if (b.Cp[j] < b.C[j] || b.Cout[j] <= 0 || b.RS[j] <= 0 || !b.w[j] || !b.krsc[j] || !b.crsk[j])
+            return (int)hipErrorInvalidValue;
+    conv_weight_layouts_batch_kernel<<<dim3(64, b.n), 256, 0, s>>>(b);
+    TDL_LAUNCH_CHECK();
+}
+
 TDL_API int tdl_conv_weight_layouts(const void* w, void* krsc, void* crsk, int Cout, int C, int Cp, int RS, hipStream_t s) {
     if (Cp < C || Cout <= 0 || RS <= 0) return (int)hipErrorInvalidValue;
     const int64_t n = (int64_t)Cout * Cp * RS;

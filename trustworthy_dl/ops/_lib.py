@@ -71,6 +71,14 @@ def check(err: int, name: str):
 
 _P, _I, _L, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 
+class LayoutBatch(ctypes.Structure):
+    """csrc/conv.hip LayoutBatch (passed by value): up to 32 conv weights' layout jobs."""
+    MAX = 32
+    _fields_ = [("w", ctypes.c_void_p * 32), ("krsc", ctypes.c_void_p * 32), ("crsk", ctypes.c_void_p * 32),
+                ("Cout", ctypes.c_int * 32), ("C", ctypes.c_int * 32), ("Cp", ctypes.c_int * 32),
+                ("RS", ctypes.c_int * 32), ("n", ctypes.c_int)]
+
+
 # name -> argtypes (restype is int for all)
 _SIGNATURES = {
     # norm_act.hip
@@ -141,6 +149,7 @@ _SIGNATURES = {
     "tdl_bn_act_bwd_pro": [_P] * 11 + [_L, _I, _I, _P],
     "tdl_conv_nt_pro": [_P] * 5 + [_I] * 11 + [_P, _P],
     "tdl_conv_wgrad_pro": [_P] * 4 + [_I] * 12 + [_P, _P],
+    "tdl_conv_weight_layouts_batch": [LayoutBatch, _P],
 }
 
 

@@ -90,6 +90,38 @@ def _weight_layout(weight: torch.Tensor, cp: int, kind: str) -> torch.Tensor:
     return hit[1][kind]
 
 
+def prebuild_layouts(weights) -> None:
+    """Build the kernel layouts of every conv weight in ``weights`` whose cached layouts are stale
+    (a new weight generation) in batched native launches (tdl_conv_weight_layouts_batch, 32
+    weights per launch) instead of one launch per weight at its first use: the pipeline stage calls
+    this at the head of each forward (parallel/stage.py).  Same outputs and cache as _weight_layout."""
+    from .layers import _WEIGHT_GEN
+    todo = []
+    for w in weights:
+        if not (w.is_cuda and w.dtype == torch.bfloat16 and w.is_contiguous() and w.dim() == 4):
+            continue
+        cp = (w.shape[1] + 7) // 8 * 8
+        key = (_WEIGHT_GEN[0], w._version, w.data_ptr(), cp)
+        hit = getattr(w, "_tdl_conv_layouts", None)
+        if hit is None or hit[0] != key:
+            todo.append((w, cp, key))
+    for i in range(0, len(todo), _lib.LayoutBatch.MAX):
+        chunk = todo[i:i + _lib.LayoutBatch.MAX]
+        b = _lib.LayoutBatch()
+        b.n = len(chunk)
+        for j, (w, cp, key) in enumerate(chunk):
+            Cout, C, R, S = w.shape
+            krsc = torch.empty((Cout, R, S, cp), dtype=w.dtype, device=w.device)
+            crsk = torch.empty((cp, R, S, Cout), dtype=w.dtype, device=w.device)
+            b.w[j], b.krsc[j], b.crsk[j] = w.data_ptr(), krsc.data_ptr(), crsk.data_ptr()
+            b.Cout[j], b.C[j], b.Cp[j], b.RS[j] = Cout, C, cp, R * S
+            try:
+                w._tdl_conv_layouts = (key, {"krsc": krsc, "crsk": crsk})
+            except (AttributeError, RuntimeError):
+                pass
+        _lib.call("tdl_conv_weight_layouts_batch", b, stream_ptr(chunk[0][0].device))
+
+
 def _pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
     N, C, H, W = x.shape
     xp = torch.empty((N, cp, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last).zero_()

@@ -193,6 +193,13 @@ class Stage:
         layer input so that layer's gradient statistics start on the verifier's side stream as
         soon as its backward is done, overlapping the backward of the layers before it."""
         layers = self._runners()
+        if x.is_cuda:
+            cw = getattr(self, "_conv_weights", None)
+            if cw is None:   # the stage's conv weights (bf16 views into the flat buffer)
+                cw = self._conv_weights = [m.weight for m in self.module.modules() if isinstance(m, nn.Conv2d)]
+            if cw:   # their kernel layouts for this weight generation, batched (ops/conv.py)
+                from ..ops.conv import prebuild_layouts
+                prebuild_layouts(cw)
         arm = arm_grad_stats and getattr(self, "_layer_seg_runs", None) is not None
         for k, layer in enumerate(layers[:-1]):
             if arm and x.requires_grad:
