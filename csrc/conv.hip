@@ -26,6 +26,10 @@
 //   parameter's [Cout][Cin][R][S] gradient by one transpose pass (1x1: straight into it).
 #include "common.h"
 
+#include <math.h>
+#include <mutex>
+#include <unordered_map>
+
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short short4_t __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
@@ -73,6 +77,79 @@ constexpr int BM = 128;  // m (pixels) per workgroup
 constexpr int FIN_CNT = 256;  // statistics-finalize arrival counters (column blocks of 64, 2 Cout <= 16384)
 constexpr int BK = 64;   // k per step
 
+// In-kernel statistics finalize.  The partial rows of a call are summed in a FIXED order (the
+// recompute audit needs bit-identical statistics, see stats_finalize_kernel) by the workgroups that
+// produce them, so no finalize launch sits between a convolution and its BatchNorm: rows are
+// grouped by gs; the last workgroup (per column tile) to store a row of a group sums the group's
+// rows into the group's first row, and the last group to finish adds the group totals in group
+// order into stats (and acc_lo / acc_hi, see stats_finalize_kernel).  cnt: per-stream arrival
+// counters, left at zero by the workgroups that consume them; tile t uses [t (ngroups + 1), ...).
+struct FinArgs {
+    unsigned* cnt;      // null: partial rows only (stats_finalize_kernel runs after)
+    int gs, ngroups, rows, accumulate;
+    float *stats, *acc_lo, *acc_hi;
+};
+
+// sum over q in [q0, q1) of p[q * step * ld], agent-scope loads, fixed order: 8 lanes of partial
+// sums (q mod 8) added pairwise at the end
+__device__ __forceinline__ float sum_rows(const float* p, int q0, int q1, int step, int ld) {
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int q = q0;
+    for (; q + 8 <= q1; q += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = __hip_atomic_load(p + (size_t)(q + u) * step * ld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] += v[u];
+    }
+    for (int u = 0; q < q1; ++q, ++u)
+        a[u] += __hip_atomic_load(p + (size_t)q * step * ld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// Every thread of the workgroup calls this after its row's columns [c0, c0 + nc) of both halves
+// (sum | sum of squares, row stride 2 Cout) were written with agent-scope stores.
+__device__ __forceinline__ void stats_arrive(float* __restrict__ part, int Cout, int row, int c0, int nc, int tile,
+                                             const FinArgs& f) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's row stores have landed
+    __syncthreads();
+    const int g = row / f.gs, r0 = g * f.gs, r1 = min(f.rows, r0 + f.gs);
+    unsigned* gc = f.cnt + (size_t)tile * (f.ngroups + 1) + g;
+    unsigned* cc = f.cnt + (size_t)tile * (f.ngroups + 1) + f.ngroups;
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (unsigned)(r1 - r0 - 1);
+        if (last) __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    const int t = threadIdx.x;
+    const int ch = c0 + (t < nc ? t : t - nc);
+    const bool act = t < 2 * nc && ch < Cout;
+    const size_t col = (size_t)(t < nc ? 0 : Cout) + ch;
+    if (act)   // 8 independent loads in flight (a serial chain of agent-scope loads is latency-bound)
+        __hip_atomic_store(part + (size_t)r0 * 2 * Cout + col, sum_rows(part + col, r0, r1, 1, 2 * Cout),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (unsigned)(f.ngroups - 1);
+        if (last) __hip_atomic_store(cc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last || !act) return;
+    const float a = sum_rows(part + col, 0, f.ngroups, f.gs, 2 * Cout);
+    const float v = f.accumulate ? f.stats[col] + a : a;
+    f.stats[col] = v;
+    if (f.acc_lo != nullptr) {
+        if (t < nc) f.acc_lo[ch] += v;
+        else f.acc_hi[ch] += v;
+    }
+}
+
 // ============================================================================ conv_nt (fwd / dgrad)
 // BatchNorm-apply + ReLU of the PREVIOUS layer folded into an activation operand load: the staged
 // 8-channel vector of pre-BN values y becomes relu(y * scale[c] + shift[c]) (pro = [scale[C] |
@@ -104,7 +181,8 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
                                                          const bf16_t* __restrict__ bx = nullptr,
                                                          float* __restrict__ zero_stats = nullptr,
                                                          unsigned* __restrict__ fin_cnt = nullptr,
-                                                         float* __restrict__ splitws = nullptr, int kps = 0) {
+                                                         float* __restrict__ splitws = nullptr, int kps = 0,
+                                                         FinArgs fin = FinArgs{}) {
     // the statistics finalize (next launch on the stream) accumulates into stats: zero it here
     // instead of a separate memset launch per convolution; likewise its arrival counters
     if (zero_stats != nullptr && blockIdx.x == 0)
@@ -346,11 +424,18 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(const bf16_t* __restric
         for (int c = tid; c < BCO; c += 256) {
             const int co = co0 + c;
             if (co < d.Cout) {
-                const size_t row = (size_t)(cl.row_off + tm) * 2 * d.Cout;
-                part[row + co] = red[c * 2] + red[(BCO + c) * 2];
-                part[row + d.Cout + co] = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
+                float* rowp = part + (size_t)(cl.row_off + tm) * 2 * d.Cout;
+                const float s_ = red[c * 2] + red[(BCO + c) * 2], q_ = red[c * 2 + 1] + red[(BCO + c) * 2 + 1];
+                if (fin.cnt != nullptr) {   // read back by another workgroup: agent-scope (sc1) stores
+                    __hip_atomic_store(rowp + co, s_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(rowp + d.Cout + co, q_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    rowp[co] = s_;
+                    rowp[d.Cout + co] = q_;
+                }
             }
         }
+        if (fin.cnt != nullptr) stats_arrive(part, d.Cout, cl.row_off + tm, co0, BCO, tco, fin);
     }
 }
 
@@ -362,7 +447,7 @@ template <bool STATS, bool BNB>
 __global__ __launch_bounds__(256) void conv_split_epi_kernel(const float* __restrict__ ws, int split, int M, int Cout,
                                                              bf16_t* __restrict__ out, float* __restrict__ part,
                                                              const bf16_t* __restrict__ bx,
-                                                             const float* __restrict__ bnp) {
+                                                             const float* __restrict__ bnp, FinArgs fin) {
     __shared__ float red[16][64][2];
     const int tm = blockIdx.x, cb = blockIdx.y * 64;
     const int cg = threadIdx.x & 15, rr = threadIdx.x >> 4;
@@ -422,8 +507,11 @@ __global__ __launch_bounds__(256) void conv_split_epi_kernel(const float* __rest
         const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
         float t = 0.f;
         for (int k = 0; k < 16; ++k) t += red[k][c][q];
-        if (cb + c < Cout) part[(size_t)tm * 2 * Cout + q * Cout + cb + c] = t;
+        if (cb + c < Cout)
+            __hip_atomic_store(part + (size_t)tm * 2 * Cout + q * Cout + cb + c, t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (fin.cnt != nullptr) stats_arrive(part, Cout, tm, cb, 64, blockIdx.y, fin);
 }
 
 // stats[c] += sum over the ntm partial rows of part[r][c], c < 2*Cout, in a FIXED order: the
@@ -639,6 +727,34 @@ __global__ __launch_bounds__(256) void krsc_to_kcrs_add_kernel(const float* __re
     }
 }
 
+// TDL_CONV_FIN_FUSED=0: statistics finalize as its own launch (stats_finalize_kernel; A/B switch)
+bool conv_fin_fused_on() {
+    static const bool v = [] {
+        const char* e = getenv("TDL_CONV_FIN_FUSED");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    return v;
+}
+
+// Arrival counters of the in-kernel statistics finalize (FinArgs), one zeroed block per stream
+// (calls on one stream are ordered; every counter is reset to zero by the workgroup that consumes it).
+constexpr int CNT_MAX = 8192;
+unsigned* stream_counters(hipStream_t s) {
+    static std::mutex mu;
+    static std::unordered_map<uint64_t, unsigned*> blocks;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const uint64_t key = (uint64_t)(uintptr_t)s ^ ((uint64_t)dev << 56);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = blocks.find(key);
+    if (it != blocks.end()) return it->second;
+    unsigned* p = nullptr;
+    if (hipMalloc(&p, CNT_MAX * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, CNT_MAX * sizeof(unsigned), s) != hipSuccess) return nullptr;
+    blocks[key] = p;
+    return p;
+}
+
 // TDL_CONV_SPLIT=0: no split-K for convolutions whose grid leaves the chip short (A/B switch)
 bool conv_split_on() {
     static const bool v = [] {
@@ -719,6 +835,27 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
     if (st && (2 * Cout + 63) / 64 > FIN_CNT) return (int)hipErrorInvalidValue;
     // a stride-2 data gradient runs as its 4 output-parity classes (ConvCls), the rest as one class
     const int cs = (transposed && stride == 2 && conv_parity_on()) ? 2 : 1;
+    const int Kall = R * S * Cin;
+    const int split = (!(transposed && stride == 2) && stats_ws != nullptr) ? conv_split_of(M, Cout, Kall) : 1;
+    // statistics finalized inside the producing kernels (FinArgs) when the counters fit
+    FinArgs fin{};
+    if (st && conv_fin_fused_on()) {
+        int total = 0;
+        for (int h0 = 0; h0 < cs; ++h0)
+            for (int w0 = 0; w0 < cs; ++w0) {
+                const int ps = (P - h0 + cs - 1) / cs, qs = (Q - w0 + cs - 1) / cs;
+                if (ps > 0 && qs > 0) total += (N * ps * qs + BM - 1) / BM;
+            }
+        const int ntiles = split > 1 ? (Cout + 63) / 64 : (Cout + (big ? 127 : 63)) / (big ? 128 : 64);
+        const int gs = max(4, (int)ceilf(sqrtf((float)total)));
+        const int ngroups = (total + gs - 1) / gs;
+        unsigned* sc = ntiles * (ngroups + 1) <= CNT_MAX ? stream_counters(s) : nullptr;
+        if (sc != nullptr) {
+            fin = FinArgs{sc, gs, ngroups, total, stats_accumulate ? 1 : 0, stats, acc_lo, acc_hi};
+            zs = nullptr;   // the last workgroup stores the totals (=, or += when accumulating)
+            cnt = nullptr;
+        }
+    }
     int rows = 0;
     for (int h0 = 0; h0 < cs; ++h0)
         for (int w0 = 0; w0 < cs; ++w0) {
@@ -735,21 +872,22 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
             const int ntm = (N * cl.Ps * cl.Qs + BM - 1) / BM;
             rows += ntm;
             const int nblk0 = ntm * ((Cout + (big ? 127 : 63)) / (big ? 128 : 64));
-            // split-K (one-class GEMMs, workspace given): slices after the statistics area
-            const int K = R * S * Cin, nk = (K + BK - 1) / BK;
-            // (never for a stride-2 data gradient, parity classes or not: tdl_conv_ws_floats(parity = 1)
-            // sized the caller's workspace without slices)
-            const int split = (!(transposed && stride == 2) && stats_ws != nullptr) ? conv_split_of(M, Cout, K) : 1;
+            // split-K (one-class GEMMs, workspace given): slices after the statistics area (never for a
+            // stride-2 data gradient, parity classes or not: tdl_conv_ws_floats(parity = 1) sized the
+            // caller's workspace without slices)
+            const int nk = (Kall + BK - 1) / BK;
             const int kps = (nk + split - 1) / split;
+            const FinArgs fin_nt = split > 1 ? FinArgs{} : fin;   // split: the epilogue kernel finalizes
             float* sws = split > 1 ? stats_ws + tdl_conv_stats_ws_floats(M, Cout) : nullptr;
             const dim3 nblk(nblk0, split);
             // a class with no taps (1x1 stride 2: three of four) runs an empty K loop and stores zeros
 #define LAUNCH(BCO, TR, ST) conv_nt_kernel<BCO, TR, ST><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, nullptr, nullptr, \
-                                                                             zs, cnt, sws, kps)
+                                                                             zs, cnt, sws, kps, fin_nt)
 #define LAUNCHP(BCO, ST) conv_nt_kernel<BCO, false, ST, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, nullptr, \
-                                                                                  zs, cnt, sws, kps)
+                                                                                  zs, cnt, sws, kps, fin_nt)
 #define LAUNCHB(BCO) conv_nt_kernel<BCO, true, true, false, true><<<nblk, 256, 0, s>>>(A, W, O, stats_ws, d, cl, pro, \
-                                                                                    (const bf16_t*)bnb_x, nullptr, cnt, sws, kps)
+                                                                                    (const bf16_t*)bnb_x, nullptr, cnt, sws, kps, \
+                                                                                    fin_nt)
     if (bnb) {
         if (big) LAUNCHB(128);
         else LAUNCHB(64);
@@ -770,16 +908,16 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
                 const dim3 ge(ntm, (Cout + 63) / 64);
                 if (bnb)
                     conv_split_epi_kernel<true, true><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, stats_ws,
-                                                                         (const bf16_t*)bnb_x, pro);
+                                                                         (const bf16_t*)bnb_x, pro, fin);
                 else if (st)
                     conv_split_epi_kernel<true, false><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, stats_ws, nullptr,
-                                                                          nullptr);
+                                                                          nullptr, fin);
                 else
                     conv_split_epi_kernel<false, false><<<ge, 256, 0, s>>>(sws, split, M, Cout, O, nullptr, nullptr,
-                                                                           nullptr);
+                                                                           nullptr, FinArgs{});
             }
         }
-    if (st) {
+    if (st && fin.cnt == nullptr) {
         const int rpb = 64;
         const dim3 g((2 * Cout + 63) / 64, (rows + rpb - 1) / rpb);
         stats_finalize_kernel<<<g, 256, 0, s>>>(stats_ws, rows, 2 * Cout, rpb, stats, cnt, acc_lo, acc_hi);
