@@ -373,3 +373,21 @@ def test_resnet50_backward_audit_clean_on_gpu():
                         "target": torch.randint(0, 1000, (32,), generator=g)})
     eng.flush()
     assert eng.attack_history == []
+
+
+def test_batched_weight_layouts_match_permutes():
+    """prebuild_layouts (one LDS-tiled launch for many weights, tiles spread by size) writes the same
+    [Cout][R][S][Cp] / [Cp][R][S][Cout] images as the per-weight path, padded channels zero."""
+    from trustworthy_dl.ops.conv import _weight_layout, prebuild_layouts
+    from trustworthy_dl.ops import layers
+    shapes = [(64, 3, 7, 7), (512, 512, 3, 3), (40, 24, 3, 3), (2048, 512, 1, 1), (72, 200, 1, 1), (8, 8, 3, 3)]
+    ws = [torch.randn(s, device="cuda").to(torch.bfloat16) for s in shapes]
+    layers._WEIGHT_GEN[0] += 1
+    prebuild_layouts(ws)
+    for w in ws:
+        Cout, C, R, S = w.shape
+        cp = (C + 7) // 8 * 8
+        wp = torch.zeros((Cout, cp, R, S), dtype=w.dtype, device=w.device)
+        wp[:, :C] = w
+        assert torch.equal(_weight_layout(w, cp, "krsc"), wp.permute(0, 2, 3, 1).contiguous())
+        assert torch.equal(_weight_layout(w, cp, "crsk"), wp.permute(1, 2, 3, 0).contiguous())
