@@ -84,10 +84,22 @@ constexpr int BK = 64;   // k per step
 // rows into the group's first row, and the last group to finish adds the group totals in group
 // order into stats (and acc_lo / acc_hi, see stats_finalize_kernel).  cnt: per-stream arrival
 // counters, left at zero by the workgroups that consume them; tile t uses [t (ngroups + 1), ...).
+// Training-mode BatchNorm finalize of the convolution's output (the BN folded into the next
+// convolution, ops/conv.py): what bn.hip tdl_bn_finalize computes, done by the finishing workgroups
+// (mean / rstd, running statistics, pro = [gamma * rstd | beta - mean * gamma * rstd], zeroed
+// backward-sum row), so the next convolution follows without a finalize launch in between.
+struct BnFin {
+    const bf16_t *gamma, *beta;
+    float *save_mean, *save_rstd, *upd_mean, *upd_var, *pro, *zero_sums;
+    int64_t count;
+    float eps, momentum;
+};
+
 struct FinArgs {
     unsigned* cnt;      // null: partial rows only (stats_finalize_kernel runs after)
     int gs, ngroups, rows, accumulate;
     float *stats, *acc_lo, *acc_hi;
+    BnFin bn;           // bn.pro null: no BN finalize
 };
 
 // sum over q in [q0, q1) of p[q * step * ld], agent-scope loads, fixed order: 8 lanes of partial
@@ -140,14 +152,38 @@ __device__ __forceinline__ void stats_arrive(float* __restrict__ part, int Cout,
         if (last) __hip_atomic_store(cc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!last || !act) return;
-    const float a = sum_rows(part + col, 0, f.ngroups, f.gs, 2 * Cout);
-    const float v = f.accumulate ? f.stats[col] + a : a;
-    f.stats[col] = v;
-    if (f.acc_lo != nullptr) {
-        if (t < nc) f.acc_lo[ch] += v;
-        else f.acc_hi[ch] += v;
+    if (!last) return;
+    __shared__ float tot[256];   // this tile's column totals (2 nc <= 256) for the BN finalize
+    if (act) {
+        const float a = sum_rows(part + col, 0, f.ngroups, f.gs, 2 * Cout);
+        const float v = f.accumulate ? f.stats[col] + a : a;
+        f.stats[col] = v;
+        tot[t] = v;
+        if (f.acc_lo != nullptr) {
+            if (t < nc) f.acc_lo[ch] += v;
+            else f.acc_hi[ch] += v;
+        }
     }
+    if (f.bn.pro == nullptr) return;
+    __syncthreads();
+    if (t >= nc || ch >= Cout) return;
+    const BnFin& b = f.bn;
+    const float invM = 1.f / (float)b.count;
+    const float mean = tot[t] * invM;
+    const float var = fmaxf(tot[nc + t] * invM - mean * mean, 0.f);
+    const float rs = rsqrtf(var + b.eps);
+    b.save_mean[ch] = mean;
+    b.save_rstd[ch] = rs;
+    if (b.upd_mean != nullptr) {
+        const float unbiased = b.count > 1 ? var * (float)b.count / (float)(b.count - 1) : var;
+        b.upd_mean[ch] = (1.f - b.momentum) * b.upd_mean[ch] + b.momentum * mean;
+        b.upd_var[ch] = (1.f - b.momentum) * b.upd_var[ch] + b.momentum * unbiased;
+    }
+    const float sc = rs * bf2f(b.gamma[ch]);
+    b.pro[ch] = sc;
+    b.pro[Cout + ch] = bf2f(b.beta[ch]) - mean * sc;
+    b.zero_sums[ch] = 0.f;
+    b.zero_sums[Cout + ch] = 0.f;
 }
 
 // ============================================================================ conv_nt (fwd / dgrad)
@@ -727,6 +763,15 @@ __global__ __launch_bounds__(256) void krsc_to_kcrs_add_kernel(const float* __re
     }
 }
 
+// TDL_BN_IN_CONV=0: the folded BN's finalize as its own launch after the convolution (A/B switch)
+bool tdl_bn_in_conv_on() {
+    static const bool v = [] {
+        const char* e = getenv("TDL_BN_IN_CONV");
+        return e == nullptr || atoi(e) != 0;
+    }();
+    return v;
+}
+
 // TDL_CONV_FIN_FUSED=0: statistics finalize as its own launch (stats_finalize_kernel; A/B switch)
 bool conv_fin_fused_on() {
     static const bool v = [] {
@@ -818,7 +863,9 @@ TDL_API int64_t tdl_conv_ws_floats(int M, int Cout, int K, int parity) {
 static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
                         int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad, int transposed,
                         const float* pro, hipStream_t s, const void* bnb_x = nullptr, bool stats_accumulate = false,
-                        float* acc_lo = nullptr, float* acc_hi = nullptr) {
+                        float* acc_lo = nullptr, float* acc_hi = nullptr, const BnFin* bnfin = nullptr,
+                        int* bn_done = nullptr) {
+    if (bn_done != nullptr) *bn_done = 0;
     ConvDims d{N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad};
     const bool bnb = bnb_x != nullptr;
     if (!dims_ok(d) || (pro != nullptr && transposed && !bnb)) return (int)hipErrorInvalidValue;
@@ -851,7 +898,11 @@ static int conv_nt_impl(const void* act, const void* wk, void* out, float* stats
         const int ngroups = (total + gs - 1) / gs;
         unsigned* sc = ntiles * (ngroups + 1) <= CNT_MAX ? stream_counters(s) : nullptr;
         if (sc != nullptr) {
-            fin = FinArgs{sc, gs, ngroups, total, stats_accumulate ? 1 : 0, stats, acc_lo, acc_hi};
+            fin = FinArgs{sc, gs, ngroups, total, stats_accumulate ? 1 : 0, stats, acc_lo, acc_hi, BnFin{}};
+            if (bnfin != nullptr && bnfin->pro != nullptr && tdl_bn_in_conv_on()) {
+                fin.bn = *bnfin;
+                if (bn_done != nullptr) *bn_done = 1;
+            }
             zs = nullptr;   // the last workgroup stores the totals (=, or += when accumulating)
             cnt = nullptr;
         }
@@ -976,6 +1027,17 @@ TDL_API int tdl_conv_nt(const void* act, const void* wk, void* out, float* stats
                         hipStream_t s) {
     return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, transposed,
                         nullptr, s);
+}
+
+// Forward convolution with batch statistics whose BatchNorm (folded into the NEXT convolution) is
+// finalized by the same kernels (BnFin; pro = null for a plain convolution input).  *bn_done = 1
+// when it was; 0 -> the caller runs tdl_bn_finalize (statistics finalized by a separate launch).
+TDL_API int tdl_conv_fwd_bn(const void* act, const void* wk, void* out, float* stats, float* stats_ws, int N, int Hin,
+                            int Win, int Cin, int P, int Q, int Cout, int R, int S, int stride, int pad,
+                            const float* pro, const BnFin* bn, int* bn_done, hipStream_t s) {
+    if (stats == nullptr || bn == nullptr || bn_done == nullptr) return (int)hipErrorInvalidValue;
+    return conv_nt_impl(act, wk, out, stats, stats_ws, N, Hin, Win, Cin, P, Q, Cout, R, S, stride, pad, 0, pro, s,
+                        nullptr, false, nullptr, nullptr, bn, bn_done);
 }
 
 // Forward convolution of relu(BN(y)) without materialising it: act = the previous layer's pre-BN

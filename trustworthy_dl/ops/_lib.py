@@ -79,6 +79,14 @@ class LayoutBatch(ctypes.Structure):
                 ("RS", ctypes.c_int * 32), ("n", ctypes.c_int)]
 
 
+class BnFin(ctypes.Structure):
+    """csrc/conv.hip BnFin: a folded BatchNorm finalized by the producing convolution's kernels."""
+    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("save_mean", ctypes.c_void_p),
+                ("save_rstd", ctypes.c_void_p), ("upd_mean", ctypes.c_void_p), ("upd_var", ctypes.c_void_p),
+                ("pro", ctypes.c_void_p), ("zero_sums", ctypes.c_void_p), ("count", ctypes.c_int64),
+                ("eps", ctypes.c_float), ("momentum", ctypes.c_float)]
+
+
 # name -> argtypes (restype is int for all)
 _SIGNATURES = {
     # norm_act.hip
@@ -150,6 +158,7 @@ _SIGNATURES = {
     "tdl_conv_nt_pro": [_P] * 5 + [_I] * 11 + [_P, _P],
     "tdl_conv_wgrad_pro": [_P] * 4 + [_I] * 12 + [_P, _P],
     "tdl_conv_weight_layouts_batch": [LayoutBatch, _P],
+    "tdl_conv_fwd_bn": [_P] * 5 + [_I] * 11 + [_P, ctypes.POINTER(BnFin), ctypes.POINTER(ctypes.c_int), _P],
 }
 
 

@@ -51,6 +51,27 @@ def _conv_ws(M: int, Cout: int, K: int, parity: bool, dev) -> torch.Tensor:
     return torch.empty(int(_lib.lib().tdl_conv_ws_floats(M, Cout, K, int(parity))), dtype=torch.float32, device=dev)
 
 
+def _conv_fwd_bn(bnfin: dict, act, wk, out, stats, ws, dims, pro, dev) -> None:
+    """Forward convolution whose output's BatchNorm (``bnfin["bn"]``, folded into the next
+    convolution) is finalized by the convolution's own finishing workgroups (csrc/conv.hip BnFin):
+    fills bnfin with the BN's [scale | shift | mean | rstd] buffer, its zeroed backward-sum row and
+    ``done`` (False: the consumer runs tdl_bn_finalize itself)."""
+    import ctypes
+    bn = bnfin["bn"]
+    Cout, M = dims[6], dims[0] * dims[4] * dims[5]   # dims = (N, H, W, C, P, Q, Cout, R, S, stride, pad)
+    bnp = torch.empty(4 * Cout, dtype=torch.float32, device=dev)
+    sums = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(Cout)), dtype=torch.float32, device=dev)
+    upd = bn.running_mean is not None
+    b = _lib.BnFin(bn.weight.data_ptr(), bn.bias.data_ptr(), bnp[2 * Cout:].data_ptr(), bnp[3 * Cout:].data_ptr(),
+                   bn.running_mean.data_ptr() if upd else None, bn.running_var.data_ptr() if upd else None,
+                   bnp.data_ptr(), sums.data_ptr(), M, float(bn.eps),
+                   float(bn.momentum if bn.momentum is not None else 0.1))
+    done = ctypes.c_int(0)
+    _lib.call("tdl_conv_fwd_bn", ptr(act), ptr(wk), ptr(out), ptr(stats), ptr(ws), *dims, ptr(pro), ctypes.byref(b),
+              ctypes.byref(done), stream_ptr(dev))
+    bnfin.update(bnp=bnp, sums=sums, done=bool(done.value))
+
+
 def native_conv_ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype == torch.bfloat16
 
@@ -133,7 +154,7 @@ class _Conv2dNHWC(torch.autograd.Function):
     """y = conv2d(x, w) on NHWC bf16; also returns per-channel (sum, sumsq) of y when asked."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, want_stats: bool):
+    def forward(ctx, x, weight, stride: int, pad: int, want_stats: bool, bnfin=None):
         N, C, H, W = x.shape
         Cout, Cw, R, S = weight.shape
         if Cw != C or Cout % 8 != 0:
@@ -149,8 +170,11 @@ class _Conv2dNHWC(torch.autograd.Function):
         if want_stats:
             stats = torch.empty(2 * Cout, dtype=torch.float32, device=x.device)
         ws = _conv_ws(N * P * Q, Cout, R * S * cp, False, x.device)
-        _lib.call("tdl_conv_nt", ptr(xs), ptr(wk), ptr(y), ptr(stats), ptr(ws), N, H, W, cp, P, Q, Cout, R, S, stride,
-                  pad, 0, stream_ptr(x.device))
+        if want_stats and bnfin is not None:
+            _conv_fwd_bn(bnfin, xs, wk, y, stats, ws, (N, H, W, cp, P, Q, Cout, R, S, stride, pad), None, x.device)
+        else:
+            _lib.call("tdl_conv_nt", ptr(xs), ptr(wk), ptr(y), ptr(stats), ptr(ws), N, H, W, cp, P, Q, Cout, R, S,
+                      stride, pad, 0, stream_ptr(x.device))
         ctx.save_for_backward(xs, weight)
         ctx.geom = (N, C, cp, H, W, Cout, R, S, P, Q, stride, pad)
         # the statistics output never gets a gradient: without this autograd launches a zero fill
@@ -164,7 +188,7 @@ class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         xs, weight = ctx.saved_tensors
         N, C, cp, H, W, Cout, R, S, P, Q, stride, pad = ctx.geom
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -197,7 +221,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                     mg.add_(g)
                 else:
                     gw = g.to(weight.dtype)
-        return dx, gw, None, None, None
+        return dx, gw, None, None, None, None
 
 
 class _BatchNormActNHWC(torch.autograd.Function):
@@ -265,7 +289,7 @@ class _BNActConvNHWC(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, stats, gamma, beta, running_mean, running_var, momentum: float, eps: float, weight,
-                stride: int, pad: int, want_stats: bool):
+                stride: int, pad: int, want_stats: bool, pre=None, bnfin=None):
         N, C, H, W = y.shape
         Cout, Cw, R, S = weight.shape
         if Cw != C or C % 8 or Cout % 8:
@@ -274,13 +298,18 @@ class _BNActConvNHWC(torch.autograd.Function):
         ys = y.contiguous(memory_format=torch.channels_last)
         M = N * H * W
         # [scale | shift | mean | rstd] in one buffer: the backward's data-gradient epilogue reads all four
-        bnp = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        # pre: this BN already finalized by the producing convolution (_conv_fwd_bn)
+        if pre is not None and "bnp" in pre:
+            bnp, sums = pre["bnp"], pre["sums"]
+        else:
+            bnp = torch.empty(4 * C, dtype=torch.float32, device=dev)
+            sums = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(C)), dtype=torch.float32, device=dev)
         pro, mean, rstd = bnp[:2 * C], bnp[2 * C:3 * C], bnp[3 * C:]
-        sums = torch.empty(int(_lib.lib().tdl_bn_bwd_ws_floats(C)), dtype=torch.float32, device=dev)
         upd = running_mean is not None
-        _lib.call("tdl_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
-                  ptr(running_mean if upd else None), ptr(running_var if upd else None), ptr(pro), ptr(sums), M, C,
-                  float(eps), float(momentum), stream_ptr(dev))
+        if not (pre is not None and pre.get("done")):
+            _lib.call("tdl_bn_finalize", ptr(stats), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd),
+                      ptr(running_mean if upd else None), ptr(running_var if upd else None), ptr(pro), ptr(sums), M,
+                      C, float(eps), float(momentum), stream_ptr(dev))
         wk = _weight_layout(weight, C, "krsc")
         P, Q = _out_hw(H, W, R, S, stride, pad)
         out = torch.empty((N, Cout, P, Q), dtype=y.dtype, device=dev, memory_format=torch.channels_last)
@@ -288,8 +317,11 @@ class _BNActConvNHWC(torch.autograd.Function):
         if want_stats:
             st = torch.empty(2 * Cout, dtype=torch.float32, device=dev)
         ws = _conv_ws(N * P * Q, Cout, R * S * C, False, dev)
-        _lib.call("tdl_conv_nt_pro", ptr(ys), ptr(wk), ptr(out), ptr(st), ptr(ws), N, H, W, C, P, Q, Cout, R, S,
-                  stride, pad, ptr(pro), stream_ptr(dev))
+        if want_stats and bnfin is not None:
+            _conv_fwd_bn(bnfin, ys, wk, out, st, ws, (N, H, W, C, P, Q, Cout, R, S, stride, pad), pro, dev)
+        else:
+            _lib.call("tdl_conv_nt_pro", ptr(ys), ptr(wk), ptr(out), ptr(st), ptr(ws), N, H, W, C, P, Q, Cout, R, S,
+                      stride, pad, ptr(pro), stream_ptr(dev))
         ctx.save_for_backward(ys, bnp, gamma, weight)
         ctx.sums = sums
         ctx.beta = beta  # a parameter (leaf): only its identity / main_grad is needed
@@ -303,7 +335,7 @@ class _BNActConvNHWC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout, _dstats):
         if dout is None:
-            return (None,) * 12
+            return (None,) * 14
         ys, bnp, gamma, weight = ctx.saved_tensors
         C_ = ys.shape[1]
         pro, mean, rstd = bnp[:2 * C_], bnp[2 * C_:3 * C_], bnp[3 * C_:]
@@ -351,7 +383,7 @@ class _BNActConvNHWC(torch.autograd.Function):
                   ptr(ctx.sums), ptr(dy), N * H * W, C, stream_ptr(dev))
         gg = None if mg_g is not None else dg.to(gamma.dtype)
         gb = None if mg_b is not None else db.to(beta.dtype)
-        return dy, None, gg, gb, None, None, None, None, gw, None, None, None
+        return dy, None, gg, gb, None, None, None, None, gw, None, None, None, None, None
 
 
 def _bn_fold_enabled() -> bool:
@@ -372,14 +404,17 @@ def conv_bn_chain(x: torch.Tensor, units, relu: bool = True, residual: Optional[
     conv0, _ = units[0]
     if conv0.bias is not None:
         raise NotImplementedError("native conv: bias")
-    y, stats = _Conv2dNHWC.apply(x, conv0.weight, _single(conv0.stride), _single(conv0.padding), True)
-    for (_, bn), (conv, _) in zip(units[:-1], units[1:]):
+    # each folded BN is finalized by the kernels of the convolution producing its input
+    fins = [{"bn": bn} for _, bn in units[:-1]] + [None]
+    y, stats = _Conv2dNHWC.apply(x, conv0.weight, _single(conv0.stride), _single(conv0.padding), True, fins[0])
+    for i, ((_, bn), (conv, _)) in enumerate(zip(units[:-1], units[1:])):
         if conv.groups != 1 or _single(conv.dilation) != 1 or conv.bias is not None \
                 or conv.kernel_size[0] != conv.kernel_size[1]:
             raise NotImplementedError(f"native conv: unsupported configuration {conv}")
         momentum = bn.momentum if bn.momentum is not None else 0.1
         y, stats = _BNActConvNHWC.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, momentum, bn.eps,
-                                        conv.weight, _single(conv.stride), _single(conv.padding), True)
+                                        conv.weight, _single(conv.stride), _single(conv.padding), True, fins[i],
+                                        fins[i + 1])
     bn = units[-1][1]
     momentum = bn.momentum if bn.momentum is not None else 0.1
     return _BatchNormActNHWC.apply(y, stats, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, True,
