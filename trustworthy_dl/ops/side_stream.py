@@ -49,6 +49,21 @@ class WgradSide:
             torch.autograd.Variable._execution_engine.queue_callback(_join)
 
     @classmethod
+    def join_all(cls):
+        """Make each device's current stream wait for its side stream and clear the pending flags:
+        called by the engine at every step start, so a backward that raised after a side-stream
+        launch (its final callback never ran) cannot leave the next step's consumers unordered
+        (ADVICE r4)."""
+        for idx, side in cls.streams.items():
+            if cls.pending.get(idx):
+                torch.cuda.current_stream(torch.device("cuda", idx)).wait_stream(side)
+                cls.pending[idx] = False
+
+    @classmethod
+    def count(cls) -> int:
+        return len(cls.streams)
+
+    @classmethod
     def wait(cls, stream: torch.cuda.Stream, dev: torch.device):
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
         if cls.pending.get(idx):

@@ -57,6 +57,13 @@ class Stage:
             self._hooks.append(p.register_post_accumulate_grad_hook(self._fold_grad))
         vk = dict(verifier_kwargs or {})
         self.verifier = StageVerifier(self.flat.sizes, self.device, **vk)
+        self.clip_excluded: List[Tuple[int, int]] = []
+        # weight-integrity checksums (parallel/attribution.py): post-update commitment, the checksum
+        # of the weights in use this step, one taken early on the side stream, the tail re-check
+        self.param_checksum: Optional[torch.Tensor] = None
+        self._cur_checksum: Optional[torch.Tensor] = None
+        self._early_checksum: Optional[torch.Tensor] = None
+        self._tail_flag: Optional[torch.Tensor] = None
 
     def set_clip_exclusions(self, excluded_ids) -> None:
         """Parameters whose gradient another stage already counts in the global clipping norm (the
@@ -72,7 +79,7 @@ class Stage:
         """Sum of squares of ``grad`` (this stage's flat gradient) over the parameters this stage
         counts for clipping (device scalar)."""
         sq = (grad * grad).sum()
-        for o, n in getattr(self, "clip_excluded", []):
+        for o, n in self.clip_excluded:
             g = grad[o:o + n]
             sq = sq - (g * g).sum()
         return sq

@@ -88,6 +88,7 @@ def save_checkpoint(trainer, path: Optional[str] = None) -> str:
             ck["shards"] = [os.path.basename(path.replace(".pt", f".rank{r}.pt")) for r in range(e.world)]
             _atomic_save(ck, path)
         dist.barrier()
+    e.note_checkpoint(path, e.global_step)
     logger.info("Checkpoint saved: %s", path)
     return path
 
@@ -292,6 +293,7 @@ def load_checkpoint(trainer, path: str):
     if "detector" in ck:
         trainer.attack_detector.load_state_dict(ck["detector"])
     trainer.config.num_nodes = e.num_nodes
+    e.note_checkpoint(path, e.global_step)
     logger.info("Checkpoint loaded: %s (step %d, plan %s)", path, e.global_step, e.plan.describe())
 
 
