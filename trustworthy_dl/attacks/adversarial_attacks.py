@@ -26,6 +26,13 @@ weight-gradient contributions (sign-flipped / scaled / zeroed / noised as ``grad
 instead of on the step's accumulated gradient — the one-of-M adversary that a one-micro-batch
 audit catches with probability k / M per step.  ``lie_integrity``: the target's engine reports a
 passing weight-integrity check whatever it measured (a rank that lies about its own checksum).
+
+``adaptive`` (gradient poisoning): the attacker knows everything public about the audit — the job
+seed, the step, the stage's layer range, hence r4's public gradient sketch (its sampled window
+offset and sign vectors; the engine hands it over as ``public_sketch_fn``) — and confines its
+tamper to the coordinates that sketch does not sample, so the sketch of the tampered gradient
+equals the clean one bit for bit.  r4's commitments passed it; the commit-then-reveal check
+(exact hashes + keyed sketches under a key revealed after the commitment) catches it.
 """
 from __future__ import annotations
 
@@ -64,6 +71,7 @@ class AttackConfig:
     label_flip_fraction: Optional[float] = None  # default intensity
     micro_batches: Optional[int] = None  # tamper only this many of the step's micro-batches (None: all)
     lie_integrity: bool = False          # the target reports its weight-integrity check as passing
+    adaptive: bool = False               # gradient tampers avoid everything the public sketch samples
     seed: int = 1234
 
     def grad_factor(self) -> float:
@@ -84,6 +92,9 @@ class AdversarialAttacker:
         self.first_attack_step: Dict[int, int] = {}
         self.first_detect_step: Dict[int, int] = {}
         self.last_batch_truth: Dict[int, bool] = {}
+        # set by the engine: node -> (public GradSketch, its per-step window offset) — public data
+        self.public_sketch_fn = None
+        self._gsnap = None
 
     # ---------------------------------------------------------------- activation
     def activate_attacks(self):
@@ -145,12 +156,28 @@ class AdversarialAttacker:
             a = float(c.intensity * 10.0 * g.float().pow(2).mean().sqrt().item() + 1e-12)
         return mode, a
 
+    def _hide(self, node: int, delta: torch.Tensor) -> torch.Tensor:
+        """``adaptive``: zero the tamper on every coordinate the public sketch reads (its sampled
+        window in each block), so that sketch cannot see it at all."""
+        if not self.config.adaptive or self.public_sketch_fn is None:
+            return delta
+        sk, off = self.public_sketch_fn(node)
+        if sk is not None and sk.nblk > 0:
+            delta[: sk.nblk * sk.block].view(sk.nblk, sk.block)[:, off:off + sk.win] = 0.0
+        return delta
+
     def on_gradients(self, node: int, flat_grad: torch.Tensor, step: int) -> bool:
         if self.per_micro_gradients() or not self._fires("gradient_poisoning", node, step):
             return False
         mode, a = self._grad_magnitude(flat_grad)
-        inject_(flat_grad, mode, a, self._seed(node, step), 0)
-        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a)
+        if self.config.adaptive:
+            t = flat_grad.detach().clone()
+            inject_(t, mode, a, self._seed(node, step), 0)
+            flat_grad.add_(self._hide(node, t - flat_grad))
+        else:
+            inject_(flat_grad, mode, a, self._seed(node, step), 0)
+        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a,
+                  adaptive=self.config.adaptive)
         return True
 
     # gradient poisoning inside the backward (``micro_batches`` set): the engine calls
@@ -161,16 +188,18 @@ class AdversarialAttacker:
             self._gsnap = (node, step, micro, flat_grad.detach().clone())
 
     def after_micro_backward(self, node: int, flat_grad: torch.Tensor, step: int, micro: int, num_micro: int) -> bool:
-        snap = getattr(self, "_gsnap", None)
+        snap = self._gsnap
         if snap is None or snap[:3] != (node, step, micro):
             return False
         self._gsnap = None
         before = snap[3]
         d = flat_grad - before
         mode, a = self._grad_magnitude(d)
-        inject_(d, mode, a, self._seed(node, step) + micro, 0)
-        flat_grad.copy_(before + d)
-        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a, micro=micro)
+        t = d.clone()
+        inject_(t, mode, a, self._seed(node, step) + micro, 0)
+        flat_grad.copy_(before + d + self._hide(node, t - d) if self.config.adaptive else before + t)
+        self._log("gradient_poisoning", node, step, mode=self.config.gradient_mode, magnitude=a, micro=micro,
+                  adaptive=self.config.adaptive)
         return True
 
     def on_input_grad(self, node: int, dx: torch.Tensor, step: int, micro: Optional[int] = None,
