@@ -130,6 +130,10 @@ __device__ __forceinline__ void stats_arrive(float* __restrict__ part, int Cout,
     const int g = row / f.gs, r0 = g * f.gs, r1 = min(f.rows, r0 + f.gs);
     unsigned* gc = f.cnt + (size_t)tile * (f.ngroups + 1) + g;
     unsigned* cc = f.cnt + (size_t)tile * (f.ngroups + 1) + f.ngroups;
+    // hand-off form (MI355X_MICROARCH.md, "Hand-offs measured with sc1 loads", row 1): every storing
+    // wave drained its sc1 (agent-scope) stores, a workgroup barrier, ONE lane's agent-scope add;
+    // the workgroup whose add came last reads the rows with sc1 loads after a barrier: no acquire
+    // fence needed (and none of its ~1.7 us per workgroup)
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = prev == (unsigned)(r1 - r0 - 1);
@@ -787,15 +791,25 @@ constexpr int CNT_MAX = 8192;
 unsigned* stream_counters(hipStream_t s) {
     static std::mutex mu;
     static std::unordered_map<uint64_t, unsigned*> blocks;
+    // the counters live on the STREAM's device (local mode runs stages on several GPUs from one
+    // thread whose current device need not be the stream's: ADVICE r4)
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) return nullptr;
     const uint64_t key = (uint64_t)(uintptr_t)s ^ ((uint64_t)dev << 56);
     std::lock_guard<std::mutex> lock(mu);
     auto it = blocks.find(key);
     if (it != blocks.end()) return it->second;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
     unsigned* p = nullptr;
-    if (hipMalloc(&p, CNT_MAX * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, CNT_MAX * sizeof(unsigned), s) != hipSuccess) return nullptr;
+    bool ok = hipMalloc(&p, CNT_MAX * sizeof(unsigned)) == hipSuccess;
+    if (ok && hipMemsetAsync(p, 0, CNT_MAX * sizeof(unsigned), s) != hipSuccess) {
+        (void)hipFree(p);
+        ok = false;
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) return nullptr;
     blocks[key] = p;
     return p;
 }
