@@ -38,6 +38,7 @@
 //   6 F32ATOM   atomicAdd(C32[m][n], acc)                  (split-K straight into main_grad)
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -70,7 +71,34 @@ struct GemmParams {
     long long split_stride;  // EPI_F32: elements between split slabs
     int tiles_n, tiles;
     int splits;
+    int group_m;          // tile order: 0 = row-major over (tm, tn); G > 0 = groups of G tile rows, tn-major
+    unsigned long long* ts;  // diagnostics (tdl_gemm_set_timestamps): per-workgroup s_memrealtime stamps
 };
+
+// timestamp slot `k` of this workgroup (wave 0, lane 0; 64 slots per workgroup)
+__device__ __forceinline__ void stamp(const GemmParams& p, int k) {
+    if (p.ts != nullptr && threadIdx.x == 0 && k < 64)
+        p.ts[(size_t)(blockIdx.x + gridDim.x * blockIdx.y) * 64 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// tile index (after the XCD remap) -> (tm, tn).  Grouped order (G tile rows per group, the tile
+// column advancing slowest inside a group): the CUs of one XCD that run concurrently then share a
+// G x (32 / G) block of A / B panels instead of ~3 A panels x every B panel (L2 reuse).
+__device__ __forceinline__ void tile_coords(const GemmParams& p, int wg, int& tm, int& tn) {
+    const int G = p.group_m;
+    if (G <= 0) {
+        tm = wg / p.tiles_n;
+        tn = wg - tm * p.tiles_n;
+        return;
+    }
+    const int tiles_m = p.tiles / p.tiles_n;
+    const int per = G * p.tiles_n;
+    const int grp = wg / per, in = wg - grp * per;
+    const int first = grp * G;
+    const int gs = tiles_m - first < G ? tiles_m - first : G;
+    tn = in / gs;
+    tm = first + (in - tn * gs);
+}
 
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
@@ -396,6 +424,129 @@ __device__ __forceinline__ void wait_vmc() {
 // XOR-swizzled by row) and reads it back row-contiguous, so every store instruction writes 8 whole
 // 128-B row segments (1 KiB) instead of 16 rows x 32 B: a quarter of the store instructions and
 // L2 requests of the direct MFMA-layout store.
+// LDS-staged epilogue of the 8-wave ping-pong kernel (EPI_BF16 / GELU / RESADD / DGELU):
+// each wave writes its 128 x 64 bf16 block into its own 16 KiB of the (then idle) operand LDS
+// (16-B chunks XOR-swizzled by row) and reads it back row-contiguous, so every store instruction
+// writes 8 whole 128-B row segments (1 KiB) instead of 16 rows x 32 B: a quarter of the store
+// instructions and L2 requests of the direct MFMA-layout store.  RESADD / DGELU bring their
+// operand tile (residual C / pre-activation aux) in the same way reversed.
+template <int EPI>
+__device__ __forceinline__ void pp_lds_epilogue(const GemmParams& p, f32x4 (&acc)[8][4], char* smem, int m0, int n0,
+                                                int wr, int wc, int w, int lane) {
+    char* ws = smem + w * 16384;
+    const int g = lane >> 4, rl = lane & 15;
+    const int mw = m0 + wr * 128, nw = n0 + wc * 64;
+    const long long rem = (long long)(p.M - mw) * p.ldc * 2;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const bf16_t*)p.C + (size_t)mw * p.ldc, rem);
+    const __amdgpu_buffer_rsrc_t rx =
+        EPI == EPI_GELU || EPI == EPI_DGELU ? make_rsrc(p.aux + (size_t)mw * p.ldc, rem) : rc;
+    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
+    float bv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int n = nw + 16 * j + 4 * g;
+        const u32x2_t b = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
+        unpack4(make_uint2(b.x, b.y), bv[j]);
+    }
+    // read-back: lane -> row 8 q + (lane >> 3), 16-B chunk lane & 7 (columns nw + 8 c ..+7)
+    const int cb = lane & 7;
+    const uint32_t coff = nw + 8 * cb < p.N ? (uint32_t)(nw + 8 * cb) * 2u : 0x80000000u;
+    auto pass = [&](bool post, __amdgpu_buffer_rsrc_t dst) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = acc[i][j][r] + bv[j][r];
+                    if (post) v[r] = gelu_tanh(v[r]);
+                }
+                const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
+                *(uint2*)(ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3)) = pack4(v);
+            }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
+            const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, dst, off, 0, 0);
+        }
+    };
+    if constexpr (EPI == EPI_RESADD || EPI == EPI_DGELU) {
+        // the operand tile (residual C / pre-activation aux) comes in the same way reversed:
+        // row-contiguous 16-B loads -> swizzled LDS -> each lane's MFMA-layout 4-vectors, which
+        // the lane combines with its accumulators in fp32 and writes back to the same 8 bytes
+        const __amdgpu_buffer_rsrc_t rs = EPI == EPI_RESADD ? rc : rx;
+        uint4 ld[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            ld[q] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            *(uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4)) = ld[q];
+        }
+        float csum[4][4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
+                char* a8 = ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3);
+                float o[4], v[4];
+                unpack4(*(const uint2*)a8, o);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if constexpr (EPI == EPI_RESADD) {
+                        v[r] = acc[i][j][r] + bv[j][r] + o[r];
+                    } else {
+                        v[r] = acc[i][j][r] * gelu_tanh_grad(o[r]);
+                        csum[j][r] = (i == 0 ? 0.f : csum[j][r]) + v[r];
+                    }
+                }
+                *(uint2*)a8 = pack4(v);
+            }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
+            const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, rc, off, 0, 0);
+        }
+        if constexpr (EPI == EPI_DGELU) {
+            if (p.colsum != nullptr) {  // rows past M / columns past N had zero operands
+                const __amdgpu_buffer_rsrc_t rsum = make_rsrc(p.colsum, (long long)p.N * 4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        float t = csum[j][r];
+                        t += __shfl_xor(t, 1, 64);
+                        t += __shfl_xor(t, 2, 64);
+                        t += __shfl_xor(t, 4, 64);
+                        t += __shfl_xor(t, 8, 64);
+                        csum[j][r] = t;
+                    }
+                    const int n = nw + 16 * j + 4 * g, r = lane & 3;
+                    const float t = r == 0 ? csum[j][0] : r == 1 ? csum[j][1] : r == 2 ? csum[j][2] : csum[j][3];
+                    const bool writer = (lane & 15) < 4 && n + r < p.N;
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(t, rsum, writer ? (uint32_t)(n + r) * 4u : 0x80000000u, 0, 0);
+                }
+            }
+        }
+    } else if constexpr (EPI == EPI_GELU) {
+        pass(false, rx);  // the pre-activation
+        pass(true, rc);
+    } else {
+        pass(false, rc);
+    }
+}
+
 template <bool TA, bool TB, int EPI, bool LEPI = false>
 __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     static_assert(!LEPI || EPI <= EPI_DGELU, "LDS epilogue: bf16 outputs");
@@ -406,14 +557,16 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     const int wr = w >> 2, wc = w & 3;
     auto coords = [&](int item, int& mm, int& nn) {
         const int wg = xcd_remap(item, p.tiles);
-        const int tm = wg / p.tiles_n;
+        int tm, tn;
+        tile_coords(p, wg, tm, tn);
         mm = tm * BM;
-        nn = (wg - tm * p.tiles_n) * BN;
+        nn = tn * BN;
     };
     int m0, n0;
     coords(blockIdx.x, m0, n0);
     const int kbeg = blockIdx.y * p.k_per_split;
     const int nk = p.k_per_split / BK;  // >= 2 (host)
+    stamp(p, 0);
 
     // Per-lane byte offsets of piece 0 of each unit (piece 1 adds the uniform di_a / di_b).
     //  k-contiguous operand: unit image [128 unit-rows][64 k], 128-B rows, 16-B chunk c of row r at
@@ -589,123 +742,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
         for (; t < nk - 2; ++t) step(t, I15{}, I15{});
         step(t, I15{}, I3{});
         step(t + 1, I3{}, I0{});
+        stamp(p, 1);
         // group 0's extra barrier first: past it every wave has retired its last fragment reads and
         // waited its last copies (vmcnt(0) in the final phase), so the operand LDS is free
         if (!wr) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");  // no LDS access of the epilogue moves above that barrier
         __builtin_amdgcn_sched_barrier(0);
-        char* ws = smem + w * 16384;
-        const int g = lane >> 4, rl = lane & 15;
-        const int mw = m0 + wr * 128, nw = n0 + wc * 64;
-        const long long rem = (long long)(p.M - mw) * p.ldc * 2;
-        const __amdgpu_buffer_rsrc_t rc = make_rsrc((const bf16_t*)p.C + (size_t)mw * p.ldc, rem);
-        const __amdgpu_buffer_rsrc_t rx =
-            EPI == EPI_GELU || EPI == EPI_DGELU ? make_rsrc(p.aux + (size_t)mw * p.ldc, rem) : rc;
-        const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
-        float bv[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int n = nw + 16 * j + 4 * g;
-            const u32x2_t b = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
-            unpack4(make_uint2(b.x, b.y), bv[j]);
-        }
-        // read-back: lane -> row 8 q + (lane >> 3), 16-B chunk lane & 7 (columns nw + 8 c ..+7)
-        const int cb = lane & 7;
-        const uint32_t coff = nw + 8 * cb < p.N ? (uint32_t)(nw + 8 * cb) * 2u : 0x80000000u;
-        auto pass = [&](bool post, __amdgpu_buffer_rsrc_t dst) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float v[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        v[r] = acc[i][j][r] + bv[j][r];
-                        if (post) v[r] = gelu_tanh(v[r]);
-                    }
-                    const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
-                    *(uint2*)(ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3)) = pack4(v);
-                }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int row = 8 * q + (lane >> 3);
-                const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
-                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, dst, off, 0, 0);
-            }
-        };
-        if constexpr (EPI == EPI_RESADD || EPI == EPI_DGELU) {
-            // the operand tile (residual C / pre-activation aux) comes in the same way reversed:
-            // row-contiguous 16-B loads -> swizzled LDS -> each lane's MFMA-layout 4-vectors, which
-            // the lane combines with its accumulators in fp32 and writes back to the same 8 bytes
-            const __amdgpu_buffer_rsrc_t rs = EPI == EPI_RESADD ? rc : rx;
-            uint4 ld[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int row = 8 * q + (lane >> 3);
-                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
-                const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-                ld[q] = make_uint4(v[0], v[1], v[2], v[3]);
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int row = 8 * q + (lane >> 3);
-                *(uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4)) = ld[q];
-            }
-            float csum[4][4];
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int row = 16 * i + rl, ch = 2 * j + (g >> 1);
-                    char* a8 = ws + row * 128 + ((ch ^ (row & 7)) << 4) + ((g & 1) << 3);
-                    float o[4], v[4];
-                    unpack4(*(const uint2*)a8, o);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        if constexpr (EPI == EPI_RESADD) {
-                            v[r] = acc[i][j][r] + bv[j][r] + o[r];
-                        } else {
-                            v[r] = acc[i][j][r] * gelu_tanh_grad(o[r]);
-                            csum[j][r] = (i == 0 ? 0.f : csum[j][r]) + v[r];
-                        }
-                    }
-                    *(uint2*)a8 = pack4(v);
-                }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int row = 8 * q + (lane >> 3);
-                const uint4 val = *(const uint4*)(ws + row * 128 + ((cb ^ (row & 7)) << 4));
-                const uint32_t off = coff == 0x80000000u ? coff : (uint32_t)row * (uint32_t)p.ldc * 2u + coff;
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{val.x, val.y, val.z, val.w}, rc, off, 0, 0);
-            }
-            if constexpr (EPI == EPI_DGELU) {
-                if (p.colsum != nullptr) {  // rows past M / columns past N had zero operands
-                    const __amdgpu_buffer_rsrc_t rsum = make_rsrc(p.colsum, (long long)p.N * 4);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            float t = csum[j][r];
-                            t += __shfl_xor(t, 1, 64);
-                            t += __shfl_xor(t, 2, 64);
-                            t += __shfl_xor(t, 4, 64);
-                            t += __shfl_xor(t, 8, 64);
-                            csum[j][r] = t;
-                        }
-                        const int n = nw + 16 * j + 4 * g, r = lane & 3;
-                        const float t = r == 0 ? csum[j][0] : r == 1 ? csum[j][1] : r == 2 ? csum[j][2] : csum[j][3];
-                        const bool writer = (lane & 15) < 4 && n + r < p.N;
-                        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(t, rsum, writer ? (uint32_t)(n + r) * 4u : 0x80000000u, 0, 0);
-                    }
-                }
-            }
-        } else if constexpr (EPI == EPI_GELU) {
-            pass(false, rx);  // the pre-activation
-            pass(true, rc);
-        } else {
-            pass(false, rc);
-        }
+        pp_lds_epilogue<EPI>(p, acc, smem, m0, n0, wr, wc, w, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        stamp(p, 2);
         return;
     } else {
         int t = 0;
@@ -717,6 +762,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pp(GemmParams p) {
     }
     if (!wr) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
 }
+
 
 template <int N, int I = 0, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -880,9 +926,10 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
         const int item = lb + i * G;
         sp = item / p.tiles;
         const int tile = item - sp * p.tiles;
-        const int tm = tile / p.tiles_n;
+        int tm, tn;
+        tile_coords(p, tile, tm, tn);
         m0 = tm * BM;
-        n0 = (tile - tm * p.tiles_n) * BN;
+        n0 = tn * BN;
     };
 
     // ---- producer: the (item, k step) it loads next; after the last step it repeats that step
@@ -953,6 +1000,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
 
     PFrags F;
     Acc acc;
+    stamp(p, 0);
     {   // prologue: step 0 -> LDS buffer 0, step 1 -> R, F = step 0's k-half 0
         produce_rsrc();
         static_for<16>(load_piece);
@@ -1023,6 +1071,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
 #pragma clang loop unroll(disable)
         for (int ct = 1; ct < nk - 1; ++ct) kstep(std::false_type{}, std::false_type{});
         kstep(std::false_type{}, std::true_type{});  // nk >= 2 (host)
+        stamp(p, 1 + 2 * ci);
         // ---- epilogue: the last MFMAs' results must be written before the accumulator reads.
         // Inline-asm MFMAs are opaque to the hazard recognizer, and hipcc copied finished
         // accumulators to VGPRs right behind their last MFMA (stale values): after the nop sled,
@@ -1045,6 +1094,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
             epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         }
         __builtin_amdgcn_sched_barrier(0);
+        stamp(p, 2 + 2 * ci);
         read_half0(s & 1);  // the next tile's first k-half (step s, staged in buffer s & 1)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1058,6 +1108,12 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
 // 6 (atomics); the split is reduced until it divides K / 64 (every slice the same depth).
 // `kernel` (epi bits 8..15): 0 = the persistent 4-wave kernel (gemm_p4), 1 = the staggered
 // ping-pong kernel (gemm_pp; LDS-staged row-contiguous epilogue on NT operands with bf16 outputs).
+static unsigned long long* g_gemm_ts = nullptr;   // diagnostics: stamps of every GEMM launch
+TDL_API int tdl_gemm_set_timestamps(void* buf) {
+    g_gemm_ts = (unsigned long long*)buf;
+    return 0;
+}
+
 static int num_cus() {
     static int n = 0;
     if (n == 0) {
@@ -1086,7 +1142,15 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     if (split > 1 && epi != EPI_F32 && epi != EPI_F32ATOM) return (int)hipErrorInvalidValue;
     const int kps = K / split;
     GemmParams p{(const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (bf16_t*)aux, colsum, M, N, K,
-                 lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split};
+                 lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split, 0, g_gemm_ts};
+    {
+        // tile order: groups of 8 tile rows for the wide (N >= 4096) products, where the 32 CUs of
+        // an XCD then share an 8 x 4 block of A / B panels (fc forward +7-8 %, interleaved A/B,
+        // profiles/r5_gemm_order_ring_ab.jsonl); row-major elsewhere (within noise).
+        // TDL_GEMM_GROUPM overrides (read per launch: in-process A/B)
+        const char* g = std::getenv("TDL_GEMM_GROUPM");
+        p.group_m = g ? std::atoi(g) : (p.tiles_n >= 16 ? 8 : 0);
+    }
     p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
 #ifdef TDL_GEMM_ISA_ONLY  // inspection builds: one instantiation (scripts/isa_p4.sh)
 #ifndef P4_TA
@@ -1133,15 +1197,6 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     }
     if (kps / BK < 2) return (int)hipErrorInvalidValue;  // the ping-pong schedule needs two K steps
     const dim3 grid(p.tiles, split);
-    if (!ta && !tb && epi <= EPI_DGELU && split == 1 && p.ldc % 8 == 0) {
-        switch (epi) {
-            case EPI_BF16: gemm_pp<false, false, EPI_BF16, true><<<grid, NTHR, 0, s>>>(p); break;
-            case EPI_GELU: gemm_pp<false, false, EPI_GELU, true><<<grid, NTHR, 0, s>>>(p); break;
-            case EPI_RESADD: gemm_pp<false, false, EPI_RESADD, true><<<grid, NTHR, 0, s>>>(p); break;
-            default: gemm_pp<false, false, EPI_DGELU, true><<<grid, NTHR, 0, s>>>(p); break;
-        }
-        TDL_LAUNCH_CHECK();
-    }
 #define PP_LAUNCH(TA_, TB_, E_) gemm_pp<TA_, TB_, E_><<<grid, NTHR, 0, s>>>(p)
 #define PP_EPI(TA_, TB_)                       \
     switch (epi) {                             \

@@ -94,6 +94,22 @@ def test_epilogues(kernel, M, N, K):
         assert _rel(acc, ref + 1.0) < 1e-4, mode
 
 
+@pytest.mark.parametrize("group", ["0", "8", "3"])
+def test_tile_orders(group, monkeypatch):
+    """every tile order (row-major, grouped by 8 tile rows, a group size that leaves a partial last
+    group) covers every output tile exactly once: ragged M / N, ping-pong and persistent kernels"""
+    from trustworthy_dl.ops import gemm
+    monkeypatch.setenv("TDL_GEMM_GROUPM", group)
+    M, N, K = 2824, 4360, 256          # 12 x 18 tiles
+    x = _rand(M, K)
+    wt = _rand(N, K, scale=0.1)
+    ref = x.float() @ wt.float().t()
+    for kn in ("pp", "p4", "p4l"):
+        out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+        gemm._launch(x, wt.t(), out, N, "none", kernel=kn)
+        assert _rel(out, ref) < 1e-2, (kn, group)
+
+
 def test_dgelu_rejects_transposed_a():
     """the dGELU column sums need rows past M to read as zero, which a transposed A cannot give"""
     from trustworthy_dl.ops import gemm
