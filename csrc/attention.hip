@@ -52,6 +52,17 @@ static int dkdv_pf() {
     return pf;
 }
 
+// waves per workgroup of the attention kernels: TDL_ATTN_WAVES=4|8 (read per launch: in-process A/B)
+// waves per workgroup of kernel i (0 forward, 1 dQ, 2 dK/dV): TDL_ATTN_WAVES = one digit for all
+// three or three digits ("844"); 8 waves stage each K/V (Q/dO) tile once for twice the rows
+static int attn_waves(int i) {
+    static const char dflt[] = "844";
+    const char* e = std::getenv("TDL_ATTN_WAVES");
+    if (e == nullptr || e[0] == 0) return dflt[i] - '0';
+    const char c = (e[1] == 0) ? e[0] : (std::strlen(e) > (size_t)i ? e[i] : dflt[i]);
+    return c == '8' ? 8 : 4;
+}
+
 static int attn_nbh_arg(int nbh) {
     const char* e = std::getenv("TDL_ATTN_MAP");
     return (e && std::strcmp(e, "xcd") == 0) ? -nbh : nbh;
@@ -138,10 +149,13 @@ __device__ __forceinline__ float max32(const f32x16& a, const f32x16& b) {
 // back on one XCD, longest causal rows first (longest-processing-time-first inside each head).
 // PF: K / V register prefetch depth in tiles (1: tile t+1 loads during tile t; 2: tile t+2, so a
 // load has two tiles of compute to land: TDL_ATTN_FWD_PF, read per launch for in-process A/B)
-template <bool CAUSAL, int PF = 1, bool OPT = false>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                       float* __restrict__ lse, int T, int H, int nbh, float scale_log2) {
-    constexpr int BM = 128, BN = 64;
+// NW: waves per workgroup (32 queries each): 8 waves share every staged K / V tile between twice
+// the queries (half the K / V traffic and LDS writes per MFMA of the 4-wave form)
+template <bool CAUSAL, int PF = 1, bool OPT = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                           float* __restrict__ lse, int T, int H, int nbh, float scale_log2) {
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    constexpr int BM = 32 * NW, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][BN * HD];
     __shared__ __attribute__((aligned(16))) bf16_t Vs[2][BN * HD];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
@@ -170,9 +184,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     }
     // tr-read lane geometry (16-lane groups): lane 4q+p supplies row q, cols 4p..4p+3
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
-    // staging: 2 x 16 B of K and of V per thread per 64-key tile; the NEXT tile is loaded into
-    // registers while the current one computes (one barrier per tile, LDS double-buffered)
-    // staging registers as named scalars (an indexed array lands in scratch)
+    // staging: 16 B of K and of V per thread and key row it stages (2 rows with 4 waves, 1 with 8)
+    // per 64-key tile; the NEXT tile is loaded into registers while the current one computes (one
+    // barrier per tile, LDS double-buffered); staging registers as named scalars (an indexed array
+    // lands in scratch)
     uint4 kreg0, kreg1, vreg0, vreg1;      // tile t+1
     uint4 kf0, kf1, vf0, vf1;              // tile t+2 (PF = 2)
     const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
@@ -180,15 +195,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
         const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
         k0 = *(const uint4*)(kbase + g0);
         v0 = *(const uint4*)(vbase + g0);
-        k1 = *(const uint4*)(kbase + g1);
-        v1 = *(const uint4*)(vbase + g1);
+        if constexpr (NW == 4) {
+            k1 = *(const uint4*)(kbase + g1);
+            v1 = *(const uint4*)(vbase + g1);
+        }
     };
     auto gload = [&](int kb) { gload_to(kb, kreg0, kreg1, vreg0, vreg1); };
     auto sstore = [&](int buf) {
         *(uint4*)(Ks[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
         *(uint4*)(Vs[buf] + swz_tr(srow0, sch * 8)) = vreg0;
-        *(uint4*)(Ks[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
-        *(uint4*)(Vs[buf] + swz_tr(srow1, sch * 8)) = vreg1;
+        if constexpr (NW == 4) {
+            *(uint4*)(Ks[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+            *(uint4*)(Vs[buf] + swz_tr(srow1, sch * 8)) = vreg1;
+        }
     };
     gload(0);
     sstore(0);
@@ -329,7 +348,6 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
     (void)unused;
     if (D != HD || T % 64 != 0) return (int)hipErrorInvalidValue;
     if (T % 128 != 0) return (int)hipErrorInvalidValue;
-    const int grid = B * H * (T / 128);
     const float sl2 = scale * 1.4426950408889634f;
     const char* pfe = std::getenv("TDL_ATTN_FWD_PF");
     const bool pf2 = pfe && pfe[0] == '2';
@@ -338,6 +356,11 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
     auto Q = (const bf16_t*)qkv;
     auto O = (bf16_t*)out;
     const int nb = attn_nbh_arg(B * H);
+    if (causal && opt && attn_waves(0) == 8 && T % 256 == 0) {
+        attn_fwd_kernel<true, 1, true, 8><<<B * H * (T / 256), 512, 0, s>>>(Q, O, lse, T, H, nb, sl2);
+        TDL_LAUNCH_CHECK();
+    }
+    const int grid = B * H * (T / 128);
     if (causal) {
         if (opt) attn_fwd_kernel<true, 1, true><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
         else if (pf2) attn_fwd_kernel<true, 2><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
@@ -390,12 +413,15 @@ __device__ __forceinline__ float bf16_round(float x) {
     return b[0];
 }
 
-template <bool CAUSAL, int NS, int PF>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+// NW = 8: 256 keys per workgroup, every staged Q / dO tile shared by twice the keys (waves 0-3
+// stage Q, waves 4-7 dO)
+template <bool CAUSAL, int NS, int PF, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                             const float* __restrict__ lse, const float* __restrict__ delta,
                                                             bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale,
                                                             float* __restrict__ bias_part) {
-    constexpr int BK = 128, BQ = 32 * NS;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    constexpr int BK = 32 * NW, BQ = 32 * NS;
     // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
     // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
     __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
@@ -432,20 +458,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     f32x16 dv0 = {}, dv1 = {}, dk0 = {}, dk1 = {};
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     const int q_start = CAUSAL ? kblk : 0;   // multiple of 128, so BQ (32 or 64) tiles end at T
-    const int srow = tid >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 slab per operand
+    const int srow = (tid & 255) >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 slab per operand
     const int swz = ((sch ^ (srow & 7)) * 8);  // (srow + 32 j) & 7 == srow & 7
+    // which operand this thread stages: both (4 waves), Q (waves 0-3) or dO (waves 4-7) with 8
+    const bool stq = NW == 4 || tid < 256, std_ = NW == 4 || tid >= 256;
     constexpr float LOG2E = 1.4426950408889634f;
     const float sl2 = scale * LOG2E;
     // prologue: tile q_start -> buffer 0
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
         const int row = srow + 32 * j;
-        const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + row) * ldq + sch * 8);
-        const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + row) * ldo + sch * 8);
-        *(uint4*)(Qs[0] + swz_tr(row, sch * 8)) = q;
-        *(uint4*)(Qw[0] + row * HD + swz) = q;
-        *(uint4*)(dOs[0] + swz_tr(row, sch * 8)) = d;
-        *(uint4*)(dOw[0] + row * HD + swz) = d;
+        if (stq) {
+            const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + row) * ldq + sch * 8);
+            *(uint4*)(Qs[0] + swz_tr(row, sch * 8)) = q;
+            *(uint4*)(Qw[0] + row * HD + swz) = q;
+        }
+        if (std_) {
+            const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + row) * ldo + sch * 8);
+            *(uint4*)(dOs[0] + swz_tr(row, sch * 8)) = d;
+            *(uint4*)(dOw[0] + row * HD + swz) = d;
+        }
     }
     if (tid < BQ) {
         lse_s[0][tid] = lse_row[q_start + tid] * LOG2E;
@@ -461,8 +493,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     auto load_tile = [&](int t0, uint4 (&q)[NS], uint4 (&d)[NS], float& l, float& dl) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            q[j] = *(const uint4*)(qbase + (size_t)(t0 + srow + 32 * j) * ldq + sch * 8);
-            d[j] = *(const uint4*)(dobase + (size_t)(t0 + srow + 32 * j) * ldo + sch * 8);
+            if (stq) q[j] = *(const uint4*)(qbase + (size_t)(t0 + srow + 32 * j) * ldq + sch * 8);
+            if (std_) d[j] = *(const uint4*)(dobase + (size_t)(t0 + srow + 32 * j) * ldo + sch * 8);
         }
         if (tid < BQ) {
             l = lse_row[t0 + tid] * LOG2E;
@@ -549,10 +581,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 const int row = srow + 32 * j;
-                *(uint4*)(Qs[buf ^ 1] + swz_tr(row, sch * 8)) = qn[j];
-                *(uint4*)(Qw[buf ^ 1] + row * HD + swz) = qn[j];
-                *(uint4*)(dOs[buf ^ 1] + swz_tr(row, sch * 8)) = dn[j];
-                *(uint4*)(dOw[buf ^ 1] + row * HD + swz) = dn[j];
+                if (stq) {
+                    *(uint4*)(Qs[buf ^ 1] + swz_tr(row, sch * 8)) = qn[j];
+                    *(uint4*)(Qw[buf ^ 1] + row * HD + swz) = qn[j];
+                }
+                if (std_) {
+                    *(uint4*)(dOs[buf ^ 1] + swz_tr(row, sch * 8)) = dn[j];
+                    *(uint4*)(dOw[buf ^ 1] + row * HD + swz) = dn[j];
+                }
             }
             if (tid < BQ) {
                 lse_s[buf ^ 1][tid] = ln;
@@ -587,7 +623,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     }
     if (bias_part != nullptr) {
         // value i = 16 kind + 4 g + e, kind 0/1: dK columns (32 kind + 8 g + 4 h + e), 2/3: dV
-        __shared__ float cs[4][2][64];
+        __shared__ float cs[NW][2][64];
         float v[64];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -604,11 +640,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         __syncthreads();
         if (tid < 128) {
             const int hh = tid >> 6, i = tid & 63;
-            const float t = cs[0][hh][i] + cs[1][hh][i] + cs[2][hh][i] + cs[3][hh][i];
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) t += cs[k][hh][i];   // fixed order: deterministic
             const int kind = i >> 4, g = (i >> 2) & 3, e = i & 3;
             const int c = 32 * (kind & 1) + 8 * g + 4 * hh + e;
             const int col = (kind < 2 ? H * HD : 2 * H * HD) + hd * HD + c;
-            bias_part[((size_t)b * (T / BK) + kbi) * (3 * H * HD) + col] = t;
+            // partial rows are per 128 tokens: an 8-wave workgroup (256 keys) fills two, the second with 0
+            const size_t row = (size_t)b * (T / 128) + kbi * (BK / 128);
+            bias_part[row * (3 * H * HD) + col] = t;
+            if (BK == 256) bias_part[(row + 1) * (3 * H * HD) + col] = 0.f;
         }
     }
 }
@@ -618,13 +659,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 // dP^T = V.dO^T and S^T = K.Q^T (row-read A), dS^T = P^T * (dP^T - delta) in registers, then
 // dQ^T += K^T.dS^T with K^T from the transposed read of a plain K image and dS^T as the B operand.
 // No atomics, no LDS round trip for dS.
-template <bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
+template <bool CAUSAL, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ out,
                                                           float* __restrict__ delta,
                                                           bf16_t* __restrict__ dqkv, int T, int H, int nbh, float scale,
                                                           float* __restrict__ bias_part) {
-    constexpr int BM = 128, BN = 64;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    constexpr int BM = 32 * NW, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Kr[2][BN * HD];  // swizzled, row reads
     __shared__ __attribute__((aligned(16))) bf16_t Kp[2][BN * HD];  // plain, transposed reads
     __shared__ __attribute__((aligned(16))) bf16_t Vr[2][BN * HD];  // swizzled, row reads
@@ -676,16 +718,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
         kreg0 = *(const uint4*)(kbase + g0);
         vreg0 = *(const uint4*)(vbase + g0);
-        kreg1 = *(const uint4*)(kbase + g1);
-        vreg1 = *(const uint4*)(vbase + g1);
+        if constexpr (NW == 4) {
+            kreg1 = *(const uint4*)(kbase + g1);
+            vreg1 = *(const uint4*)(vbase + g1);
+        }
     };
     auto sstore = [&](int buf) {
         *(uint4*)(Kr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
         *(uint4*)(Kp[buf] + swz_tr(srow0, sch * 8)) = kreg0;
         *(uint4*)(Vr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = vreg0;
-        *(uint4*)(Kr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
-        *(uint4*)(Kp[buf] + swz_tr(srow1, sch * 8)) = kreg1;
-        *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
+        if constexpr (NW == 4) {
+            *(uint4*)(Kr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+            *(uint4*)(Kp[buf] + swz_tr(srow1, sch * 8)) = kreg1;
+            *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
+        }
     };
     gload(0);
     sstore(0);
@@ -755,7 +801,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     }
     if (bias_part != nullptr) {
         // value i = 16 kind + 4 g + e: dQ column 32 kind + 8 g + 4 h + e
-        __shared__ float cs[4][2][32];
+        __shared__ float cs[NW][2][32];
         float v[32];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -769,10 +815,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         __syncthreads();
         if (tid < 64) {
             const int hh = tid >> 5, i = tid & 31;
-            const float t = cs[0][hh][i] + cs[1][hh][i] + cs[2][hh][i] + cs[3][hh][i];
+            float t = 0.f;
+#pragma unroll
+            for (int k = 0; k < NW; ++k) t += cs[k][hh][i];   // fixed order: deterministic
             const int kind = i >> 4, g = (i >> 2) & 3, e = i & 3;
             const int col = hd * HD + 32 * kind + 8 * g + 4 * hh + e;
-            bias_part[((size_t)b * (T / BM) + qb) * (3 * H * HD) + col] = t;
+            const size_t row = (size_t)b * (T / 128) + qb * (BM / 128);
+            bias_part[row * (3 * H * HD) + col] = t;
+            if (BM == 256) bias_part[(row + 1) * (3 * H * HD) + col] = 0.f;
         }
     }
 }
@@ -794,9 +844,13 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     auto dQKV = (bf16_t*)dqkv;
     const int nb = attn_nbh_arg(B * H);
     float* bp = bias_part;
+    const int g8 = B * H * (T / 256);
+    const bool w8 = causal && T % 256 == 0;
     if (causal) {
-        attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        if (w8 && attn_waves(1) == 8) attn_bwd_dq_kernel<true, 8><<<g8, 512, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
+        else attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
+        if (w8 && attn_waves(2) == 8) attn_bwd_dkdv_kernel<true, 1, 2, 8><<<g8, 512, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
