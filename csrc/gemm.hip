@@ -1197,6 +1197,15 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     }
     if (kps / BK < 2) return (int)hipErrorInvalidValue;  // the ping-pong schedule needs two K steps
     const dim3 grid(p.tiles, split);
+    if (!ta && !tb && epi <= EPI_DGELU && split == 1 && p.ldc % 8 == 0) {
+        switch (epi) {
+            case EPI_BF16: gemm_pp<false, false, EPI_BF16, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_GELU: gemm_pp<false, false, EPI_GELU, true><<<grid, NTHR, 0, s>>>(p); break;
+            case EPI_RESADD: gemm_pp<false, false, EPI_RESADD, true><<<grid, NTHR, 0, s>>>(p); break;
+            default: gemm_pp<false, false, EPI_DGELU, true><<<grid, NTHR, 0, s>>>(p); break;
+        }
+        TDL_LAUNCH_CHECK();
+    }
 #define PP_LAUNCH(TA_, TB_, E_) gemm_pp<TA_, TB_, E_><<<grid, NTHR, 0, s>>>(p)
 #define PP_EPI(TA_, TB_)                       \
     switch (epi) {                             \
