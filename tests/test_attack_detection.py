@@ -63,6 +63,7 @@ def _f1_run(det, transform, seed=0, warm=100, steps=200, p=0.2):
     return 2 * prec * rec / (prec + rec) if prec + rec else 0.0, fp
 
 
+@pytest.mark.slow
 def test_gradient_f1_reference_vs_fixed():
     f1_ref, _ = _f1_run(AttackDetector(compat=True), lambda g: g * 10)
     f1_new, fp_new = _f1_run(AttackDetector(), lambda g: g * 10)

@@ -49,6 +49,7 @@ def _blamed(eng):
     return sorted({(a["step"], a["node_id"], a["attack_type"]) for a in eng.attack_history})
 
 
+@pytest.mark.slow
 def test_local_byzantine_blames_only_the_tampering_stages():
     eng = _engine(4, "byzantine", targets=(0, 2))
     for b in _batches(10):
@@ -60,6 +61,7 @@ def test_local_byzantine_blames_only_the_tampering_stages():
     assert {s for s, _, _ in got} == set(range(6, 11))       # every attacked step, nothing before
 
 
+@pytest.mark.slow
 def test_local_clean_run_blames_nobody():
     eng = _engine(4)
     for b in _batches(12):
@@ -68,6 +70,7 @@ def test_local_clean_run_blames_nobody():
     assert eng.attack_history == []
 
 
+@pytest.mark.slow
 def test_local_param_perturbation_is_integrity_not_audit():
     eng = _engine(3, "model_poisoning", targets=(1,))
     for b in _batches(9):
@@ -94,7 +97,8 @@ def _worker(rank, world, port, out_path, attack, targets):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("attack,targets", [("byzantine", (1,)), ("byzantine", (0,)), (None, ())])
+@pytest.mark.parametrize("attack,targets", [pytest.param("byzantine", (1,), marks=pytest.mark.slow), pytest.param("byzantine", (0,), marks=pytest.mark.slow),
+                                            pytest.param(None, (), marks=pytest.mark.slow)])
 def test_distributed_audit(attack, targets):
     world = 3
     with tempfile.TemporaryDirectory() as td:

@@ -53,6 +53,7 @@ def _blamed(eng):
     return sorted({(a["step"], a["node_id"], a["attack_type"]) for a in eng.attack_history})
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("mode", ["sign_flip", "scale", "zero"])
 def test_local_gradient_poisoning_caught_by_commitment(mode):
     """The applied gradient differs from the committed per-micro-batch contributions: proof, on
@@ -67,6 +68,7 @@ def test_local_gradient_poisoning_caught_by_commitment(mode):
     assert {s for s, _, _ in got} == set(range(6, 10))
 
 
+@pytest.mark.slow
 def test_local_dx_tamper_caught_and_upstream_victims_not_blamed():
     """A stage that tampers the activation gradient it sends upstream (Byzantine backward): its
     auditor recomputes the input gradient and finds the mismatch; the upstream stages whose
@@ -83,6 +85,7 @@ def test_local_dx_tamper_caught_and_upstream_victims_not_blamed():
 
 @pytest.mark.parametrize("attack,kind", [("byzantine_backward", "gradient_tampering"),
                                          ("gradient_poisoning", "gradient_poisoning")])
+@pytest.mark.slow
 def test_local_loss_stage_is_audited(attack, kind):
     """The last (loss) stage is audited by its predecessor (round 3 never recomputed it)."""
     eng = _engine(3, attack, targets=(2,), atk_kw={"gradient_mode": "sign_flip"})
@@ -94,6 +97,7 @@ def test_local_loss_stage_is_audited(attack, kind):
     assert all(k == kind for _, _, k in got)
 
 
+@pytest.mark.slow
 def test_local_one_of_m_gradient_poisoning_caught_by_recompute():
     """Gradient poisoning of ONE micro-batch's contribution inside the backward: the commitments
     are consistent, only the recompute of the audited micro-batch sees it (probability 1/M per
@@ -109,6 +113,7 @@ def test_local_one_of_m_gradient_poisoning_caught_by_recompute():
     assert all(k == "gradient_poisoning" for _, _, k in got)
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("targeted", [None, False])
 def test_local_one_of_m_output_tamper_targeted(targeted):
     """A Byzantine stage that tampers ONE micro-batch's output per step: the uniform private choice
@@ -130,6 +135,7 @@ def test_local_one_of_m_output_tamper_targeted(targeted):
         assert eng.audit_summary()["targeted_extra"] == 0
 
 
+@pytest.mark.slow
 def test_local_one_of_m_gradient_scale_targeted():
     """One micro-batch's weight-gradient contribution scaled inside the backward: its committed
     sketch norm stands out, the targeted audit recomputes it on most tampered steps."""
@@ -143,6 +149,7 @@ def test_local_one_of_m_gradient_scale_targeted():
     assert len({s for s, _, _ in got}) >= 15, got      # of 21 tampered steps (uniform alone: ~5)
 
 
+@pytest.mark.slow
 def test_local_clean_run_no_blame_with_backward_audit():
     eng = _engine(4, micro=4)
     for b in _batches(10, bs=8):
@@ -151,6 +158,7 @@ def test_local_clean_run_no_blame_with_backward_audit():
     assert eng.attack_history == []
 
 
+@pytest.mark.slow
 def test_proof_compromises_at_once_and_recovery_uses_shadow():
     """An audit mismatch compromises the node at its first detection (no two-consecutive-flags
     rule) and the re-shard restores its layers from the build-time committed snapshot — not from
@@ -169,6 +177,7 @@ def test_proof_compromises_at_once_and_recovery_uses_shadow():
     assert eng.trust.get_node_status(1) == NodeStatus.COMPROMISED
 
 
+@pytest.mark.slow
 def test_no_verified_shadow_restores_initial_weights_not_own():
     """With the shadow copy corrupted on its holder, the compromised stage's layers restart from
     the initial weights; its own memory is never packed."""
@@ -211,6 +220,7 @@ def _worker(rank, world, port, out_path, attack, targets, atk_kw, micro, cfg=Non
     ("gradient_poisoning", (0,), {"gradient_mode": "sign_flip"}, "gradient_poisoning"),
     ("model_poisoning", (1,), {"lie_integrity": True}, "model_poisoning"),         # lies about its checksum
     (None, (), None, None)])
+@pytest.mark.slow
 def test_distributed_backward_audit(attack, targets, atk_kw, kind):
     world = 3
     with tempfile.TemporaryDirectory() as td:
@@ -227,6 +237,7 @@ def test_distributed_backward_audit(attack, targets, atk_kw, kind):
     assert {s for s, _, _ in got} == set(range(6, 10)), got
 
 
+@pytest.mark.slow
 def test_distributed_targeted_audit_one_of_m():
     """Distributed opt-in targeted audit (audit_targeted=True): the auditor scores the M outputs it
     received, reveals the uniform choice plus the outlier through the store, the auditee ships both

@@ -36,6 +36,7 @@ def _run(n, *extra, model="gpt2-tiny", timeout=300):
 
 @pytest.mark.parametrize("n,mode", [(2, "async"), (2, "grouped"), (4, "async"), (4, "grouped"),
                                     (8, "async"), (8, "grouped")])
+@pytest.mark.slow
 def test_bench_multirank_json_line(n, mode):
     model = "gpt2-mini" if n == 8 else "gpt2-tiny"   # gpt2-tiny has fewer pipeline units than 8
     out, lines, _ = _run(n, "--p2p-mode", mode, model=model)
@@ -75,6 +76,7 @@ def test_bench_multirank_json_line(n, mode):
     assert max(streams) <= 32
 
 
+@pytest.mark.slow
 def test_bench_midrun_reassign():
     out, lines, _ = _run(4, "--reassign-at", "2")
     assert out.returncode == 0, out.stderr[-3000:]
@@ -87,6 +89,7 @@ def test_bench_midrun_reassign():
     assert d["config"]["process_groups_created"] == 2 + 1 + 1 + 1
 
 
+@pytest.mark.slow
 @pytest.mark.parametrize("fault", ["hang", "raise"])
 def test_bench_failure_is_legible(fault):
     out, lines, wall = _run(4, "--watchdog", "8", "--debug-fault", fault, "--debug-fault-rank", "2",

@@ -86,6 +86,7 @@ def _bench(n, d, *extra, model="gpt2-tiny"):
     (2, ("--p2p-mode", "async")), (4, ("--p2p-mode", "grouped")), (4, ("--p2p-mode", "async", "--reassign-at", "2")),
     (4, ("--p2p-mode", "async", "--audit-targeted")),
     (8, ("--p2p-mode", "async")), (8, ("--p2p-mode", "grouped"))])
+@pytest.mark.slow
 def test_bench_schedule_replays_under_rccl_model(n, extra):
     """The bench's whole run (build-time shadows, 1F1B, forward + backward audit with its store
     reveal, digest all-gathers, tied all-reduce, re-shard) recorded on gloo and replayed under the

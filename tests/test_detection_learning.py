@@ -18,6 +18,7 @@ def _engine(attacker=None, nodes=4):
     return PipelineEngine(m, cfg, attacker=attacker, metrics=MetricsCollector())
 
 
+@pytest.mark.slow
 def test_markov_stream_deterministic_and_low_entropy():
     a = next(iter(MarkovLanguageModeling(2, 32, 1024, num_batches=1, seed=3)))
     b = next(iter(MarkovLanguageModeling(2, 32, 1024, num_batches=1, seed=3)))
@@ -26,6 +27,7 @@ def test_markov_stream_deterministic_and_low_entropy():
     assert ds.entropy() < 1.5     # nats; ln(1024) = 6.9
 
 
+@pytest.mark.slow
 def test_clean_learning_has_no_false_positives():
     e = _engine()
     for b in MarkovLanguageModeling(4, 64, 1024, num_batches=120):
@@ -42,6 +44,7 @@ def test_clean_learning_has_no_false_positives():
     ("model_poisoning", dict(intensity=0.05)),
     ("byzantine", dict(intensity=0.5)),
 ])
+@pytest.mark.slow
 def test_attacks_detected_during_learning(kind, kw):
     from trustworthy_dl.attacks.adversarial_attacks import AdversarialAttacker, AttackConfig
     att = AdversarialAttacker(AttackConfig(attack_types=[kind], target_nodes=[2], start_step=30, probability=0.25,

@@ -70,8 +70,9 @@ def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="asy
 
 
 @pytest.mark.parametrize("model_name,micro,world,p2p,gran", [
-    ("resnet32", 2, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "async", "auto"), ("gpt2-tiny", 4, 2, "grouped", "auto"),
-    ("gpt2-tiny", 2, 4, "async", "auto"), ("gpt2-tiny", 8, 4, "async", "auto"),
+    ("resnet32", 2, 2, "async", "auto"), pytest.param("gpt2-tiny", 4, 2, "async", "auto", marks=pytest.mark.slow),
+    ("gpt2-tiny", 4, 2, "grouped", "auto"),
+    pytest.param("gpt2-tiny", 2, 4, "async", "auto", marks=pytest.mark.slow), ("gpt2-tiny", 8, 4, "async", "auto"),
     ("gpt2-tiny", 4, 4, "async", "half")])  # stage boundaries inside blocks, one process per stage
 def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran, monkeypatch):
     steps = 4

@@ -39,6 +39,7 @@ def test_checkpoint_faults_parse():
         faults.parse("explode:rank=0")
 
 
+@pytest.mark.slow
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("fault,victim", [("crash", 2), ("hang", 2), ("crash", 1)])
 def test_elastic_shrink_and_resume(tmp_path, fault, victim):

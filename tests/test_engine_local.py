@@ -121,6 +121,7 @@ def test_reshard_preserves_function_and_optimizer_state():
     assert eng.flush() is not None
 
 
+@pytest.mark.slow
 def test_trainer_facade_checkpoint_roundtrip(tmp_path):
     from trustworthy_dl import DistributedTrainer
     from trustworthy_dl.utils.checkpoint import consolidate

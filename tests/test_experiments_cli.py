@@ -74,6 +74,7 @@ def test_node_monitor_baselines_and_scores():
     assert mon.get_expected_mean(0) is None
 
 
+@pytest.mark.slow
 def test_experiment_runner_writes_reference_artifacts(tmp_path):
     from trustworthy_dl.experiments.runner import ExperimentConfig, ExperimentRunner
     cfg = ExperimentConfig(experiment_name="tiny", model_name="gpt2", dataset_name="openwebtext", num_nodes=2,

@@ -90,7 +90,7 @@ def test_local_adaptive_post_backward_caught_every_step():
     assert {s for s, _, _ in got} == set(tampered)
 
 
-@pytest.mark.parametrize("k", [1, 4])
+@pytest.mark.parametrize("k", [pytest.param(1, marks=pytest.mark.slow), 4])
 def test_local_adaptive_one_of_m_caught_by_keyed_recompute(k):
     """Adaptive tamper of ONE micro-batch's contribution inside the backward (consistent with the
     commitments): only the keyed recompute of an audited micro-batch sees it.  With k = M audited
@@ -112,6 +112,7 @@ def test_local_adaptive_one_of_m_caught_by_keyed_recompute(k):
         assert {s for s, _, _ in got} == set(tampered)
 
 
+@pytest.mark.slow
 def test_local_clean_run_no_false_keyed_flags():
     """No attack: the keyed recompute and the exact applied hash never flag a clean stage, k = M."""
     from trustworthy_dl.models import get_model

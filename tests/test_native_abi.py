@@ -11,7 +11,7 @@ def _c_arity():
     out = {}
     for path in glob.glob(os.path.join(ROOT, "csrc", "*.hip")):
         src = open(path).read()
-        for m in re.finditer(r"TDL_API\s+\w+\s+(tdl_\w+)\s*\(([^)]*)\)", src):
+        for m in re.finditer(r"TDL_API\s+(?:\w+\s+)+?(tdl_\w+)\s*\(([^)]*)\)", src):
             args = [a for a in m.group(2).split(",") if a.strip()]
             out[m.group(1)] = len(args)
     return out

@@ -78,6 +78,7 @@ def _worker(rank, world, port, ckpt, out_path, phase, save_at, total):
     tr.cleanup()
 
 
+@pytest.mark.slow
 def test_resume_4_ranks_into_3():
     total, save_at = 5, 3
     with tempfile.TemporaryDirectory() as d:

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -456,6 +456,19 @@ def cosine_gram(xs: List[torch.Tensor]) -> torch.Tensor:
     return G / (nrm[:, None] * nrm[None, :])
 
 
+_pos_w: Dict = {}
+
+
+def _position_weights(n: int, device) -> torch.Tensor:
+    key = (n, str(device))
+    w = _pos_w.get(key)
+    if w is None:
+        if len(_pos_w) > 64:
+            _pos_w.clear()
+        w = _pos_w[key] = (torch.arange(n, dtype=torch.float64, device=device) % 1021) + 1
+    return w
+
+
 def checksum(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Deterministic (sum, sum of squares, position-weighted sum) of a flat buffer, float64 [3].
     Bit-identical data -> bit-identical result (fixed reduction order; csrc/stats.hip)."""
@@ -467,6 +480,6 @@ def checksum(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tenso
         _lib.call("tdl_checksum_bf16", ptr(x), x.numel(), ptr(ws), ptr(out), stream_ptr(x.device))
         return out
     v = x.double()
-    w = (torch.arange(v.numel(), dtype=torch.float64, device=v.device) % 1021) + 1
+    w = _position_weights(v.numel(), v.device)
     out.copy_(torch.stack([v.sum(), (v * v).sum(), (v * w).sum()]))
     return out

@@ -71,26 +71,48 @@ BYZANTINE_SIM = 0.5    # attack_detector.py:158
 BACKDOOR_KL = 2.0      # attack_detector.py:179
 
 
+def _quantiles(x: np.ndarray, ps: Sequence[float]) -> List[float]:
+    """numpy's default ('linear') quantiles of ``x`` at fractions ``ps`` from ONE multi-kth
+    partition (np.median + two np.percentile calls partition the array three times)."""
+    n = x.size
+    if n == 0:
+        return [0.0 for _ in ps]
+    pos = [(n - 1) * p for p in ps]
+    lo = [int(np.floor(v)) for v in pos]
+    hi = [min(l + 1, n - 1) for l in lo]
+    part = np.partition(x, sorted(set(lo) | set(hi)))
+    out = []
+    for v, l, h in zip(pos, lo, hi):
+        a, b, t = float(part[l]), float(part[h]), v - l
+        out.append(a + (b - a) * t if t < 0.5 else b - (b - a) * (1.0 - t))
+    return out
+
+
 def numpy_tensor_statistics(x: np.ndarray) -> Dict[str, float]:
     """Exact host statistics with the reference definitions (attack_detector.py:185-200):
     population std, biased skewness, Fisher (excess) kurtosis."""
-    x = np.asarray(x, dtype=np.float64).ravel()
-    n = x.size
-    mean = float(x.mean())
-    d = x - mean
-    m2 = float(np.mean(d * d))
-    m3 = float(np.mean(d * d * d))
-    m4 = float(np.mean((d * d) ** 2))
+    x32 = np.asarray(x).ravel()
+    n = x32.size
+    q25, q50, q75 = _quantiles(x32, (0.25, 0.5, 0.75))
+    # moments in float64 through torch (multi-threaded on the host; same definitions)
+    t = torch.from_numpy(np.ascontiguousarray(x32)).double()
+    mean = float(t.mean())
+    d = t - mean
+    d2 = d * d
+    m2 = float(d2.mean())
+    m3 = float((d2 * d).mean())
+    m4 = float((d2 * d2).mean())
     std = m2 ** 0.5
     skew = m3 / m2 ** 1.5 if m2 > 0 else 0.0
     kurt = m4 / (m2 * m2) - 3.0 if m2 > 0 else -3.0
+    a = t.abs()
     return {
-        "mean": mean, "std": std, "min": float(x.min()), "max": float(x.max()),
-        "median": float(np.median(x)), "skewness": skew, "kurtosis": kurt,
-        "percentile_25": float(np.percentile(x, 25)),
-        "percentile_75": float(np.percentile(x, 75)),
-        "norm_l1": float(np.abs(x).sum()), "norm_l2": float(np.sqrt((x * x).sum())),
-        "norm_inf": float(np.abs(x).max()) if n else 0.0,
+        "mean": mean, "std": std, "min": float(t.min()), "max": float(t.max()),
+        "median": q50, "skewness": skew, "kurtosis": kurt,
+        "percentile_25": q25,
+        "percentile_75": q75,
+        "norm_l1": float(a.sum()), "norm_l2": float(torch.sqrt((t * t).sum())),
+        "norm_inf": float(a.max()) if n else 0.0,
     }
 
 

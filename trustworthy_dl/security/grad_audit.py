@@ -38,7 +38,7 @@ for the targeted audit.  The binding checks use
 from __future__ import annotations
 
 import hashlib
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -70,6 +70,20 @@ def _segments(n: int, masked: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int,
     return segs
 
 
+_pmix: Dict[Tuple[int, int, int], torch.Tensor] = {}
+
+
+def _position_mix(lo: int, hi: int, seed: int) -> torch.Tensor:
+    """CPU path: mix(j ^ seed) over [lo, hi) (one seed serves every commitment of a step)."""
+    key = (lo, hi, seed)
+    t = _pmix.get(key)
+    if t is None:
+        if len(_pmix) > 16:
+            _pmix.clear()
+        t = _pmix[key] = _mix32((torch.arange(lo, hi, dtype=torch.int64) & M32) ^ seed)
+    return t
+
+
 @torch.no_grad()
 def word_hash(x: torch.Tensor, segments: Sequence[Tuple[int, int]], seed: int = 0,
               snapshot: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -93,8 +107,7 @@ def word_hash(x: torch.Tensor, segments: Sequence[Tuple[int, int]], seed: int = 
     w = x.view(torch.int32).to(torch.int64) & M32
     tot = torch.zeros((), dtype=torch.int64)
     for lo, hi in segments:
-        j = torch.arange(lo, hi, dtype=torch.int64) & M32
-        tot = tot + _mix32(w[lo:hi] ^ _mix32(j ^ (int(seed) & M32))).sum()
+        tot = tot + _mix32(w[lo:hi] ^ _position_mix(lo, hi, int(seed) & M32)).sum()
         if snapshot is not None:
             snapshot.reshape(-1)[lo:hi].copy_(x[lo:hi])
     out.copy_(tot.reshape(1))
