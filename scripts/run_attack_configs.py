@@ -60,6 +60,15 @@ CONFIGS["5m"] = dict(model="gpt2-medium", attack=dict(attack_types=["byzantine"]
 # targeted audit picks it)
 CONFIGS["3ms"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="scale",
                                                        micro_batches=1), targets=[3], lr=1e-4)
+# round 5 (commit-then-reveal audit): ADAPTIVE gradient poisoning that knows the public job seed and
+# hides its sign flip from the public sketch window; "3a" rewrites the gradient after the backward,
+# "3am" tampers one micro-batch's contribution inside it (caught by the keyed recompute of an audited
+# micro-batch: k of M per step, here k = 4 of 16)
+CONFIGS["3a"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip",
+                                                      adaptive=True), targets=[3], lr=1e-4)
+CONFIGS["3am"] = dict(model="gpt2-medium", attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip",
+                                                       adaptive=True, micro_batches=1), targets=[3], lr=1e-4,
+                      audit_micro_k=4)
 CONFIGS["liar"] = dict(model="gpt2-medium", attack=dict(attack_types=["model_poisoning"], intensity=0.05,
                                                         lie_integrity=True), targets=[6], lr=1e-4)
 
@@ -89,7 +98,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
                        # reference protocol warms up on 100 clean steps: BASELINE.md); at 20 the
                        # baselines of GPT-2 hidden states caught early-training transients as z ~ 30
                        # output anomalies; the monitored micro-batch RNG is pinned for reproducibility
-                       verifier={"warmup": warmup}, monitor_seed=seed, **extra)
+                       verifier={"warmup": warmup}, monitor_seed=seed, audit_micro_k=c.get("audit_micro_k", 1), **extra)
     eng = PipelineEngine(model, cfg, attacker=att, metrics=MetricsCollector())
     del model
     plan0 = eng.plan.describe()
@@ -131,7 +140,8 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
                       if k in ("tp", "fp", "fn", "precision", "recall", "f1", "mean_time_to_detect_steps")},
         "injections": len(att.injections) if att is not None else 0,
         "tampered_steps": len({(i["node"], i["step"]) for i in att.injections}) if att is not None else 0,
-        "per_target": lag, "micro_batches": max(1, batch // mbs), "audit_summary": eng.audit_summary(),
+        "per_target": lag, "micro_batches": max(1, batch // mbs), "audit_micro_k": c.get("audit_micro_k", 1),
+        "audit_summary": eng.audit_summary(),
         "clean_nodes_blamed": clean_blamed,
         "clean_nodes_compromised": [n for n in compromised if n not in c["targets"]],
         "clean_nodes_resharded": sorted({n for r in rs for n in r["from_nodes"] if n not in c["targets"]}),
@@ -157,7 +167,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean, 3s, dx, last, 3m, 3ms, 5m, liar")
+    ap.add_argument("--configs", default="3,4,5", help="comma list of 3, 4, 5, clean, 3s, dx, last, 3m, 3ms, 5m, liar, 3a, 3am")
     ap.add_argument("--seeds", default="3", help="comma list of attacker / monitor seeds")
     ap.add_argument("--no-reassign", action="store_true", help="detection only: the target keeps its layers, so "
                     "every injection is scored (a re-shard ends the attack after the first detections)")
