@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(const bf16_t* __
 // audit evaluates a stage twice and compares; see conv.hip stats_finalize_kernel): grid (2C / 256,
 // FOLD_G), each thread one column over the rows r = y (mod FOLD_G) of its group (coalesced across
 // the wave, 4 loads in flight), the group total stored in row y (read by this group only); the LAST
-// group of the column block to arrive (agent-scope counter, release / acquire) adds the FOLD_G
+// group of the column block to arrive (agent-scope counter; hand-off by drained sc1 stores + barrier + one relaxed add, sc1 loads on the reading side: conv.hip stats_arrive) adds the FOLD_G
 // totals in group order.  cnt: zeroed by bn_act_bwd_reduce_kernel.
 __global__ __launch_bounds__(256) void bn_partial_fold_kernel(float* __restrict__ sums, float* __restrict__ partials,
                                                               int nb, int C, unsigned* __restrict__ cnt,

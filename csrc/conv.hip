@@ -560,8 +560,8 @@ __global__ __launch_bounds__(256) void conv_split_epi_kernel(const float* __rest
 // atomic version differed by up to one bf16 ulp per call, which the BN backward amplified to 4-10 %
 // of the largest input gradient: scripts/audit_probe.py, profiles/r4_audit_probe_resnet50.txt).
 // Workgroup (x, y) sums rows [y rpb, (y + 1) rpb) of its 64 columns and stores the total in the
-// group's first row; the LAST workgroup of column block x to arrive (agent-scope counter, release /
-// acquire) adds the gridDim.y group totals in group order.  fin_cnt: zeroed by the conv kernel.
+// group's first row; the LAST workgroup of column block x to arrive (agent-scope counter, drained sc1 stores /
+// sc1 loads, see stats_arrive) adds the gridDim.y group totals in group order.  fin_cnt: zeroed by the conv kernel.
 // acc_lo / acc_hi (nullable): the completed column c is also added into acc_lo[c] (c < cols / 2) or
 // acc_hi[c - cols / 2] (a folded BN's backward sums -> dbeta / dgamma).
 __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__ part, int rows, int cols,

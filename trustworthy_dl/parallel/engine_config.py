@@ -29,34 +29,25 @@ class EngineConfig:
     trust_decay_per_step: float = 0.01
     reassign: bool = True
     max_reassignment_attempts: int = 3
-    min_stages: int = 1
     output_check: str = "random"         # which micro-batch output is monitored each step: "random" (a
                                          # per-step choice from a private seeded RNG, so an attacker
                                          # cannot predict which output is inspected) | "first" | "none"
     monitor_seed: Optional[int] = None   # seed of that RNG (None: $TDL_MONITOR_SEED, else os.urandom)
     early_grad_stats: bool = True        # start each layer's gradient statistics on the side stream
                                          # as soon as its last-micro-batch backward is done
-    compromise_after: int = 2            # consecutive flagged steps before mark_compromised (1 = reference)
     defer_wgrad: bool = True             # B/W split: weight grads run after dx is posted upstream
     data_parallel: int = 1               # pipeline replicas (distributed): world = stages x replicas
-    robust_aggregation: bool = True      # DP: flagged / outlier replicas are left out of the gradient mean
-    outlier_ratio: float = 4.0           # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
-    direction_margin: float = 0.2        # DP (>= 3 replicas): cosine to the other replicas' sum below 0 and
-                                         # this far below the median = outlier (sign flips)
     param_audit_interval: int = 10       # DP: steps between cross-replica weight-digest audits (0 = off)
     param_integrity: bool = True         # checksum compute weights after each update, re-check before the next
     shadow_interval: int = 25            # steps between trusted weight snapshots held by the next stage's GPU
                                          # (0 = off); a compromised stage is restored from it, not from itself.
                                          # A snapshot is also taken when the stages are (re)built
-    shadow_copies: int = 2               # holders per snapshot (the next 1-2 stages of the ring): a stage
-                                         # whose first holder is compromised too is still restorable
     audit: bool = True                   # deterministic stage cross-check: the next stage recomputes every
                                          # non-loss stage's monitored micro-batch from its input and weights and
                                          # compares the output it received; blame for a tampered forward comes
                                          # only from such a mismatch or a failed weight-integrity check, output
                                          # z-scores no longer blame (they stay in the trust metrics)
     audit_prob: float = 1.0              # fraction of steps audited (drawn privately by each auditor)
-    audit_tol: float = 1e-2              # relative max error above which a recomputed output mismatches
     audit_backward: bool = True          # the audit covers the backward too: the auditor recomputes the
                                          # audited micro-batch's input gradient and the sketch of its
                                          # weight-gradient contribution (security/grad_audit.py), the
@@ -75,21 +66,6 @@ class EngineConfig:
                                          # then recomputed in the step it happens, not with probability 1/M.
                                          # None = local mode only (distributed: one device->host read of the
                                          # M scores per auditor and step, opt-in with True)
-    audit_target_z: float = 4.0
-    compromise_on_proof: bool = True     # a failed audit / integrity / gradient-consistency check (proof of
-                                         # tampering, not a statistic) compromises the node at once
-    attribute_flags: bool = True         # blame the earliest anomalous stage, not its downstream/upstream echoes
-    soft_output_z: float = 5.0           # with an output flag in a replica, an EARLIER stage whose output z
-                                         # exceeds this (below its own decision threshold) is the source: a
-                                         # tampered output moves its own statistics at least as much as the
-                                         # downstream echoes (0 = off)
-    global_event_fraction: float = 0.5   # gradient anomalies on >= this fraction of a replica's stages (>= 3
-                                         # stages) in one step = a pipeline-wide event (a loss spike of real
-                                         # training), not a Byzantine stage: the step's update is skipped, nobody
-                                         # is blamed, and blame stays off for ``global_event_grace`` steps while
-                                         # the detector baselines re-settle
-    global_event_grace: int = 8
-    pipeline_quarantine: bool = True     # output / integrity evidence anywhere skips the whole replica's update
     layer_granularity: str = "auto"      # "block" | "half" (GPT-2 attention / MLP halves as pipeline
                                          # units) | "auto": half when it lowers the slowest stage
     p2p_mode: str = "async"              # "async": per-direction communicators + receives posted a phase
@@ -101,6 +77,30 @@ class EngineConfig:
     trace_phases: bool = False           # HIP-event per-phase step breakdown (runtime/tracing.py)
     serialize_streams: bool = field(default_factory=lambda: os.environ.get("TDL_SERIALIZE_STREAMS", "0") == "1")
                                          # debug: verification on the compute stream (no side-stream overlap)
+
+    # ---- fixed policy constants: class attributes, not constructor knobs (no test, record or
+    # experiment varies them; read as cfg.<name> like the fields above)
+    min_stages = 1
+    compromise_after = 2        # consecutive flagged steps before mark_compromised (1 = reference)
+    robust_aggregation = True   # DP: flagged / outlier replicas are left out of the gradient mean
+    outlier_ratio = 4.0         # DP (>= 3 replicas): grad norm vs replica median beyond this = outlier
+    direction_margin = 0.2      # DP (>= 3 replicas): cosine to the other replicas' sum below 0 and
+                                # this far below the median = outlier (sign flips)
+    shadow_copies = 2           # holders per snapshot (the next 1-2 stages of the ring): a stage
+                                # whose first holder is compromised too is still restorable
+    audit_tol = 1e-2            # relative max error above which a recomputed output mismatches
+    audit_target_z = 4.0        # robust z of a micro-batch score that makes the targeted audit pick it
+    compromise_on_proof = True  # a failed audit / integrity / gradient-consistency check (proof of
+                                # tampering, not a statistic) compromises the node at once
+    attribute_flags = True      # blame the earliest anomalous stage, not its downstream/upstream echoes
+    soft_output_z = 5.0         # with an output flag in a replica, an EARLIER stage whose output z
+                                # exceeds this (below its own decision threshold) is the source
+    global_event_fraction = 0.5  # gradient anomalies on >= this fraction of a replica's stages (>= 3)
+                                 # in one step = a pipeline-wide event (a loss spike of real training):
+                                 # the update is skipped, nobody is blamed, and blame stays off for
+                                 # ``global_event_grace`` steps while the detector baselines re-settle
+    global_event_grace = 8
+    pipeline_quarantine = True  # output / integrity evidence anywhere skips the whole replica's update
 
 
 def _resolve_dtype(name: str, device: torch.device) -> torch.dtype:

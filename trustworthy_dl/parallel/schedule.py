@@ -79,6 +79,8 @@ class ScheduleMixin:
         for i in range(M):
             x = inputs[i]
             watch = i == self._mon_idx
+            y_copy = None   # the previous stage's recorded output: the next stage's recorded input when
+            #                 it arrives unchanged (same device), kept once instead of twice
             for sidx, (node, _) in enumerate(order):
                 st = self.stages[node]
                 x = self._stage_input(x, st) if sidx == 0 else x.to(st.device, non_blocking=True)
@@ -87,7 +89,7 @@ class ScheduleMixin:
                 rec = self._audit_rec.setdefault(node, {}).setdefault(i, {}) \
                     if self._audit_now and (i in self._audit_ms or self._targeted) else None
                 if rec is not None:
-                    rec["x"] = x.detach().clone()
+                    rec["x"] = y_copy if y_copy is not None and y_copy.device == x.device else x.detach().clone()
                     if st.computes_loss:
                         rec["labels"] = labels
                 if sidx > 0 and x.requires_grad:
@@ -102,8 +104,10 @@ class ScheduleMixin:
                     x.register_hook(_dx_hook)
                     prec = self._audit_rec.get(order[sidx - 1][0], {}).get(i) if rec is not None and bwd_audit else None
                     if prec is not None:
-                        def _dy_hook(g, prec=prec):
-                            prec["dy"] = g.detach().clone()
+                        def _dy_hook(g, prec=prec, rec=rec):
+                            # runs after _dx_hook: the gradient as sent, already copied there
+                            dx = rec.get("dx") if rec is not None else None
+                            prec["dy"] = dx if dx is not None and dx.device == g.device else g.detach().clone()
                         x.register_hook(_dy_hook)
                 with self.tracer.phase("fwd"):
                     y, mon = st.forward(x, labels, observe=obs, arm_grad_stats=i == M - 1)
@@ -111,8 +115,9 @@ class ScheduleMixin:
                     y = self._attack_output(node, y, truth, i, M)
                     if watch:
                         mon = y
+                    y_copy = None
                     if rec is not None:
-                        rec["y"] = y.detach().clone()
+                        rec["y"] = y_copy = y.detach().clone()
                         if self._targeted:
                             rec["ystat"] = self._output_stat(rec["y"])
                 if watch and mon is not None:
