@@ -150,6 +150,7 @@ def run(cfg_id, device: str, steps: int, start: int, batch: int, mbs: int, seq_l
                       "migration_ms": round(1000 * r["migration_time"], 2),
                       "estimated_ms": round(1000 * r["estimated_migration_time"], 2),
                       "phases_ms": {k: round(1000 * v, 2) for k, v in r.get("phases", {}).items() if k.endswith("_s")},
+                      "rebuild_new_reserved_mb": round(r.get("phases", {}).get("rebuild_new_reserved_bytes", 0) / 2**20, 1),
                       "moved_params": r["moved_params"], "restored_from_shadow": r.get("restored_from_shadow"),
                       "restored_from_initial": r.get("restored_from_initial"),
                       "plan": r["plan"]} for r in rs],

@@ -5,6 +5,7 @@ perform_task_reassignment (distributed_trainer.py:324-380), a no-op there.
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import time
@@ -20,6 +21,34 @@ from .partition import PlacementPlan, make_plan
 from .stage import Stage
 
 logger = logging.getLogger(__name__)
+
+
+class _RebuildProbe:
+    """Diagnostics of a stage rebuild: seconds spent in Python garbage collections that ran inside
+    it and the device memory the caching allocator had to newly reserve (hipMalloc) for it — the
+    two suspects behind rebuilds 2-3x slower than the median (profiles/r5_cfg_full.jsonl)."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.gc_s = 0.0
+        self._t = 0.0
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self._t = time.perf_counter()
+        else:
+            self.gc_s += time.perf_counter() - self._t
+
+    def __enter__(self):
+        self.res0 = torch.cuda.memory_reserved(self.device) if self.device.type == "cuda" else 0
+        gc.callbacks.append(self._cb)
+        return self
+
+    def __exit__(self, *exc):
+        gc.callbacks.remove(self._cb)
+        res1 = torch.cuda.memory_reserved(self.device) if self.device.type == "cuda" else 0
+        self.new_reserved = max(0, res1 - self.res0)
+        return False
 
 
 class ReshardMixin:
@@ -69,7 +98,11 @@ class ReshardMixin:
             if ph.get("flattened_params"):
                 flat.append(max(0.0, ph["rebuild_s"] - ph["materialized_params"] * mat_rate) / ph["flattened_params"])
             groups.append(ph.get("groups_s", 0.0))
-        med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+        def med(v):   # true median (an even count averages the middle two: the upper one alone let
+            #           one slow first re-shard set the next prediction, r5_cfg_full.jsonl config 5 s1)
+            v = sorted(v)
+            n = len(v)
+            return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
         return {"copy_s_per_byte": med(copy), "flatten_s_per_param": med(flat),
                 "materialize_s_per_param": mat_rate, "groups_s": med(groups)}
 
@@ -352,10 +385,13 @@ class ReshardMixin:
                 reuse[a + k] = m
         self.plan = new_plan
         self.stages = {}
-        self._build(layer_modules=reuse)
+        with _RebuildProbe(self.device) as probe:
+            self._build(layer_modules=reuse)
         del reuse
         bt = self._build_times
         ph["rebuild_s"] = bt["materialize_s"] + bt["flatten_s"]
+        ph["rebuild_gc_s"] = probe.gc_s
+        ph["rebuild_new_reserved_bytes"] = probe.new_reserved
         ph["groups_s"] = bt["groups_s"]
         t3 = time.perf_counter()
         for node, st in self.stages.items():
