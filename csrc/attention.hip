@@ -44,12 +44,14 @@ static int dkdv_ns() {
 }
 
 // dK/dV register prefetch depth (tiles ahead): TDL_ATTN_DKDV_PF=1|2 (default 2).
-static int dkdv_pf() {
-    static int pf = [] {
-        const char* e = std::getenv("TDL_ATTN_DKDV_PF");
-        return (e && e[0] == '1') ? 1 : 2;
-    }();
-    return pf;
+static int dq_pf() {   // dQ kernel K/V prefetch depth (TDL_ATTN_DQ_PF = 1 | 2), read per call
+    const char* e = std::getenv("TDL_ATTN_DQ_PF");
+    return (e && e[0] == '2') ? 2 : 1;
+}
+
+static int dkdv_pf() {   // read per call: in-process A/B
+    const char* e = std::getenv("TDL_ATTN_DKDV_PF");
+    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
 }
 
 // waves per workgroup of the attention kernels: TDL_ATTN_WAVES=4|8 (read per launch: in-process A/B)
@@ -488,8 +490,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     // register staging of the next tile(s): PF = 1 loads tile t+1 during tile t; PF = 2 loads
     // tile t+2 during tile t (tile t+1 already sits in registers), so a load has two tiles of
     // compute (~1.5k cycles) to land instead of one (PMC: 47 % of wave cycles waiting)
-    uint4 qn[NS], dn[NS];
+    uint4 qn[NS], dn[NS];     // tile t + 1
     float ln = 0.f, dln = 0.f;
+    uint4 qm[NS], dm[NS];     // tile t + 2 (PF = 3: a load then has two tiles of compute to land)
+    float lm = 0.f, dlm = 0.f;
     auto load_tile = [&](int t0, uint4 (&q)[NS], uint4 (&d)[NS], float& l, float& dl) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
@@ -501,13 +505,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
             dl = delta_row[t0 + tid];
         }
     };
-    if (PF == 2 && q_start + BQ < T) load_tile(q_start + BQ, qn, dn, ln, dln);
+    if (PF >= 2 && q_start + BQ < T) load_tile(q_start + BQ, qn, dn, ln, dln);
+    if (PF == 3 && q_start + 2 * BQ < T) load_tile(q_start + 2 * BQ, qm, dm, lm, dlm);
     int buf = 0;
     for (int qt = q_start; qt < T; qt += BQ) {
         const bool has_next = qt + BQ < T;
         uint4 qf[NS], df[NS];
         float lf = 0.f, dlf = 0.f;
-        if (PF == 2) {
+        if (PF == 3) {
+            if (qt + 3 * BQ < T) load_tile(qt + 3 * BQ, qf, df, lf, dlf);
+        } else if (PF == 2) {
             if (qt + 2 * BQ < T) load_tile(qt + 2 * BQ, qf, df, lf, dlf);
         } else if (has_next) {
             load_tile(qt + BQ, qn, dn, ln, dln);
@@ -597,7 +604,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
         }
         __syncthreads();
         buf ^= 1;
-        if (PF == 2) {
+        if (PF == 3) {
+#pragma unroll
+            for (int j = 0; j < NS; ++j) {
+                qn[j] = qm[j];
+                dn[j] = dm[j];
+                qm[j] = qf[j];
+                dm[j] = df[j];
+            }
+            ln = lm;
+            dln = dlm;
+            lm = lf;
+            dlm = dlf;
+        } else if (PF == 2) {
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
                 qn[j] = qf[j];
@@ -659,7 +678,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
 // dP^T = V.dO^T and S^T = K.Q^T (row-read A), dS^T = P^T * (dP^T - delta) in registers, then
 // dQ^T += K^T.dS^T with K^T from the transposed read of a plain K image and dS^T as the B operand.
 // No atomics, no LDS round trip for dS.
-template <bool CAUSAL, int NW = 4>
+template <bool CAUSAL, int NW = 4, int PF = 1>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ out,
                                                           float* __restrict__ delta,
@@ -712,17 +731,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
         nkb = lim < nkb ? lim : nkb;
     }
     // staging registers as named scalars (an indexed array lands in scratch)
-    uint4 kreg0, kreg1, vreg0, vreg1;
+    // PF = 2: tile kb + 2 is loaded into a second set during tile kb (two tiles of compute to land)
+    uint4 kreg0, kreg1, vreg0, vreg1, kx0, kx1, vx0, vx1;
     const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
-    auto gload = [&](int kb) {
+    auto gload_to = [&](int kb, uint4& k0, uint4& k1, uint4& v0, uint4& v1) {
         const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
-        kreg0 = *(const uint4*)(kbase + g0);
-        vreg0 = *(const uint4*)(vbase + g0);
+        k0 = *(const uint4*)(kbase + g0);
+        v0 = *(const uint4*)(vbase + g0);
         if constexpr (NW == 4) {
-            kreg1 = *(const uint4*)(kbase + g1);
-            vreg1 = *(const uint4*)(vbase + g1);
+            k1 = *(const uint4*)(kbase + g1);
+            v1 = *(const uint4*)(vbase + g1);
         }
     };
+    auto gload = [&](int kb) { gload_to(kb, kreg0, kreg1, vreg0, vreg1); };
     auto sstore = [&](int buf) {
         *(uint4*)(Kr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
         *(uint4*)(Kp[buf] + swz_tr(srow0, sch * 8)) = kreg0;
@@ -735,11 +756,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
     };
     gload(0);
     sstore(0);
+    if (PF == 2 && nkb > 1) gload(1);
     __syncthreads();
     for (int kb = 0; kb < nkb; ++kb) {
         const int buf = kb & 1;
         const bool has_next = kb + 1 < nkb;
-        if (has_next) gload(kb + 1);
+        if (PF == 2) {
+            if (kb + 2 < nkb) gload_to(kb + 2, kx0, kx1, vx0, vx1);
+        } else if (has_next) {
+            gload(kb + 1);
+        }
         const bf16_t* Kr_ = Kr[buf];
         const bf16_t* Kp_ = Kp[buf];
         const bf16_t* Vr_ = Vr[buf];
@@ -789,6 +815,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
         }
         if (has_next) sstore(buf ^ 1);
         __syncthreads();
+        if (PF == 2) {
+            kreg0 = kx0;
+            vreg0 = vx0;
+            if constexpr (NW == 4) {
+                kreg1 = kx1;
+                vreg1 = vx1;
+            }
+        }
     }
     bf16_t* qrow = dqkv + ((size_t)b * T + qi) * ldq + hd * HD;
 #pragma unroll
@@ -848,9 +882,11 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     const bool w8 = causal && T % 256 == 0;
     if (causal) {
         if (w8 && attn_waves(1) == 8) attn_bwd_dq_kernel<true, 8><<<g8, 512, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
+        else if (dq_pf() == 2) attn_bwd_dq_kernel<true, 4, 2><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         if (w8 && attn_waves(2) == 8) attn_bwd_dkdv_kernel<true, 1, 2, 8><<<g8, 512, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_pf() == 3) attn_bwd_dkdv_kernel<true, 1, 3><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
