@@ -34,6 +34,12 @@ CONFIGS = {
     "liar": dict(attack=dict(attack_types=["model_poisoning"], intensity=0.05, lie_integrity=True), targets=[6]),
     "byz1m": dict(attack=dict(attack_types=["byzantine"], intensity=0.5, micro_batches=1), targets=[2],
                   cfg=dict(audit_targeted=True)),
+    # round 5: adaptive attacker (knows the job seed; hides from the public sketch window): rewrite after
+    # the backward / one micro-batch's contribution inside it, k = 2 of M = 8 audited per step
+    "adapt": dict(attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip", adaptive=True),
+                  targets=[3]),
+    "adapt1m": dict(attack=dict(attack_types=["gradient_poisoning"], gradient_mode="sign_flip", adaptive=True,
+                                micro_batches=1), targets=[3], cfg=dict(audit_micro_k=2)),
     "clean": dict(attack=None, targets=[]),
 }
 
