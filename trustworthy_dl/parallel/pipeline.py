@@ -45,7 +45,7 @@ from .commitments import CommitmentMixin
 from .dp import DataParallelMixin
 from .engine_config import EngineConfig, _resolve_dtype, split_micro  # noqa: F401  (re-exported)
 from .partition import make_plan
-from .reshard import ReshardMixin
+from .reshard import ReshardMixin, no_gc
 from .schedule import ScheduleMixin
 from .shadows import ShadowMixin
 from .stage import Stage, tied_groups
@@ -130,7 +130,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         base = self.replica * self.pp
         self.plan = make_plan(self.costs, [base + i for i in range(n_stages)], 0, cfg.balanced_partition)
         self._init_trust_state()
-        self._build()
+        with no_gc():   # the build's timings calibrate the re-shard estimate: no GC pause inside
+            self._build()
         self._init_build_times = dict(self._build_times)
         self.link_meter = LinkMeter(150e9 if self.device.type == "cuda" else 2e9)
         self.heartbeat = None

@@ -23,6 +23,23 @@ from .stage import Stage
 logger = logging.getLogger(__name__)
 
 
+class no_gc:
+    """Automatic Python garbage collection off for a block (re-enabled on exit if it was on).  A
+    generation-2 collection over the engine's module graph costs 70-145 ms; landing inside a
+    re-shard it tripled the measured rebuild and skewed the calibration (r5_cfg_full2.jsonl
+    ``rebuild_gc_s``).  The collection then runs at a later allocation instead."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
+
+
 class _RebuildProbe:
     """Diagnostics of a stage rebuild: seconds spent in Python garbage collections that ran inside
     it and the device memory the caching allocator had to newly reserve (hipMalloc) for it — the
@@ -160,7 +177,8 @@ class ReshardMixin:
                       any(self.plan.owner_of_layer(li) == c for c in compromised))
         predicted = self.estimate_migration_time(to_move, plan=new_plan)   # before the move: a prediction
         t0 = time.perf_counter()
-        moved = self._migrate(new_plan, restore={c: sources[c] for c in restored}, fresh=fresh, ckpt=from_ckpt)
+        with no_gc():
+            moved = self._migrate(new_plan, restore={c: sources[c] for c in restored}, fresh=fresh, ckpt=from_ckpt)
         dt = time.perf_counter() - t0
         self.excluded = sorted(set(self.excluded) | set(compromised))
         for c in compromised:     # the tampered weights now live nowhere (restored or re-placed)
