@@ -51,12 +51,17 @@ static int dq_pf() {   // dQ kernel K/V prefetch depth (TDL_ATTN_DQ_PF = 1 | 2),
 
 static int dkdv_pf() {   // read per call: in-process A/B
     const char* e = std::getenv("TDL_ATTN_DKDV_PF");
-    return (e && (e[0] == '1' || e[0] == '3')) ? e[0] - '0' : 2;
+    return (e && e[0] == '1') ? 1 : 2;
 }
 
 // waves per workgroup of the attention kernels: TDL_ATTN_WAVES=4|8 (read per launch: in-process A/B)
 // waves per workgroup of kernel i (0 forward, 1 dQ, 2 dK/dV): TDL_ATTN_WAVES = one digit for all
 // three or three digits ("844"); 8 waves stage each K/V (Q/dO) tile once for twice the rows
+// longest sequence the dK/dV kernel stages lse / delta for (2 x 16 KiB of LDS per workgroup)
+#define ATTN_BWD_MAXT 4096
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their no-wait maxima), gfx9 encoding
+#define VMCNT0 0x0F70
+
 static int attn_waves(int i) {
     static const char dflt[] = "844";
     const char* e = std::getenv("TDL_ATTN_WAVES");
@@ -78,6 +83,22 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+
+// Operand prefetch the compiler does not track: a 16-byte global load issued from inline asm, and a
+// counted wait that hands the registers back (as "+v" operands, so nothing reads them before the
+// wait).  The compiler's own waits stay safe — the extra loads only make them stricter — but it no
+// longer drains a younger prefetch set before storing an older one (its bookkeeping across the
+// loop's back edge cannot prove the order; attn_bwd_dkdv_kernel PF = 2).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4_t gload16_async(const void* p) {
+    u32x4_t v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait2(u32x4_t& a, u32x4_t& b) {
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
 
 __device__ __forceinline__ short4_t tr_read(const bf16_t* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
@@ -214,6 +235,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
     gload(0);
     sstore(0);
     __syncthreads();
+    // the Q fragments have landed before the loop (an empty asm consuming them pins their loads
+    // and the wait here): otherwise the compiler sinks the loads into the loop's first tile and,
+    // unsure of them, drains every K / V prefetch before a tile's first MFMA (s_waitcnt vmcnt(0))
+    asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));
     if (PF == 2 && nkb > 1) gload(1);
 
     for (int kb = 0; kb < nkb; ++kb) {
@@ -430,8 +455,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t Qw[2][BQ * HD];
     __shared__ __attribute__((aligned(16))) bf16_t dOw[2][BQ * HD];
-    __shared__ __attribute__((aligned(16))) float lse_s[2][BQ];  // lse pre-scaled by log2(e)
-    __shared__ __attribute__((aligned(16))) float delta_s[2][BQ];
+    // lse (pre-scaled by log2(e)) and delta of every query this workgroup visits, staged once in the
+    // prologue: no per-tile scalar loads in the loop (their waits drained the operand prefetch)
+    __shared__ __attribute__((aligned(16))) float lse_s[ATTN_BWD_MAXT];
+    __shared__ __attribute__((aligned(16))) float delta_s[ATTN_BWD_MAXT];
 
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile-level branches stay scalar
@@ -481,149 +508,164 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
             *(uint4*)(dOw[0] + row * HD + swz) = d;
         }
     }
-    if (tid < BQ) {
-        lse_s[0][tid] = lse_row[q_start + tid] * LOG2E;
-        delta_s[0][tid] = delta_row[q_start + tid];
+    for (int i = tid; i < T - q_start; i += 64 * NW) {
+        lse_s[i] = lse_row[q_start + i] * LOG2E;
+        delta_s[i] = delta_row[q_start + i];
     }
+    // every prologue load (K / V fragments included) has landed before the loop: the compiler's
+    // wait bookkeeping then never has to drain the loop's prefetches on their account
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
     __syncthreads();
 
-    // register staging of the next tile(s): PF = 1 loads tile t+1 during tile t; PF = 2 loads
-    // tile t+2 during tile t (tile t+1 already sits in registers), so a load has two tiles of
-    // compute (~1.5k cycles) to land instead of one (PMC: 47 % of wave cycles waiting)
-    uint4 qn[NS], dn[NS];     // tile t + 1
-    float ln = 0.f, dln = 0.f;
-    uint4 qm[NS], dm[NS];     // tile t + 2 (PF = 3: a load then has two tiles of compute to land)
-    float lm = 0.f, dlm = 0.f;
-    auto load_tile = [&](int t0, uint4 (&q)[NS], uint4 (&d)[NS], float& l, float& dl) {
+    // Register staging of the next tiles.  A tile's global loads land in a register set that is
+    // stored to LDS one iteration later (PF = 1) or two (PF = 2).  With PF = 2 the loop is unrolled
+    // by two and the two register sets swap roles statically: a copy from the "loaded" set into the
+    // "to store" set would make the wave wait for the loads it just issued (ISA of the r4 form:
+    // s_waitcnt vmcnt before the v_mov rotation, so the loads had one tile to land, not two).  The
+    // lse scaling is applied when the value is stored to LDS, not when it arrives, for the same
+    // reason (a multiply of the just-loaded lse made wave 0 wait for it every tile).
+    auto load_tile = [&](int t0, uint4 (&q)[NS], uint4 (&d)[NS]) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             if (stq) q[j] = *(const uint4*)(qbase + (size_t)(t0 + srow + 32 * j) * ldq + sch * 8);
             if (std_) d[j] = *(const uint4*)(dobase + (size_t)(t0 + srow + 32 * j) * ldo + sch * 8);
         }
-        if (tid < BQ) {
-            l = lse_row[t0 + tid] * LOG2E;
-            dl = delta_row[t0 + tid];
-        }
     };
-    if (PF >= 2 && q_start + BQ < T) load_tile(q_start + BQ, qn, dn, ln, dln);
-    if (PF == 3 && q_start + 2 * BQ < T) load_tile(q_start + 2 * BQ, qm, dm, lm, dlm);
-    int buf = 0;
-    for (int qt = q_start; qt < T; qt += BQ) {
-        const bool has_next = qt + BQ < T;
-        uint4 qf[NS], df[NS];
-        float lf = 0.f, dlf = 0.f;
-        if (PF == 3) {
-            if (qt + 3 * BQ < T) load_tile(qt + 3 * BQ, qf, df, lf, dlf);
-        } else if (PF == 2) {
-            if (qt + 2 * BQ < T) load_tile(qt + 2 * BQ, qf, df, lf, dlf);
-        } else if (has_next) {
-            load_tile(qt + BQ, qn, dn, ln, dln);
-        }
+    auto store_tile = [&](int nb, const uint4 (&q)[NS], const uint4 (&d)[NS]) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
-            const int qs = qt + 32 * j;   // this sub-tile's first query
-            if (CAUSAL && qs + 31 < k0) continue;
-            const bf16_t* Qb = Qs[buf] + 32 * j * HD;
-            const bf16_t* dOb = dOs[buf] + 32 * j * HD;
-            const bf16_t* Qr = Qw[buf] + 32 * j * HD;
-            const bf16_t* dOr = dOw[buf] + 32 * j * HD;
-            const float* lsb = lse_s[buf] + 32 * j;
-            const float* dlb = delta_s[buf] + 32 * j;
-            f32x16 sacc = {}, dpacc = {};
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int c = ((2 * s + h) ^ (r & 7)) * 8;
-                const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qr + r * HD + c));
-                const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOr + r * HD + c));
-                sacc = MFMA32(aq, kf[s], sacc);
-                dpacc = MFMA32(ad, vf[s], dpacc);
+            const int row = srow + 32 * j;
+            if (stq) {
+                *(uint4*)(Qs[nb] + swz_tr(row, sch * 8)) = q[j];
+                *(uint4*)(Qw[nb] + row * HD + swz) = q[j];
             }
-            // the causal mask matters only on the tiles that straddle this wave's diagonal (a few
-            // of T / 32): elsewhere the per-element compare + select is dropped (VALU-bound loop)
-            // lse / delta of the lane's 16 query rows: 4 groups of 4 consecutive rows -> 4 + 4
-            // 16-byte LDS reads instead of 32 scalar ones
-            float lsv[16], dlv[16];
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const float4 a = *(const float4*)(lsb + 8 * g4 + 4 * h);
-                const float4 c = *(const float4*)(dlb + 8 * g4 + 4 * h);
-                lsv[4 * g4] = a.x; lsv[4 * g4 + 1] = a.y; lsv[4 * g4 + 2] = a.z; lsv[4 * g4 + 3] = a.w;
-                dlv[4 * g4] = c.x; dlv[4 * g4 + 1] = c.y; dlv[4 * g4 + 2] = c.z; dlv[4 * g4 + 3] = c.w;
-            }
-            if (CAUSAL && qs < k0 + 31) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
-                    float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
-                    if (kj > qs + ql) p = 0.f;
-                    sacc[i] = p;
-                    dpacc[i] = p * (dpacc[i] - dlv[i]);
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
-                    sacc[i] = p;
-                    dpacc[i] = p * (dpacc[i] - dlv[i]);
-                }
-            }
-            const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
-            const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int qr = 16 * s2 + 4 * h + tq;
-                const bf16x8_t pb = s2 == 0 ? pb0 : pb1;
-                const bf16x8_t dsb = s2 == 0 ? db0 : db1;
-                const bf16x8_t ado0 = tr_pair(dOb + swz_tr(qr, tcol), dOb + swz_tr(qr + 8, tcol));
-                const bf16x8_t ado1 = tr_pair(dOb + swz_tr(qr, 32 + tcol), dOb + swz_tr(qr + 8, 32 + tcol));
-                dv0 = MFMA32(ado0, pb, dv0);
-                dv1 = MFMA32(ado1, pb, dv1);
-                const bf16x8_t aq0 = tr_pair(Qb + swz_tr(qr, tcol), Qb + swz_tr(qr + 8, tcol));
-                const bf16x8_t aq1 = tr_pair(Qb + swz_tr(qr, 32 + tcol), Qb + swz_tr(qr + 8, 32 + tcol));
-                dk0 = MFMA32(aq0, dsb, dk0);
-                dk1 = MFMA32(aq1, dsb, dk1);
+            if (std_) {
+                *(uint4*)(dOs[nb] + swz_tr(row, sch * 8)) = d[j];
+                *(uint4*)(dOw[nb] + row * HD + swz) = d[j];
             }
         }
-        if (has_next) {
+    };
+    // the tile at query offset qt, staged in LDS buffer `buf`
+    auto compute_tile = [&](int qt, int buf) {
 #pragma unroll
             for (int j = 0; j < NS; ++j) {
-                const int row = srow + 32 * j;
-                if (stq) {
-                    *(uint4*)(Qs[buf ^ 1] + swz_tr(row, sch * 8)) = qn[j];
-                    *(uint4*)(Qw[buf ^ 1] + row * HD + swz) = qn[j];
+                const int qs = qt + 32 * j;   // this sub-tile's first query
+                if (CAUSAL && qs + 31 < k0) continue;
+                const bf16_t* Qb = Qs[buf] + 32 * j * HD;
+                const bf16_t* dOb = dOs[buf] + 32 * j * HD;
+                const bf16_t* Qr = Qw[buf] + 32 * j * HD;
+                const bf16_t* dOr = dOw[buf] + 32 * j * HD;
+                const float* lsb = lse_s + (qs - q_start);
+                const float* dlb = delta_s + (qs - q_start);
+                f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int c = ((2 * s + h) ^ (r & 7)) * 8;
+                    const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qr + r * HD + c));
+                    const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOr + r * HD + c));
+                    sacc = MFMA32(aq, kf[s], sacc);
+                    dpacc = MFMA32(ad, vf[s], dpacc);
                 }
-                if (std_) {
-                    *(uint4*)(dOs[buf ^ 1] + swz_tr(row, sch * 8)) = dn[j];
-                    *(uint4*)(dOw[buf ^ 1] + row * HD + swz) = dn[j];
+                // the causal mask matters only on the tiles that straddle this wave's diagonal (a few
+                // of T / 32): elsewhere the per-element compare + select is dropped (VALU-bound loop)
+                // lse / delta of the lane's 16 query rows: 4 groups of 4 consecutive rows -> 4 + 4
+                // 16-byte LDS reads instead of 32 scalar ones
+                float lsv[16], dlv[16];
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const float4 a = *(const float4*)(lsb + 8 * g4 + 4 * h);
+                    const float4 c = *(const float4*)(dlb + 8 * g4 + 4 * h);
+                    lsv[4 * g4] = a.x; lsv[4 * g4 + 1] = a.y; lsv[4 * g4 + 2] = a.z; lsv[4 * g4 + 3] = a.w;
+                    dlv[4 * g4] = c.x; dlv[4 * g4 + 1] = c.y; dlv[4 * g4 + 2] = c.z; dlv[4 * g4 + 3] = c.w;
+                }
+                if (CAUSAL && qs < k0 + 31) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int ql = (i & 3) + 8 * (i >> 2) + 4 * h;
+                        float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
+                        if (kj > qs + ql) p = 0.f;
+                        sacc[i] = p;
+                        dpacc[i] = p * (dpacc[i] - dlv[i]);
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
+                        sacc[i] = p;
+                        dpacc[i] = p * (dpacc[i] - dlv[i]);
+                    }
+                }
+                const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
+                const bf16x8_t db0 = cvt8(dpacc, 0), db1 = cvt8(dpacc, 8);
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int qr = 16 * s2 + 4 * h + tq;
+                    const bf16x8_t pb = s2 == 0 ? pb0 : pb1;
+                    const bf16x8_t dsb = s2 == 0 ? db0 : db1;
+                    const bf16x8_t ado0 = tr_pair(dOb + swz_tr(qr, tcol), dOb + swz_tr(qr + 8, tcol));
+                    const bf16x8_t ado1 = tr_pair(dOb + swz_tr(qr, 32 + tcol), dOb + swz_tr(qr + 8, 32 + tcol));
+                    dv0 = MFMA32(ado0, pb, dv0);
+                    dv1 = MFMA32(ado1, pb, dv1);
+                    const bf16x8_t aq0 = tr_pair(Qb + swz_tr(qr, tcol), Qb + swz_tr(qr + 8, tcol));
+                    const bf16x8_t aq1 = tr_pair(Qb + swz_tr(qr, 32 + tcol), Qb + swz_tr(qr + 8, 32 + tcol));
+                    dk0 = MFMA32(aq0, dsb, dk0);
+                    dk1 = MFMA32(aq1, dsb, dk1);
                 }
             }
-            if (tid < BQ) {
-                lse_s[buf ^ 1][tid] = ln;
-                delta_s[buf ^ 1][tid] = dln;
+    };
+    uint4 qa[NS], da[NS];
+    if constexpr (PF == 2) {
+        // two tiles in flight, loads issued from asm with exact counted waits (gload16_async): at
+        // the top of tile t the set holding tile t + 1 (issued two tiles ago) goes to LDS — only the
+        // younger set (tile t + 2, LPS loads per thread) may still be outstanding, so
+        // vmcnt(LPS) — and the freed set receives tile t + 3.  NS = 1 here (static_assert below).
+        static_assert(NS == 1, "asm prefetch path: one 32-row slab per operand");
+        constexpr int LPS = (NW == 4) ? 2 : 1;   // loads per set and thread (Q and dO, or one of them)
+        u32x4_t A0 = {}, A1 = {}, B0 = {}, B1 = {};
+        auto issue = [&](int t0, u32x4_t& x0, u32x4_t& x1) {
+            if (stq) x0 = gload16_async(qbase + (size_t)(t0 + srow) * ldq + sch * 8);
+            if (std_) x1 = gload16_async(dobase + (size_t)(t0 + srow) * ldo + sch * 8);
+        };
+        auto stash = [&](int nb, const u32x4_t& x0, const u32x4_t& x1) {
+            if (stq) {
+                const uint4 q = __builtin_bit_cast(uint4, x0);
+                *(uint4*)(Qs[nb] + swz_tr(srow, sch * 8)) = q;
+                *(uint4*)(Qw[nb] + srow * HD + swz) = q;
             }
+            if (std_) {
+                const uint4 d = __builtin_bit_cast(uint4, x1);
+                *(uint4*)(dOs[nb] + swz_tr(srow, sch * 8)) = d;
+                *(uint4*)(dOw[nb] + srow * HD + swz) = d;
+            }
+        };
+        if (q_start + BQ < T) issue(q_start + BQ, A0, A1);
+        if (q_start + 2 * BQ < T) issue(q_start + 2 * BQ, B0, B1);
+        for (int qt = q_start; qt < T; qt += 2 * BQ) {
+            if (qt + BQ < T) {
+                if (qt + 2 * BQ < T) vm_wait2<LPS>(A0, A1); else vm_wait2<0>(A0, A1);
+                stash(1, A0, A1);
+                if (qt + 3 * BQ < T) issue(qt + 3 * BQ, A0, A1);
+            }
+            compute_tile(qt, 0);
+            __syncthreads();
+            if (qt + BQ >= T) break;
+            if (qt + 2 * BQ < T) {
+                if (qt + 3 * BQ < T) vm_wait2<LPS>(B0, B1); else vm_wait2<0>(B0, B1);
+                stash(0, B0, B1);
+                if (qt + 4 * BQ < T) issue(qt + 4 * BQ, B0, B1);
+            }
+            compute_tile(qt + BQ, 1);
+            __syncthreads();
         }
-        __syncthreads();
-        buf ^= 1;
-        if (PF == 3) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                qn[j] = qm[j];
-                dn[j] = dm[j];
-                qm[j] = qf[j];
-                dm[j] = df[j];
-            }
-            ln = lm;
-            dln = dlm;
-            lm = lf;
-            dlm = dlf;
-        } else if (PF == 2) {
-#pragma unroll
-            for (int j = 0; j < NS; ++j) {
-                qn[j] = qf[j];
-                dn[j] = df[j];
-            }
-            ln = lf;
-            dln = dlf;
+    } else {
+        int buf = 0;
+        for (int qt = q_start; qt < T; qt += BQ) {
+            const bool has_next = qt + BQ < T;
+            if (has_next) load_tile(qt + BQ, qa, da);
+            compute_tile(qt, buf);
+            if (has_next) store_tile(buf ^ 1, qa, da);
+            __syncthreads();
+            buf ^= 1;
         }
     }
     bf16_t* dkrow = dqkv + ((size_t)b * T + kj) * ldq + H * HD + hd * HD;
@@ -868,7 +910,7 @@ TDL_API int tdl_colsum_f32(const float* part, int G, int N, int ld, float* acc, 
 TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse, void* dqkv, float* bias_acc,
                          float* bias_part, float* delta, int B, int T, int H, int D, float scale, int causal,
                          hipStream_t s) {
-    if (D != HD || T % 128 != 0) return (int)hipErrorInvalidValue;
+    if (D != HD || T % 128 != 0 || T > ATTN_BWD_MAXT) return (int)hipErrorInvalidValue;
     if ((bias_acc == nullptr) != (bias_part == nullptr)) return (int)hipErrorInvalidValue;
     // the dQ kernel also produces delta = rowsum(dO * O) for the dK/dV kernel, so it runs first
     const int grid = B * H * (T / 128);
@@ -886,7 +928,6 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
         else attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         if (w8 && attn_waves(2) == 8) attn_bwd_dkdv_kernel<true, 1, 2, 8><<<g8, 512, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else if (dkdv_pf() == 3) attn_bwd_dkdv_kernel<true, 1, 3><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
