@@ -44,11 +44,6 @@ static int dkdv_ns() {
 }
 
 // dK/dV register prefetch depth (tiles ahead): TDL_ATTN_DKDV_PF=1|2 (default 2).
-static int dq_pf() {   // dQ kernel K/V prefetch depth (TDL_ATTN_DQ_PF = 1 | 2), read per call
-    const char* e = std::getenv("TDL_ATTN_DQ_PF");
-    return (e && e[0] == '2') ? 2 : 1;
-}
-
 static int dkdv_pf() {   // read per call: in-process A/B
     const char* e = std::getenv("TDL_ATTN_DKDV_PF");
     return (e && e[0] == '1') ? 1 : 2;
@@ -83,22 +78,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 __device__ __forceinline__ bf16x8_t as_bf16x8(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
-
-// Operand prefetch the compiler does not track: a 16-byte global load issued from inline asm, and a
-// counted wait that hands the registers back (as "+v" operands, so nothing reads them before the
-// wait).  The compiler's own waits stay safe — the extra loads only make them stricter — but it no
-// longer drains a younger prefetch set before storing an older one (its bookkeeping across the
-// loop's back edge cannot prove the order; attn_bwd_dkdv_kernel PF = 2).
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4_t gload16_async(const void* p) {
-    u32x4_t v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-template <int N>
-__device__ __forceinline__ void vm_wait2(u32x4_t& a, u32x4_t& b) {
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
 
 __device__ __forceinline__ short4_t tr_read(const bf16_t* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4_t*)(p));
@@ -170,11 +149,11 @@ __device__ __forceinline__ float max32(const f32x16& a, const f32x16& b) {
 
 // 1-D grid of B*H*(T/128) workgroups mapped by head_xcd_map: one head's query blocks run back to
 // back on one XCD, longest causal rows first (longest-processing-time-first inside each head).
-// PF: K / V register prefetch depth in tiles (1: tile t+1 loads during tile t; 2: tile t+2, so a
-// load has two tiles of compute to land: TDL_ATTN_FWD_PF, read per launch for in-process A/B)
+// K / V are register-staged one tile ahead (tile t+1 loads during tile t; a second in-flight set
+// measured flat in r4, profiles/r4_attn_fwd_valu_ab.txt).
 // NW: waves per workgroup (32 queries each): 8 waves share every staged K / V tile between twice
 // the queries (half the K / V traffic and LDS writes per MFMA of the 4-wave form)
-template <bool CAUSAL, int PF = 1, bool OPT = false, int NW = 4>
+template <bool CAUSAL, bool OPT = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse, int T, int H, int nbh, float scale_log2) {
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
@@ -211,8 +190,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
     // per 64-key tile; the NEXT tile is loaded into registers while the current one computes (one
     // barrier per tile, LDS double-buffered); staging registers as named scalars (an indexed array
     // lands in scratch)
-    uint4 kreg0, kreg1, vreg0, vreg1;      // tile t+1
-    uint4 kf0, kf1, vf0, vf1;              // tile t+2 (PF = 2)
+    uint4 kreg0 = {}, kreg1 = {}, vreg0 = {}, vreg1 = {};   // tile t+1 (PF = 1) / the set being stored
     const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
     auto gload_to = [&](int kb, uint4& k0, uint4& k1, uint4& v0, uint4& v1) {
         const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
@@ -239,16 +217,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
     // and the wait here): otherwise the compiler sinks the loads into the loop's first tile and,
     // unsure of them, drains every K / V prefetch before a tile's first MFMA (s_waitcnt vmcnt(0))
     asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));
-    if (PF == 2 && nkb > 1) gload(1);
-
-    for (int kb = 0; kb < nkb; ++kb) {
-        const int buf = kb & 1;
-        const bool has_next = kb + 1 < nkb;
-        if (PF == 2) {
-            if (kb + 2 < nkb) gload_to(kb + 2, kf0, kf1, vf0, vf1);
-        } else if (has_next) {
-            gload(kb + 1);
-        }
+    // the tile of keys kb, staged in LDS buffer `buf`
+    auto compute_tile = [&](int kb, int buf) {
         const bf16_t* K_ = Ks[buf];
         const bf16_t* V_ = Vs[buf];
         const bool active = !CAUSAL || (kb * BN <= q0 + 31);
@@ -346,14 +316,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
                     o1 = MFMA32(v1, pf, o1);
                 }
         }
+    };
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int buf = kb & 1;
+        const bool has_next = kb + 1 < nkb;
+        if (has_next) gload(kb + 1);
+        compute_tile(kb, buf);
         if (has_next) sstore(buf ^ 1);
         __syncthreads();
-        if (PF == 2) {
-            kreg0 = kf0;
-            kreg1 = kf1;
-            vreg0 = vf0;
-            vreg1 = vf1;
-        }
     }
     if (qi < T) {
         const float inv_l = 1.f / l;
@@ -376,25 +346,21 @@ TDL_API int tdl_attn_fwd(const void* qkv, void* out, float* lse, void* unused, i
     if (D != HD || T % 64 != 0) return (int)hipErrorInvalidValue;
     if (T % 128 != 0) return (int)hipErrorInvalidValue;
     const float sl2 = scale * 1.4426950408889634f;
-    const char* pfe = std::getenv("TDL_ATTN_FWD_PF");
-    const bool pf2 = pfe && pfe[0] == '2';
     const char* ope = std::getenv("TDL_ATTN_FWD_OPT");   // packed softmax (default); 0 = scalar form
     const bool opt = !(ope && ope[0] == '0');
     auto Q = (const bf16_t*)qkv;
     auto O = (bf16_t*)out;
     const int nb = attn_nbh_arg(B * H);
     if (causal && opt && attn_waves(0) == 8 && T % 256 == 0) {
-        attn_fwd_kernel<true, 1, true, 8><<<B * H * (T / 256), 512, 0, s>>>(Q, O, lse, T, H, nb, sl2);
+        attn_fwd_kernel<true, true, 8><<<B * H * (T / 256), 512, 0, s>>>(Q, O, lse, T, H, nb, sl2);
         TDL_LAUNCH_CHECK();
     }
     const int grid = B * H * (T / 128);
     if (causal) {
-        if (opt) attn_fwd_kernel<true, 1, true><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
-        else if (pf2) attn_fwd_kernel<true, 2><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
-        else attn_fwd_kernel<true, 1><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
+        if (opt) attn_fwd_kernel<true, true><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
+        else attn_fwd_kernel<true><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
     } else {
-        if (pf2) attn_fwd_kernel<false, 2><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
-        else attn_fwd_kernel<false, 1><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
+        attn_fwd_kernel<false><<<grid, 256, 0, s>>>(Q, O, lse, T, H, nb, sl2);
     }
     TDL_LAUNCH_CHECK();
 }
@@ -451,10 +417,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     constexpr int BK = 32 * NW, BQ = 32 * NS;
     // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
     // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
-    __shared__ __attribute__((aligned(16))) bf16_t Qs[2][BQ * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t dOs[2][BQ * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t Qw[2][BQ * HD];
-    __shared__ __attribute__((aligned(16))) bf16_t dOw[2][BQ * HD];
+    // two buffers x four images: Q / dO, plain (transposed reads) and row-swizzled (row reads)
+    constexpr int IMG = BQ * HD;
+    __shared__ __attribute__((aligned(16))) bf16_t tiles[8 * IMG];
+    auto Qs = [&](int b) { return tiles + b * IMG; };
+    auto dOs = [&](int b) { return tiles + (2 + b) * IMG; };
+    auto Qw = [&](int b) { return tiles + (4 + b) * IMG; };
+    auto dOw = [&](int b) { return tiles + (6 + b) * IMG; };
     // lse (pre-scaled by log2(e)) and delta of every query this workgroup visits, staged once in the
     // prologue: no per-tile scalar loads in the loop (their waits drained the operand prefetch)
     __shared__ __attribute__((aligned(16))) float lse_s[ATTN_BWD_MAXT];
@@ -499,13 +468,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
         const int row = srow + 32 * j;
         if (stq) {
             const uint4 q = *(const uint4*)(qbase + (size_t)(q_start + row) * ldq + sch * 8);
-            *(uint4*)(Qs[0] + swz_tr(row, sch * 8)) = q;
-            *(uint4*)(Qw[0] + row * HD + swz) = q;
+            *(uint4*)(Qs(0) + swz_tr(row, sch * 8)) = q;
+            *(uint4*)(Qw(0) + row * HD + swz) = q;
         }
         if (std_) {
             const uint4 d = *(const uint4*)(dobase + (size_t)(q_start + row) * ldo + sch * 8);
-            *(uint4*)(dOs[0] + swz_tr(row, sch * 8)) = d;
-            *(uint4*)(dOw[0] + row * HD + swz) = d;
+            *(uint4*)(dOs(0) + swz_tr(row, sch * 8)) = d;
+            *(uint4*)(dOw(0) + row * HD + swz) = d;
         }
     }
     for (int i = tid; i < T - q_start; i += 64 * NW) {
@@ -536,12 +505,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
         for (int j = 0; j < NS; ++j) {
             const int row = srow + 32 * j;
             if (stq) {
-                *(uint4*)(Qs[nb] + swz_tr(row, sch * 8)) = q[j];
-                *(uint4*)(Qw[nb] + row * HD + swz) = q[j];
+                *(uint4*)(Qs(nb) + swz_tr(row, sch * 8)) = q[j];
+                *(uint4*)(Qw(nb) + row * HD + swz) = q[j];
             }
             if (std_) {
-                *(uint4*)(dOs[nb] + swz_tr(row, sch * 8)) = d[j];
-                *(uint4*)(dOw[nb] + row * HD + swz) = d[j];
+                *(uint4*)(dOs(nb) + swz_tr(row, sch * 8)) = d[j];
+                *(uint4*)(dOw(nb) + row * HD + swz) = d[j];
             }
         }
     };
@@ -551,10 +520,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
             for (int j = 0; j < NS; ++j) {
                 const int qs = qt + 32 * j;   // this sub-tile's first query
                 if (CAUSAL && qs + 31 < k0) continue;
-                const bf16_t* Qb = Qs[buf] + 32 * j * HD;
-                const bf16_t* dOb = dOs[buf] + 32 * j * HD;
-                const bf16_t* Qr = Qw[buf] + 32 * j * HD;
-                const bf16_t* dOr = dOw[buf] + 32 * j * HD;
+                const bf16_t* Qb = Qs(buf) + 32 * j * HD;
+                const bf16_t* dOb = dOs(buf) + 32 * j * HD;
+                const bf16_t* Qr = Qw(buf) + 32 * j * HD;
+                const bf16_t* dOr = dOw(buf) + 32 * j * HD;
                 const float* lsb = lse_s + (qs - q_start);
                 const float* dlb = delta_s + (qs - q_start);
                 f32x16 sacc = {}, dpacc = {};
@@ -615,46 +584,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     };
     uint4 qa[NS], da[NS];
     if constexpr (PF == 2) {
-        // two tiles in flight, loads issued from asm with exact counted waits (gload16_async): at
-        // the top of tile t the set holding tile t + 1 (issued two tiles ago) goes to LDS — only the
-        // younger set (tile t + 2, LPS loads per thread) may still be outstanding, so
-        // vmcnt(LPS) — and the freed set receives tile t + 3.  NS = 1 here (static_assert below).
-        static_assert(NS == 1, "asm prefetch path: one 32-row slab per operand");
-        constexpr int LPS = (NW == 4) ? 2 : 1;   // loads per set and thread (Q and dO, or one of them)
-        u32x4_t A0 = {}, A1 = {}, B0 = {}, B1 = {};
-        auto issue = [&](int t0, u32x4_t& x0, u32x4_t& x1) {
-            if (stq) x0 = gload16_async(qbase + (size_t)(t0 + srow) * ldq + sch * 8);
-            if (std_) x1 = gload16_async(dobase + (size_t)(t0 + srow) * ldo + sch * 8);
-        };
-        auto stash = [&](int nb, const u32x4_t& x0, const u32x4_t& x1) {
-            if (stq) {
-                const uint4 q = __builtin_bit_cast(uint4, x0);
-                *(uint4*)(Qs[nb] + swz_tr(srow, sch * 8)) = q;
-                *(uint4*)(Qw[nb] + srow * HD + swz) = q;
-            }
-            if (std_) {
-                const uint4 d = __builtin_bit_cast(uint4, x1);
-                *(uint4*)(dOs[nb] + swz_tr(srow, sch * 8)) = d;
-                *(uint4*)(dOw[nb] + srow * HD + swz) = d;
-            }
-        };
-        if (q_start + BQ < T) issue(q_start + BQ, A0, A1);
-        if (q_start + 2 * BQ < T) issue(q_start + 2 * BQ, B0, B1);
+        // two register sets, the loop unrolled by two so they swap roles statically: set A holds
+        // tile qt + BQ (stored at the end of tile qt), set B receives tile qt + 2 BQ.  (An LDS-DMA
+        // ring was tried: the compiler drains every in-flight copy before the first LDS read of a
+        // tile — it cannot tell the ring's buffers apart — so it gained nothing.)
+        uint4 qb[NS], db[NS];
+        if (q_start + BQ < T) load_tile(q_start + BQ, qa, da);
         for (int qt = q_start; qt < T; qt += 2 * BQ) {
-            if (qt + BQ < T) {
-                if (qt + 2 * BQ < T) vm_wait2<LPS>(A0, A1); else vm_wait2<0>(A0, A1);
-                stash(1, A0, A1);
-                if (qt + 3 * BQ < T) issue(qt + 3 * BQ, A0, A1);
-            }
+            if (qt + 2 * BQ < T) load_tile(qt + 2 * BQ, qb, db);
             compute_tile(qt, 0);
+            if (qt + BQ < T) store_tile(1, qa, da);
             __syncthreads();
             if (qt + BQ >= T) break;
-            if (qt + 2 * BQ < T) {
-                if (qt + 3 * BQ < T) vm_wait2<LPS>(B0, B1); else vm_wait2<0>(B0, B1);
-                stash(0, B0, B1);
-                if (qt + 4 * BQ < T) issue(qt + 4 * BQ, B0, B1);
-            }
+            if (qt + 3 * BQ < T) load_tile(qt + 3 * BQ, qa, da);
             compute_tile(qt + BQ, 1);
+            if (qt + 2 * BQ < T) store_tile(0, qb, db);
             __syncthreads();
         }
     } else {
@@ -720,7 +664,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
 // dP^T = V.dO^T and S^T = K.Q^T (row-read A), dS^T = P^T * (dP^T - delta) in registers, then
 // dQ^T += K^T.dS^T with K^T from the transposed read of a plain K image and dS^T as the B operand.
 // No atomics, no LDS round trip for dS.
-template <bool CAUSAL, int NW = 4, int PF = 1>
+// (a second in-flight K / V set — two tiles of prefetch — spills at 256 VGPRs: one set)
+template <bool CAUSAL, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dout,
                                                           const float* __restrict__ lse, const bf16_t* __restrict__ out,
                                                           float* __restrict__ delta,
@@ -773,8 +718,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
         nkb = lim < nkb ? lim : nkb;
     }
     // staging registers as named scalars (an indexed array lands in scratch)
-    // PF = 2: tile kb + 2 is loaded into a second set during tile kb (two tiles of compute to land)
-    uint4 kreg0, kreg1, vreg0, vreg1, kx0, kx1, vx0, vx1;
+    uint4 kreg0 = {}, kreg1 = {}, vreg0 = {}, vreg1 = {};
     const int srow0 = tid >> 3, sch = tid & 7, srow1 = srow0 + 32;
     auto gload_to = [&](int kb, uint4& k0, uint4& k1, uint4& v0, uint4& v1) {
         const size_t g0 = (size_t)(kb * BN + srow0) * ldq + sch * 8, g1 = g0 + (size_t)32 * ldq;
@@ -796,18 +740,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
             *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
         }
     };
-    gload(0);
-    sstore(0);
-    if (PF == 2 && nkb > 1) gload(1);
-    __syncthreads();
-    for (int kb = 0; kb < nkb; ++kb) {
-        const int buf = kb & 1;
-        const bool has_next = kb + 1 < nkb;
-        if (PF == 2) {
-            if (kb + 2 < nkb) gload_to(kb + 2, kx0, kx1, vx0, vx1);
-        } else if (has_next) {
-            gload(kb + 1);
-        }
+    // the tile of keys kb, staged in LDS buffer `buf`
+    auto compute_tile = [&](int kb, int buf) {
         const bf16_t* Kr_ = Kr[buf];
         const bf16_t* Kp_ = Kp[buf];
         const bf16_t* Vr_ = Vr[buf];
@@ -855,16 +789,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
                     dq1 = MFMA32(a1, ds, dq1);
                 }
         }
+    };
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int buf = kb & 1;
+        const bool has_next = kb + 1 < nkb;
+        if (has_next) gload(kb + 1);
+        compute_tile(kb, buf);
         if (has_next) sstore(buf ^ 1);
         __syncthreads();
-        if (PF == 2) {
-            kreg0 = kx0;
-            vreg0 = vx0;
-            if constexpr (NW == 4) {
-                kreg1 = kx1;
-                vreg1 = vx1;
-            }
-        }
     }
     bf16_t* qrow = dqkv + ((size_t)b * T + qi) * ldq + hd * HD;
 #pragma unroll
@@ -924,7 +859,6 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     const bool w8 = causal && T % 256 == 0;
     if (causal) {
         if (w8 && attn_waves(1) == 8) attn_bwd_dq_kernel<true, 8><<<g8, 512, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
-        else if (dq_pf() == 2) attn_bwd_dq_kernel<true, 4, 2><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         if (w8 && attn_waves(2) == 8) attn_bwd_dkdv_kernel<true, 1, 2, 8><<<g8, 512, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
         else if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
