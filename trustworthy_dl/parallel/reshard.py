@@ -82,7 +82,9 @@ class ReshardMixin:
         rebuild: stage modules, flat buffers and verifiers of the new plan, at the per-parameter
         rates measured when this engine built its stages (``_build_times``) and refitted from every
         re-shard's measured phases (``_migrate_phases``);
-        groups: communicator set-up of the new plan (cached groups cost nothing).
+        groups: communicator set-up of the new plan (cached groups cost nothing);
+        other: what a re-shard spends outside those phases (device syncs, the fresh shadow ring),
+        measured as wall minus phases.
         The reference uses a fixed 1 GiB/s + 2 s (distributed_trainer.py:354-365)."""
         bw = self.link_meter.bytes_per_s() * max(1, links)
         cal = self._reshard_calibration()
@@ -97,7 +99,7 @@ class ReshardMixin:
         est = (xfer
                + local_bytes * cal["copy_s_per_byte"]
                + params * cal["flatten_s_per_param"] + fresh * cal["materialize_s_per_param"]
-               + cal["groups_s"])
+               + cal["groups_s"] + cal["other_s"])
         return est
 
     def _reshard_calibration(self) -> Dict[str, float]:
@@ -107,21 +109,29 @@ class ReshardMixin:
         bt = self._init_build_times or self._build_times
         mat_rate = bt.get("materialize_s", 0.0) / max(1, bt.get("materialized_params", 1))
         flat = [bt.get("flatten_s", 0.0) / max(1, bt.get("flattened_params", 1))]
-        copy = [1.0 / (600e9 if self.device.type == "cuda" else 4e9)]   # pack + unpack prior
+        # priors (MI355X, measured on GPT-2-medium re-shards, profiles/r5_cfg_calib.jsonl): pack +
+        # unpack gather / scatter per-layer slices at ~300 GB/s, not a bulk copy's rate; ~6 ms of
+        # syncs and shadow refresh outside the timed phases
+        gpu = self.device.type == "cuda"
+        copy = [1.0 / (300e9 if gpu else 4e9)]
         groups = [0.0]
+        other = [0.006 if gpu else 0.0]
         for ph in self._reshard_samples:
             if ph.get("local_bytes"):
                 copy.append((ph["pack_s"] + ph["unpack_s"]) / ph["local_bytes"])
             if ph.get("flattened_params"):
                 flat.append(max(0.0, ph["rebuild_s"] - ph["materialized_params"] * mat_rate) / ph["flattened_params"])
             groups.append(ph.get("groups_s", 0.0))
+            if "other_s" in ph:
+                other.append(ph["other_s"])
+
         def med(v):   # true median (an even count averages the middle two: the upper one alone let
             #           one slow first re-shard set the next prediction, r5_cfg_full.jsonl config 5 s1)
             v = sorted(v)
             n = len(v)
             return v[n // 2] if n % 2 else 0.5 * (v[n // 2 - 1] + v[n // 2])
         return {"copy_s_per_byte": med(copy), "flatten_s_per_param": med(flat),
-                "materialize_s_per_param": mat_rate, "groups_s": med(groups)}
+                "materialize_s_per_param": mat_rate, "groups_s": med(groups), "other_s": med(other)}
 
     def reassign(self, compromised: Sequence[int], step: Optional[int] = None):
         """Exclude ``compromised`` nodes and re-partition every layer over the remaining trusted
@@ -180,6 +190,9 @@ class ReshardMixin:
         with no_gc():
             moved = self._migrate(new_plan, restore={c: sources[c] for c in restored}, fresh=fresh, ckpt=from_ckpt)
         dt = time.perf_counter() - t0
+        ph = self._migrate_phases
+        ph["other_s"] = max(0.0, dt - sum(ph.get(k, 0.0) for k in ("pack_s", "transfer_s", "rebuild_s", "groups_s",
+                                                                   "unpack_s")))
         self.excluded = sorted(set(self.excluded) | set(compromised))
         for c in compromised:     # the tampered weights now live nowhere (restored or re-placed)
             if c < self.t_taint.numel():
