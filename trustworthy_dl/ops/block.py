@@ -161,9 +161,18 @@ def _mm(a, b, bias=None):
     return torch.addmm(bias, a, b) if bias is not None else torch.mm(a, b)
 
 
+def _native_env(name: str) -> bool:
+    return os.environ.get(name, "0") == "1"
+
+
 def _addmm_inplace(c, a, b):
-    """c += a @ b (c is a fresh, un-saved buffer)."""
+    """c += a @ b (c is a fresh, un-saved buffer).  TDL_NATIVE_PROJ=1: the native kernel's
+    residual-add epilogue instead of the library GEMM with beta = 1 (A/B switch)."""
     if c.is_cuda:
+        if _native_env("TDL_NATIVE_PROJ"):
+            from . import gemm
+            if gemm.supported(a, b):
+                return gemm.matmul(a, b, out=c, epi="resadd")
         return c.addmm_(a, b)
     return c.copy_((c.float() + a.float() @ b.float()).to(c.dtype))
 
@@ -180,7 +189,11 @@ class _GPT2BlockFn(torch.autograd.Function):
         qkv = _mm(h1, fwd_weight(w_qkv), b_qkv)
         o, lse, scale = attn_fwd(qkv.view(B, T, 3 * C), n_head, True)
         o2 = o.view(B * T, C)
-        z = _mm(o2, fwd_weight(w_o))
+        if _native_env("TDL_NATIVE_OPROJ") and o2.is_cuda:   # A/B switch: native out-projection
+            from . import gemm
+            z = gemm.matmul(o2, fwd_weight(w_o))
+        else:
+            z = _mm(o2, fwd_weight(w_o))
         y1, y, h2, mean2, rstd2 = _add_bias_ln_fwd(x2, z, b_o, b_p, ln2_w, ln2_b, eps, (B, T, C))
         del z
         wfc = fwd_weight(w_fc)
