@@ -1,0 +1,27 @@
+#!/usr/bin/env python3
+"""Tiny weight-gradient driver for rocprofv3 --pmc passes: the qkv weight gradient of GPT-2-medium
+at 64k tokens (fp32 main_grad += x^T dy, [1024 x 65536] @ [65536 x 3072]) on the persistent kernel
+(gemm_p4, split-K slabs + reduce), 5 launches."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from trustworthy_dl.ops import gemm  # noqa: E402
+
+T, C, N = int(os.environ.get("PMC_T", 65536)), int(os.environ.get("PMC_C", 1024)), int(os.environ.get("PMC_N", 3072))
+x = ((torch.rand(T, C, device="cuda") * 2 - 1)).bfloat16()
+dy = ((torch.rand(T, N, device="cuda") * 2 - 1) * 0.05).bfloat16()
+acc = torch.zeros(C, N, dtype=torch.float32, device="cuda")
+for _ in range(5):
+    gemm.matmul_f32_acc(acc, x.t(), dy)
+torch.cuda.synchronize()
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+for _ in range(10):
+    gemm.matmul_f32_acc(acc, x.t(), dy)
+e.record()
+e.synchronize()
+ms = s.elapsed_time(e) / 10
+print(f"done {ms * 1e3:.1f} us/call {2.0 * T * C * N / ms / 1e9:.1f} TF/s", flush=True)
