@@ -177,6 +177,10 @@ class CommitmentMixin:
         d[SV.D_GSK_APP:SV.D_GSK_APP + 2].copy_(fold_hash64(word_hash(st.flat.grad, self._commit_segments(st),
                                                                      self._hash_seed(st))))
         d[SV.D_GSK_BWD:SV.D_GSK_BWD + 2].copy_(fold_hash64(com[-1]))
+        att = self.attacker
+        if att is not None and hasattr(att, "lies_about_commitment") and att.lies_about_commitment(node, self.global_step):
+            # simulated liar: its own row claims it committed what it applies
+            d[SV.D_GSK_BWD:SV.D_GSK_BWD + 2].copy_(d[SV.D_GSK_APP:SV.D_GSK_APP + 2])
         d[SV.D_GSK_ON:SV.D_GSK_ON + 1].fill_(1.0)
         pre = self._tsk_pre.get(st.stage_id)
         if pre is not None:
@@ -188,12 +192,29 @@ class CommitmentMixin:
 
     def _gsk_mismatch(self, D: torch.Tensor) -> torch.Tensor:
         """Per-node 1.0 where the applied gradient's hash differs from the committed running
-        gradient's (a gradient rewritten after the backward: exact, every coordinate)."""
+        gradient's (a gradient rewritten after the backward: exact, every coordinate), or (distributed)
+        where the last commitment a node reports differs from the one its auditor received.  The
+        applied hash itself is the node's own report: a rank that also lies about it is outside what
+        this check sees (the recompute audit of its committed contributions still applies)."""
         from ..security.grad_audit import K_SKETCH
         app = D[:, SV.D_GSK_APP:SV.D_GSK_APP + 2]
         com = D[:, SV.D_GSK_BWD:SV.D_GSK_BWD + 2]
         on = (D[:, SV.D_GSK_ON] > 0).float()
         bad = on * (app != com).any(1).float()
+        if self.distributed and self.cfg.audit_backward:
+            for idx in self._replica_orders():
+                S = idx.numel()
+                for j in range(S):
+                    # the auditor of stage j: stage j + 1, or stage j - 1 for the loss stage
+                    if j + 1 < S:
+                        rec = D[idx[j + 1], SV.D_GCOM_RECV_PREV:SV.D_GCOM_RECV_PREV + 2]
+                    elif j > 0:
+                        rec = D[idx[j - 1], SV.D_GCOM_RECV_NEXT:SV.D_GCOM_RECV_NEXT + 2]
+                    else:
+                        continue
+                    n = idx[j]
+                    held = (rec > 0).all().float() * on[n]
+                    bad[n] = torch.maximum(bad[n], held * (rec - 1.0 != com[n]).any().float())
         # the tied weight: every member must apply the sum of the members' own contributions
         ton = (D[:, SV.D_TSK_ON] > 0).float()
         pre, tapp = D[:, SV.D_TSK_PRE:SV.D_TSK_PRE + K_SKETCH], D[:, SV.D_TSK_APP:SV.D_TSK_APP + K_SKETCH]

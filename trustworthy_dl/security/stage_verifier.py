@@ -71,7 +71,11 @@ D_GSK_ON = 45        # 1 when D_GSK_* hold commitments this step
 D_TSK_PRE = 46       # [2] sketch of this stage's OWN gradient of its tied weight (before the tied all-reduce)
 D_TSK_APP = 48       # [2] sketch of the tied weight's gradient it applies (after the all-reduce and hooks)
 D_TSK_ON = 50        # 1 when this stage holds a member of the (first) tie group
-DIGEST = 51
+D_GCOM_RECV_PREV = 51  # [2] (distributed) 1 + the fold of the last gradient commitment the audited
+                       #     previous stage SENT here (0 = none this step)
+D_GCOM_RECV_NEXT = 53  # [2] same for the audited next (loss) stage: a stage cannot report a different
+                       #     last commitment in its own row than the one its auditor holds
+DIGEST = 55
 # audit check bits
 AK_FWD, AK_DX, AK_DW, AK_WHASH, AK_DXHASH = 1, 2, 4, 8, 16
 
