@@ -82,13 +82,23 @@ def main():
         if use_cuda:
             torch.cuda.synchronize()
 
+    # the next batch's host->device copy runs on a copy stream under the current step
+    # (utils/prefetch.py); each rank copies only what its stages consume
+    from trustworthy_dl.utils.prefetch import DevicePrefetcher
+    keys = None
+    if engine.distributed:
+        st = engine.my_stage()
+        keys = ([] if st is None else (["input"] if st.stage_id == 0 else []) + (["target"] if st.computes_loss else []))
+    seq = (batches[i % 2] for i in range(args.warmup + args.steps))
+    feed = iter(seq) if os.environ.get("TDL_BENCH_PREFETCH", "1") == "0" else \
+        DevicePrefetcher(seq, engine.device, keys=keys)   # (=0: the engine's own copies, A/B)
     for i in range(args.warmup):
-        engine.train_step(batches[i % 2])
+        engine.train_step(next(feed))
     engine.flush()
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        engine.train_step(batches[i % 2])
+        engine.train_step(next(feed))
     sync()
     elapsed = time.perf_counter() - t0
     engine.flush()
