@@ -242,6 +242,16 @@ def run(args):
         if use_cuda:
             torch.cuda.synchronize()
 
+    # the next batch's host->device copy runs on a copy stream under the current step
+    # (utils/prefetch.py); each rank copies only what its stages consume
+    from trustworthy_dl.utils.prefetch import DevicePrefetcher
+    keys = None
+    if engine.distributed:
+        st = engine.my_stage()
+        keys = ([] if st is None else (["input"] if st.stage_id == 0 else []) + (["target"] if st.computes_loss else []))
+    seq = (batches[i % 2] for i in range(args.warmup + args.steps))
+    feed = iter(seq) if os.environ.get("TDL_BENCH_PREFETCH", "1") == "0" else \
+        DevicePrefetcher(seq, engine.device, keys=keys)   # (=0: the engine's own copies, A/B)
     done = [0]
 
     def step(i):
@@ -251,7 +261,7 @@ def run(args):
                 raise RuntimeError("injected fault (--debug-fault raise)")
             while True:                      # a rank that stops answering (its peers block in P2P)
                 time.sleep(3600)
-        engine.train_step(batches[i % 2])
+        engine.train_step(next(feed))
         done[0] += 1
         if done[0] == args.reassign_at:
             progress.mark(f"step {done[0]}: re-shard away from rank {engine.plan.ranks[-1]}")
