@@ -33,3 +33,12 @@ rows = [e for e in ks if e.key in ("aten::copy_", "aten::_to_copy", "aten::add_"
 rows.sort(key=lambda e: -(e.device_time_total if hasattr(e, "device_time_total") else e.cuda_time_total))
 for e in rows[:25]:
     print(e.count, e.key, round(e.device_time_total if hasattr(e, "device_time_total") else e.cuda_time_total, 1), str(e.input_shapes)[:160], file=sys.stderr)
+
+print("--- small copies with Python stacks", file=sys.stderr)
+seen = collections.Counter()
+for e in p.events():
+    if e.name in ("aten::copy_", "aten::_to_copy", "aten::fill_", "aten::zero_") and e.input_shapes and e.input_shapes[0] in ([1], [], [2]):
+        st = [s for s in (e.stack or []) if "torch/" not in s and "<built-in" not in s][:5]
+        seen[(e.name, str(e.input_shapes[0]), " | ".join(st))] += 1
+for (n, sh, st), c in seen.most_common(30):
+    print(c, n, sh, st, file=sys.stderr)
