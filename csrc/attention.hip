@@ -52,8 +52,9 @@ static int dkdv_pf() {   // read per call: in-process A/B
 // waves per workgroup of the attention kernels: TDL_ATTN_WAVES=4|8 (read per launch: in-process A/B)
 // waves per workgroup of kernel i (0 forward, 1 dQ, 2 dK/dV): TDL_ATTN_WAVES = one digit for all
 // three or three digits ("844"); 8 waves stage each K/V (Q/dO) tile once for twice the rows
-// longest sequence the dK/dV kernel stages lse / delta for (2 x 16 KiB of LDS per workgroup)
-#define ATTN_BWD_MAXT 4096
+// longest sequence the dK/dV kernel stages lse / delta for: 8 T bytes of dynamic LDS beside its
+// 32-34 KiB of static tiles, at most the 160 KiB of a CU
+#define ATTN_BWD_MAXT 16384
 // s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their no-wait maxima), gfx9 encoding
 #define VMCNT0 0x0F70
 
@@ -426,8 +427,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     auto dOw = [&](int b) { return tiles + (6 + b) * IMG; };
     // lse (pre-scaled by log2(e)) and delta of every query this workgroup visits, staged once in the
     // prologue: no per-tile scalar loads in the loop (their waits drained the operand prefetch)
-    __shared__ __attribute__((aligned(16))) float lse_s[ATTN_BWD_MAXT];
-    __shared__ __attribute__((aligned(16))) float delta_s[ATTN_BWD_MAXT];
+    // (dynamic LDS: 2 x T floats, sized at launch — dkdv_lds_bytes)
+    extern __shared__ __attribute__((aligned(16))) float lse_dyn[];
+    float* lse_s = lse_dyn;
+    float* delta_s = lse_dyn + T;
 
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: tile-level branches stay scalar
@@ -838,6 +841,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
     }
 }
 
+// launch a dK/dV kernel with `dl` bytes of dynamic LDS (raising the kernel's limit past the 64 KiB
+// default once, for T > 8192)
+template <typename Kern, typename... Args>
+static void dkdv_launch(Kern kern, int grid, int threads, size_t dl, hipStream_t s, Args... args) {
+    if (dl > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl);
+    kern<<<grid, threads, dl, s>>>(args...);
+}
+
 TDL_API int tdl_colsum_f32(const float* part, int G, int N, int ld, float* acc, hipStream_t s);  // norm_act.hip
 
 // bias_acc (nullable): fp32 [3 H HD] accumulator of the qkv bias gradient (+= column sums of dqkv,
@@ -846,6 +857,7 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
                          float* bias_part, float* delta, int B, int T, int H, int D, float scale, int causal,
                          hipStream_t s) {
     if (D != HD || T % 128 != 0 || T > ATTN_BWD_MAXT) return (int)hipErrorInvalidValue;
+    const size_t dl = (size_t)2 * T * sizeof(float);   // dK/dV dynamic LDS: lse + delta of T queries
     if ((bias_acc == nullptr) != (bias_part == nullptr)) return (int)hipErrorInvalidValue;
     // the dQ kernel also produces delta = rowsum(dO * O) for the dK/dV kernel, so it runs first
     const int grid = B * H * (T / 128);
@@ -860,15 +872,15 @@ TDL_API int tdl_attn_bwd(const void* qkv, const void* out, const void* dout, con
     if (causal) {
         if (w8 && attn_waves(1) == 8) attn_bwd_dq_kernel<true, 8><<<g8, 512, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
         else attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
-        if (w8 && attn_waves(2) == 8) attn_bwd_dkdv_kernel<true, 1, 2, 8><<<g8, 512, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<true, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<true, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else attn_bwd_dkdv_kernel<true, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        if (w8 && attn_waves(2) == 8) dkdv_launch(attn_bwd_dkdv_kernel<true, 1, 2, 8>, g8, 512, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_ns() == 2) dkdv_launch(attn_bwd_dkdv_kernel<true, 2, 1>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_pf() == 2) dkdv_launch(attn_bwd_dkdv_kernel<true, 1, 2>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else dkdv_launch(attn_bwd_dkdv_kernel<true, 1, 1>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     } else {
         attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>(Q, dO, lse, Ob, delta, dQKV, T, H, nb, scale, bp);
-        if (dkdv_ns() == 2) attn_bwd_dkdv_kernel<false, 2, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else if (dkdv_pf() == 2) attn_bwd_dkdv_kernel<false, 1, 2><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
-        else attn_bwd_dkdv_kernel<false, 1, 1><<<grid, 256, 0, s>>>(Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        if (dkdv_ns() == 2) dkdv_launch(attn_bwd_dkdv_kernel<false, 2, 1>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else if (dkdv_pf() == 2) dkdv_launch(attn_bwd_dkdv_kernel<false, 1, 2>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
+        else dkdv_launch(attn_bwd_dkdv_kernel<false, 1, 1>, grid, 256, dl, s, Q, dO, lse, delta, dQKV, T, H, nb, scale, bp);
     }
     if (bias_acc != nullptr) {
         const int rc = (int)hipGetLastError();

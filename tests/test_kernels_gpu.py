@@ -736,3 +736,21 @@ def test_verifier_fused_tail_matches_torch_form(features, monkeypatch):
             assert torch.allclose(x, y_, rtol=1e-5, atol=1e-6), step
         fe = torch.isfinite(B.norm_ema)
         assert torch.allclose(A.norm_ema[fe], B.norm_ema[fe], rtol=1e-5, atol=1e-6), step
+
+
+def test_flash_attention_long_sequence_dynamic_lds():
+    """T = 12288: the dK/dV kernel stages lse / delta for 12288 queries in 96 KiB of dynamic LDS
+    (past the 64 KiB default, raised at launch); gradients vs fp32 SDPA."""
+    from trustworthy_dl.ops import causal_attention
+    torch.manual_seed(3)
+    B, T, H, D = 1, 12288, 1, 64
+    qkv = (torch.randn(B, T, 3 * H * D, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    o = causal_attention(qkv, H, True)
+    g = torch.randn_like(o)
+    o.backward(g)
+    x = qkv.detach().float().requires_grad_(True)
+    q, k, v = x.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True).transpose(1, 2).reshape(B, T, H * D)
+    ref.backward(g.float())
+    assert _rel(o, ref) < 2e-2
+    assert _rel(qkv.grad, x.grad) < 3e-2
