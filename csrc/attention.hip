@@ -105,6 +105,14 @@ constexpr int HD = 64;
 // 4 rows cover the 64 banks once.  Writers store 16-B chunks through the same map.
 __device__ __forceinline__ int swz_tr(int row, int col) { return row * HD + (col ^ (((row >> 1) & 1) << 5)); }
 
+// 16-B chunk slot of logical chunk c in row `row` of a "row" image ([rows][64] bf16, 128-B rows)
+// read with ds_read_b128, lane l -> row l & 31.  The bank slot of a chunk is (row & 1, slot): with
+// slot = c ^ (row & 7) rows r and r + 8 share it and sit in one of ds_read_b128's 16-lane groups
+// ({0-3,12-15,20-27}, ...) -> every row read was 2-way (PMC: 0.87-1.66 conflict cycles per LDS op
+// in the three kernels).  Keyed on row >> 1 the 8 even and 8 odd rows of each group take distinct
+// slots.  Also (row + 32 j) keeps the slot of row.
+__device__ __forceinline__ int rsw(int row, int c) { return (c ^ ((row >> 1) & 7)) * 8; }
+
 // Workgroup -> (batch*head, block) with the nb blocks of one head on ONE XCD, dispatched back to
 // back (heaviest causal block first): the dispatcher sends workgroup L to XCD L % 8, so L = 8 j + x
 // puts stream position j of XCD x on head 8 (j / nb) + x.  The head's K/V (fwd, dQ) or Q/dO (dK/dV)
@@ -204,10 +212,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
     };
     auto gload = [&](int kb) { gload_to(kb, kreg0, kreg1, vreg0, vreg1); };
     auto sstore = [&](int buf) {
-        *(uint4*)(Ks[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
+        *(uint4*)(Ks[buf] + srow0 * HD + rsw(srow0, sch)) = kreg0;
         *(uint4*)(Vs[buf] + swz_tr(srow0, sch * 8)) = vreg0;
         if constexpr (NW == 4) {
-            *(uint4*)(Ks[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+            *(uint4*)(Ks[buf] + srow1 * HD + rsw(srow1, sch)) = kreg1;
             *(uint4*)(Vs[buf] + swz_tr(srow1, sch * 8)) = vreg1;
         }
     };
@@ -228,8 +236,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int r1 = 32 + r;
-                const bf16x8_t a0 = as_bf16x8(*(const uint4*)(K_ + r * HD + (((2 * s + h) ^ (r & 7)) * 8)));
-                const bf16x8_t a1 = as_bf16x8(*(const uint4*)(K_ + r1 * HD + (((2 * s + h) ^ (r1 & 7)) * 8)));
+                const bf16x8_t a0 = as_bf16x8(*(const uint4*)(K_ + r * HD + rsw(r, 2 * s + h)));
+                const bf16x8_t a1 = as_bf16x8(*(const uint4*)(K_ + r1 * HD + rsw(r1, 2 * s + h)));
                 s0 = MFMA32(a0, qf[s], s0);
                 s1 = MFMA32(a1, qf[s], s1);
             }
@@ -417,7 +425,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     constexpr int BK = 32 * NW, BQ = 32 * NS;
     // plain images (transposed tr-reads) + XOR-swizzled images (row reads: 32 rows x 128 B with
-    // the 16-B chunk index ^ (row & 7) -> conflict-free ds_read_b128 across the 32 row lanes)
+    // the 16-B chunk slot rsw(row, c) -> conflict-free ds_read_b128 across the 32 row lanes)
     // two buffers x four images: Q / dO, plain (transposed reads) and row-swizzled (row reads)
     constexpr int IMG = BQ * HD;
     __shared__ __attribute__((aligned(16))) bf16_t tiles[8 * IMG];
@@ -460,7 +468,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     const int q_start = CAUSAL ? kblk : 0;   // multiple of 128, so BQ (32 or 64) tiles end at T
     const int srow = (tid & 255) >> 3, sch = tid & 7;  // staging: 256 x 16 B = one 32 x 64 slab per operand
-    const int swz = ((sch ^ (srow & 7)) * 8);  // (srow + 32 j) & 7 == srow & 7
+    const int swz = rsw(srow, sch);  // rsw(srow + 32 j, .) == rsw(srow, .)
     // which operand this thread stages: both (4 waves), Q (waves 0-3) or dO (waves 4-7) with 8
     const bool stq = NW == 4 || tid < 256, std_ = NW == 4 || tid >= 256;
     constexpr float LOG2E = 1.4426950408889634f;
@@ -532,7 +540,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
                 f32x16 sacc = {}, dpacc = {};
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
-                    const int c = ((2 * s + h) ^ (r & 7)) * 8;
+                    const int c = rsw(r, 2 * s + h);
                     const bf16x8_t aq = as_bf16x8(*(const uint4*)(Qr + r * HD + c));
                     const bf16x8_t ad = as_bf16x8(*(const uint4*)(dOr + r * HD + c));
                     sacc = MFMA32(aq, kf[s], sacc);
@@ -734,13 +742,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
     };
     auto gload = [&](int kb) { gload_to(kb, kreg0, kreg1, vreg0, vreg1); };
     auto sstore = [&](int buf) {
-        *(uint4*)(Kr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = kreg0;
+        *(uint4*)(Kr[buf] + srow0 * HD + rsw(srow0, sch)) = kreg0;
         *(uint4*)(Kp[buf] + swz_tr(srow0, sch * 8)) = kreg0;
-        *(uint4*)(Vr[buf] + srow0 * HD + ((sch ^ (srow0 & 7)) * 8)) = vreg0;
+        *(uint4*)(Vr[buf] + srow0 * HD + rsw(srow0, sch)) = vreg0;
         if constexpr (NW == 4) {
-            *(uint4*)(Kr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = kreg1;
+            *(uint4*)(Kr[buf] + srow1 * HD + rsw(srow1, sch)) = kreg1;
             *(uint4*)(Kp[buf] + swz_tr(srow1, sch * 8)) = kreg1;
-            *(uint4*)(Vr[buf] + srow1 * HD + ((sch ^ (srow1 & 7)) * 8)) = vreg1;
+            *(uint4*)(Vr[buf] + srow1 * HD + rsw(srow1, sch)) = vreg1;
         }
     };
     // the tile of keys kb, staged in LDS buffer `buf`
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int r1 = 32 + r;
-                const int c0 = ((2 * s + h) ^ (r & 7)) * 8, c1 = ((2 * s + h) ^ (r1 & 7)) * 8;
+                const int c0 = rsw(r, 2 * s + h), c1 = rsw(r1, 2 * s + h);
                 const bf16x8_t ak0 = as_bf16x8(*(const uint4*)(Kr_ + r * HD + c0));
                 const bf16x8_t ak1 = as_bf16x8(*(const uint4*)(Kr_ + r1 * HD + c1));
                 const bf16x8_t av0 = as_bf16x8(*(const uint4*)(Vr_ + r * HD + c0));
