@@ -490,7 +490,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
     }
     for (int i = tid; i < T - q_start; i += 64 * NW) {
         lse_s[i] = lse_row[q_start + i] * LOG2E;
-        delta_s[i] = delta_row[q_start + i];
+        delta_s[i] = -delta_row[q_start + i];   // negated: the dP accumulator starts from it
     }
     // every prologue load (K / V fragments included) has landed before the loop: the compiler's
     // wait bookkeeping then never has to drain the loop's prefetches on their account
@@ -537,7 +537,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
                 const bf16_t* dOr = dOw(buf) + 32 * j * HD;
                 const float* lsb = lse_s + (qs - q_start);
                 const float* dlb = delta_s + (qs - q_start);
-                f32x16 sacc = {}, dpacc = {};
+                // dP starts from -delta (row constants as the initial accumulator): the MFMA chain
+                // leaves dP - delta, and dS = P * (dP - delta) is one multiply per score
+                f32x16 sacc = {}, dpacc;
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const float4 c = *(const float4*)(dlb + 8 * g4 + 4 * h);
+                    dpacc[4 * g4] = c.x; dpacc[4 * g4 + 1] = c.y; dpacc[4 * g4 + 2] = c.z; dpacc[4 * g4 + 3] = c.w;
+                }
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     const int c = rsw(r, 2 * s + h);
@@ -550,13 +557,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
                 // of T / 32): elsewhere the per-element compare + select is dropped (VALU-bound loop)
                 // lse / delta of the lane's 16 query rows: 4 groups of 4 consecutive rows -> 4 + 4
                 // 16-byte LDS reads instead of 32 scalar ones
-                float lsv[16], dlv[16];
+                float lsv[16];
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4) {
                     const float4 a = *(const float4*)(lsb + 8 * g4 + 4 * h);
-                    const float4 c = *(const float4*)(dlb + 8 * g4 + 4 * h);
                     lsv[4 * g4] = a.x; lsv[4 * g4 + 1] = a.y; lsv[4 * g4 + 2] = a.z; lsv[4 * g4 + 3] = a.w;
-                    dlv[4 * g4] = c.x; dlv[4 * g4 + 1] = c.y; dlv[4 * g4 + 2] = c.z; dlv[4 * g4 + 3] = c.w;
                 }
                 if (CAUSAL && qs < k0 + 31) {
 #pragma unroll
@@ -565,14 +570,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_kernel(const bf
                         float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
                         if (kj > qs + ql) p = 0.f;
                         sacc[i] = p;
-                        dpacc[i] = p * (dpacc[i] - dlv[i]);
+                        dpacc[i] = p * dpacc[i];
                     }
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const float p = fast_exp2(fmaf(sacc[i], sl2, -lsv[i]));
                         sacc[i] = p;
-                        dpacc[i] = p * (dpacc[i] - dlv[i]);
+                        dpacc[i] = p * dpacc[i];
                     }
                 }
                 const bf16x8_t pb0 = cvt8(sacc, 0), pb1 = cvt8(sacc, 8);
@@ -722,6 +727,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
     dl_q += __shfl_xor(dl_q, 32, 64);
     if (h == 0) delta[(size_t)bh * T + qi] = dl_q;
     f32x16 dq0 = {}, dq1 = {};
+    // -delta as the dP^T chains' initial accumulator (the lane's query is fixed): the chain leaves
+    // dP^T - delta and dS^T = P^T * (dP^T - delta) is one multiply per score
+    f32x16 ndl;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ndl[i] = -dl_q;
     const int tq = (lane & 15) >> 2, tp = lane & 3, tcol = 16 * ((lane >> 4) & 1) + 4 * tp;
     int nkb = T / BN;
     if (CAUSAL) {
@@ -757,7 +767,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
         const bf16_t* Kp_ = Kp[buf];
         const bf16_t* Vr_ = Vr[buf];
         if (!CAUSAL || kb * BN <= q0 + 31) {
-            f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+            f32x16 s0 = {}, s1 = {}, p0, p1;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int r1 = 32 + r;
@@ -768,8 +778,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
                 const bf16x8_t av1 = as_bf16x8(*(const uint4*)(Vr_ + r1 * HD + c1));
                 s0 = MFMA32(ak0, qf[s], s0);
                 s1 = MFMA32(ak1, qf[s], s1);
-                p0 = MFMA32(av0, df[s], p0);
-                p1 = MFMA32(av1, df[s], p1);
+                p0 = MFMA32(av0, df[s], s == 0 ? ndl : p0);
+                p1 = MFMA32(av1, df[s], s == 0 ? ndl : p1);
             }
             if (CAUSAL && kb * BN + BN - 1 > q0) {  // diagonal tile: mask keys > query
 #pragma unroll
@@ -777,14 +787,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
                     const int key0 = kb * BN + (i & 3) + 8 * (i >> 2) + 4 * h;
                     const float e0 = key0 > qi ? 0.f : fast_exp2(s0[i] * sl2 - lse_q);
                     const float e1 = key0 + 32 > qi ? 0.f : fast_exp2(s1[i] * sl2 - lse_q);
-                    s0[i] = e0 * (p0[i] - dl_q);  // dS^T
-                    s1[i] = e1 * (p1[i] - dl_q);
+                    s0[i] = e0 * p0[i];  // dS^T
+                    s1[i] = e1 * p1[i];
                 }
             } else {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    s0[i] = fast_exp2(s0[i] * sl2 - lse_q) * (p0[i] - dl_q);
-                    s1[i] = fast_exp2(s1[i] * sl2 - lse_q) * (p1[i] - dl_q);
+                    s0[i] = fast_exp2(s0[i] * sl2 - lse_q) * p0[i];
+                    s1[i] = fast_exp2(s1[i] * sl2 - lse_q) * p1[i];
                 }
             }
             const bf16x8_t d00 = cvt8(s0, 0), d01 = cvt8(s0, 8), d10 = cvt8(s1, 0), d11 = cvt8(s1, 8);
