@@ -169,7 +169,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16_t* __restr
     constexpr int BM = 32 * NW, BN = 64;
     __shared__ __attribute__((aligned(16))) bf16_t Ks[2][BN * HD];
     __shared__ __attribute__((aligned(16))) bf16_t Vs[2][BN * HD];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+    // wave-uniform (an SGPR): the causal tile tests become scalar branches, not exec-masked regions
+    // (whose conservative wait bookkeeping drains in-flight loads)
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     int bh, qb;
     head_xcd_map(blockIdx.x, nbh, T / BM, CAUSAL, bh, qb);
     const int b = bh / H, hd = bh - b * H;
@@ -692,7 +695,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_kernel(const bf16
     __shared__ __attribute__((aligned(16))) bf16_t Kr[2][BN * HD];  // swizzled, row reads
     __shared__ __attribute__((aligned(16))) bf16_t Kp[2][BN * HD];  // plain, transposed reads
     __shared__ __attribute__((aligned(16))) bf16_t Vr[2][BN * HD];  // swizzled, row reads
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+    // wave-uniform (an SGPR): the causal tile tests become scalar branches, not exec-masked regions
+    // (whose conservative wait bookkeeping drains in-flight loads)
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     int bh, qb;
     head_xcd_map(blockIdx.x, nbh, T / BM, CAUSAL, bh, qb);  // heavy (late) query blocks first
     const int b = bh / H, hd = bh - b * H;
