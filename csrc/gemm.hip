@@ -1100,6 +1100,199 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ============================================================================ persistent 4-wave, LDS-DMA
+// gemm_p4's geometry (one wave per SIMD owning 128 x 128, AGPR accumulators, persistent grid) with
+// the operands copied by LDS-DMA (buffer_load ... lds, no VGPR staging) into two 64-KiB stages, on
+// the schedule of the library kernel our step profiles name for these products (its disassembly: a
+// K step = 128 MFMAs, 16 one-KiB copies spread one per ~5 MFMAs, three barriers, ONE vmcnt wait):
+//   half 0 (64 MFMAs on F0 = k-half 0 of step s, read at the end of step s - 1):
+//     T 1..31 : read F1 = k-half 1 of step s from stage cur, one fragment every 2 MFMAs
+//     T 34    : own LDS reads retired + barrier: no wave reads stage cur any more
+//     T 40..60: copies 0-4 of step s + 2 into stage cur (one every 5 MFMAs)
+//   half 1 (64 MFMAs on F1):
+//     T 1..31 : copies 5-11
+//     T 32    : vmcnt(12) — every copy of step s + 1 (issued during step s - 1) landed, the 12
+//               issued since stay in flight — + barrier: all waves' copies of step s + 1 visible
+//     T 33..63: read F0 = k-half 0 of step s + 1 from stage nxt; copies 12-15 at T 36..51
+// So a copy has about a K step to land and the wave waits for copies once per step (gemm_p4 waits
+// for each staged register ahead of its LDS write, inside the MFMA stream: 46 % of its wave cycles).
+// NT operands only (TA = TB = false: the forward / input-gradient products).
+template <int T, bool ZERO, class Hook>
+__device__ __forceinline__ void mfma_run_pd(Acc& acc, const bf16x8_t (&a)[8], const bf16x8_t (&b)[8], Hook& hook) {
+    if constexpr (T < 64) {
+        if constexpr (ZERO) amfma0<T>(acc, b[T % 8], a[T / 8]);
+        else amfma<T>(acc, b[T % 8], a[T / 8]);
+        hook(std::integral_constant<int, T>{});
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_run_pd<T + 1, ZERO>(acc, a, b, hook);
+    }
+}
+
+// s_waitcnt vmcnt(n) with expcnt / lgkmcnt at their no-wait maxima (gfx9 encoding)
+constexpr int vmcnt_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+// copies of a step issued before global MFMA slot wg (slots ds + dp i, i < 16)
+constexpr int copies_before(int ds, int dp, int wg) {
+    int n = 0;
+    for (int i = 0; i < 16; ++i) n += (ds + dp * i < wg) ? 1 : 0;
+    return n;
+}
+
+// Schedule (global MFMA slot g = 64 half + T of a K step): RP = MFMAs per F1 fragment read at the
+// head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
+// slot WG; F0 reads after it.
+template <int EPI, int RP = 2, int DS = 40, int DP = 5, int WG = 96>
+__global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
+    static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
+    constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
+    constexpr int RP2 = 127 - WG >= 32 ? 2 : 1;          // MFMAs per F0 fragment read
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 1, wn = w & 1;
+    const int G = gridDim.x;
+    const int lb = xcd_remap(blockIdx.x, G);
+    const int nk = p.k_per_split / BK;
+    const int n_items = p.tiles * p.splits;
+    const int n_mine = lb < n_items ? (n_items - 1 - lb) / G + 1 : 0;
+    const int total = n_mine * nk;
+    if (total == 0) return;
+    auto coords = [&](int i, int& m0, int& n0, int& sp) {
+        const int item = lb + i * G;
+        sp = item / p.tiles;
+        const int tile = item - sp * p.tiles;
+        int tm, tn;
+        tile_coords(p, tile, tm, tn);
+        m0 = tm * BM;
+        n0 = tn * BN;
+    };
+    // ---- producer: the (item, k step) it copies next, two steps ahead of the MFMAs; after the last
+    // step it repeats that step (into a stage nobody reads any more)
+    int pi = 0, pt = 0, pm0, pn0, psp, pleft = total;
+    coords(0, pm0, pn0, psp);
+    Stager<false, 4> sa, sb;   // k-contiguous images: the lane offsets do not depend on the tile
+    sa.init(p.lda, pm0, p.M, w, lane);
+    sb.init(p.ldb, pn0, p.N, w, lane);
+    __amdgpu_buffer_rsrc_t qa, qb;
+    auto produce_rsrc = [&]() {
+        const int k0 = psp * p.k_per_split + pt * BK;
+        qa = sa.rsrc(p.A, p.lda, pm0, p.M, k0);
+        qb = sb.rsrc(p.B, p.ldb, pn0, p.N, k0);
+    };
+    auto produce_advance = [&]() {
+        if (--pleft > 0) {
+            if (++pt == nk) {
+                pt = 0;
+                ++pi;
+                coords(pi, pm0, pn0, psp);
+            }
+        } else {
+            pleft = 0;
+        }
+    };
+    auto copy_piece = [&](char* stage, auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < 8) sa.piece(qa, stage, w, i);
+        else sb.piece(qb, stage + TILE_BYTES, w, i - 8);
+    };
+    auto frag_base = [&](bool isB, int buf, int ks) -> uint32_t {
+        const int wb = isB ? wn : wm;
+        uint32_t v = (uint32_t)((lane & 15) * 128 + (((4 * ks + (lane >> 4)) ^ (lane & 7)) << 4) + wb * 128 * 128);
+        v += (uint32_t)(buf * STAGE_BYTES + (isB ? TILE_BYTES : 0));
+        asm volatile("" : "+v"(v));
+        return v;
+    };
+    auto frag_at = [&](uint32_t base, int t) -> bf16x8_t { return *(const bf16x8_t*)(smem + base + t * 16 * 128); };
+
+    bf16x8_t a0[8], b0[8], a1[8], b1[8];
+    Acc acc;
+    auto read_f0 = [&](int buf) {
+        const uint32_t bb = frag_base(true, buf, 0), ba = frag_base(false, buf, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b0[j] = frag_at(bb, j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a0[i] = frag_at(ba, i);
+    };
+    {   // prologue: steps 0 and 1 -> stages 0 and 1; F0 = step 0's k-half 0
+        produce_rsrc();
+        static_for<16>([&](auto ic) { copy_piece(smem, ic); });
+        produce_advance();
+        produce_rsrc();
+        static_for<16>([&](auto ic) { copy_piece(smem + STAGE_BYTES, ic); });
+        produce_advance();
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        read_f0(0);
+    }
+    int s = 0;
+    // after_epi: the first step after a tile's epilogue, whose >= 64 stores / loads per wave were
+    // issued between the copies this step waits for and the NB issued since: vmcnt(63) then retires
+    // those copies without waiting for the epilogue's stores (vmcnt(NB) stalled on them every tile)
+    auto kstep = [&](auto zc, auto lc, bool after_epi) {
+        constexpr bool ZERO = decltype(zc)::value, LAST = decltype(lc)::value;
+        const int cur = s & 1, nxt = cur ^ 1;
+        char* cstage = smem + cur * STAGE_BYTES;
+        produce_rsrc();
+        auto slot = [&](auto gc, const uint32_t* fb) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (g < 16 * RP && g % RP == RP - 1) {   // F1 = k-half 1 of step s (stage cur)
+                constexpr int k = g / RP;
+                if constexpr (k < 8) b1[k] = frag_at(fb[0], k);
+                else a1[k - 8] = frag_at(fb[1], k - 8);
+            }
+            if constexpr (g == 16 * RP + 2) {   // own reads of stage cur retired; then all waves'
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+            if constexpr (g >= DS && (g - DS) % DP == 0 && (g - DS) / DP < 16)
+                copy_piece(cstage, std::integral_constant<int, (g - DS) / DP>{});
+            if constexpr (g == WG) {   // copies of step s + 1 landed (this step's NB stay in flight)
+                if (ZERO && after_epi) __builtin_amdgcn_s_waitcnt(vmcnt_enc(63));
+                else __builtin_amdgcn_s_waitcnt(vmcnt_enc(NB));
+                __builtin_amdgcn_s_barrier();
+            }
+            if constexpr (!LAST && g > WG && (g - WG - 1) % RP2 == 0 && (g - WG - 1) / RP2 < 16) {
+                constexpr int k = (g - WG - 1) / RP2;   // F0 = k-half 0 of step s + 1 (stage nxt)
+                if constexpr (k < 8) b0[k] = frag_at(fb[2], k);
+                else a0[k - 8] = frag_at(fb[3], k - 8);
+            }
+        };
+        const uint32_t fb[4] = {frag_base(true, cur, 1), frag_base(false, cur, 1), frag_base(true, nxt, 0),
+                                frag_base(false, nxt, 0)};
+        {
+            auto hook = [&](auto tc) { slot(tc, fb); };
+            mfma_run_pd<0, ZERO>(acc, a0, b0, hook);
+        }
+        {
+            auto hook = [&](auto tc) { slot(std::integral_constant<int, 64 + decltype(tc)::value>{}, fb); };
+            mfma_run_pd<0, false>(acc, a1, b1, hook);
+        }
+        produce_advance();
+        ++s;
+    };
+    for (int ci = 0; ci < n_mine; ++ci) {
+        int cm0, cn0, csp;
+        coords(ci, cm0, cn0, csp);
+        kstep(std::true_type{}, std::false_type{}, ci > 0);
+#pragma clang loop unroll(disable)
+        for (int ct = 1; ct < nk - 1; ++ct) kstep(std::false_type{}, std::false_type{}, false);
+        kstep(std::false_type{}, std::true_type{}, false);  // nk >= 2 (host)
+        // epilogue (as gemm_p4): results of the opaque asm MFMAs written before any accumulator read
+        asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+        acc_fence<0>(acc);
+        acc_fence<16>(acc);
+        acc_fence<32>(acc);
+        acc_fence<48>(acc);
+        __builtin_amdgcn_sched_barrier(0);
+        auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
+        epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
+    }
+    // no copy may still be landing when the workgroup's LDS is handed to the next one
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 }  // namespace
 
 // C = epilogue(A x B^T) (see the header for the storage flags and epilogue codes).
@@ -1131,7 +1324,7 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     if ((ta && M % 8) || (tb && N % 8)) return (int)hipErrorInvalidValue;
     int kernel = (epi >> 8) & 0xff;
     epi &= 0xff;
-    if (epi < 0 || epi > 6 || kernel > 2) return (int)hipErrorInvalidValue;
+    if (epi < 0 || epi > 6 || kernel > 3) return (int)hipErrorInvalidValue;
     const bool lds_epi = kernel == 2;  // p4 with the LDS-staged epilogue (NT, bf16 outputs)
     if (kernel == 2) kernel = 0;
     // the dGELU column sums assume rows past M read as zero, which a transposed A cannot give
@@ -1164,6 +1357,33 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     gemm_p4<P4_TA, P4_TB, P4_EPI, P4_LEPI><<<256, PNTHR, 0, s>>>(p);
     TDL_LAUNCH_CHECK();
 #else
+    if (kernel == 3) {  // gemm_pd: NT operands only
+        if (ta || tb || kps / BK < 2) return (int)hipErrorInvalidValue;
+        const int items = p.tiles * split;
+        const int grid = items < num_cus() ? items : num_cus();
+        // schedule variants (plain bf16 epilogue only): TDL_PD_SCHED, read per launch (in-process A/B)
+        const char* sv = std::getenv("TDL_PD_SCHED");
+        const int v = (sv && epi == EPI_BF16) ? std::atoi(sv) : 0;
+        if (v > 0) {
+            switch (v) {
+                case 1: gemm_pd<0, 2, 36, 6, 110><<<grid, PNTHR, 0, s>>>(p); break;
+                case 2: gemm_pd<0, 1, 20, 7, 100><<<grid, PNTHR, 0, s>>>(p); break;
+                case 3: gemm_pd<0, 2, 36, 6, 100><<<grid, PNTHR, 0, s>>>(p); break;
+                default: gemm_pd<0, 1, 24, 6, 108><<<grid, PNTHR, 0, s>>>(p); break;
+            }
+            TDL_LAUNCH_CHECK();
+        }
+        switch (epi) {
+            case 0: gemm_pd<0><<<grid, PNTHR, 0, s>>>(p); break;
+            case 1: gemm_pd<1><<<grid, PNTHR, 0, s>>>(p); break;
+            case 2: gemm_pd<2><<<grid, PNTHR, 0, s>>>(p); break;
+            case 3: gemm_pd<3><<<grid, PNTHR, 0, s>>>(p); break;
+            case 4: gemm_pd<4><<<grid, PNTHR, 0, s>>>(p); break;
+            case 5: gemm_pd<5><<<grid, PNTHR, 0, s>>>(p); break;
+            default: gemm_pd<6><<<grid, PNTHR, 0, s>>>(p); break;
+        }
+        TDL_LAUNCH_CHECK();
+    }
     if (kernel == 0) {
         if (kps / BK < 2) return (int)hipErrorInvalidValue;  // a tile's first and last K step differ
         const int items = p.tiles * split;

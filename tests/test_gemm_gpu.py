@@ -1,6 +1,6 @@
 """Native MFMA GEMMs (csrc/gemm.hip: p4 = persistent 4-wave kernel, p4l = the same with the
-LDS-staged epilogue, pp = staggered 8-wave ping-pong kernel) vs a plain PyTorch fp32 reference of
-the same op (GPU only).
+LDS-staged epilogue, pp = staggered 8-wave ping-pong kernel, pd = persistent 4-wave kernel with
+LDS-DMA staging, NT operands only) vs a plain PyTorch fp32 reference of the same op (GPU only).
 
 Covers the four operand storage forms (k-contiguous / row-contiguous for A and B), every fused
 epilogue, ragged M and N (tile clamping + store masks), split-K slabs and atomics, and every
@@ -13,6 +13,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 KERNELS = ["p4", "p4l", "pp"]
+NT_KERNELS = KERNELS + ["pd"]      # pd takes k-contiguous (NT) operands only
 
 
 def _rel(a, b):
@@ -36,7 +37,7 @@ def _view(t_logical, transposed):
     return t_logical.t().contiguous().t() if transposed else t_logical.contiguous()
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", NT_KERNELS)
 @pytest.mark.parametrize("ta", [False, True])
 @pytest.mark.parametrize("tb", [False, True])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (776, 1032, 320), (8200, 520, 512)])
@@ -44,6 +45,8 @@ def test_layouts(kernel, ta, tb, M, N, K):
     """all four storage forms, ragged M / N, > 1 tile per persistent workgroup (8200 rows), plus an
     fp32 split-K accumulation through slabs"""
     from trustworthy_dl.ops import gemm
+    if kernel == "pd" and (ta or not tb):   # tb: B stored [N][K] (k-contiguous)
+        pytest.skip("pd: NT operands only")
     a = _view(_rand(M, K), ta)
     b = _view(_rand(K, N, scale=0.1), tb)
     out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
@@ -55,7 +58,7 @@ def test_layouts(kernel, ta, tb, M, N, K):
     assert _rel(acc, ref + 1.0) < 1e-4
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", NT_KERNELS)
 @pytest.mark.parametrize("M,N,K", [(1000, 200, 128), (8200, 1032, 256), (4096, 2048, 1024)])
 def test_epilogues(kernel, M, N, K):
     """every epilogue the GPT-2 block uses (bias, bias+GELU with the pre-activation, residual add,
@@ -104,7 +107,7 @@ def test_tile_orders(group, monkeypatch):
     x = _rand(M, K)
     wt = _rand(N, K, scale=0.1)
     ref = x.float() @ wt.float().t()
-    for kn in ("pp", "p4", "p4l"):
+    for kn in ("pp", "p4", "p4l", "pd"):
         out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
         gemm._launch(x, wt.t(), out, N, "none", kernel=kn)
         assert _rel(out, ref) < 1e-2, (kn, group)

@@ -27,8 +27,9 @@ EPI = {"none": 0, "gelu": 1, "resadd": 2, "dgelu": 3, "f32": 4, "f32acc": 5, "f3
 BK = 64
 # Kernel (csrc/gemm.hip): "p4" = the persistent 4-wave kernel (one wave per SIMD owning 128 x 128,
 # register-staged operands), "pp" = the staggered 8-wave ping-pong kernel (LDS-DMA staging,
-# LDS-staged row-contiguous epilogue on NT operands).
-KERNELS = {"p4": 0, "pp": 1, "p4l": 2}
+# LDS-staged row-contiguous epilogue on NT operands), "pd" = the persistent 4-wave kernel with
+# LDS-DMA staging on the library kernel's schedule (NT operands only).
+KERNELS = {"p4": 0, "pp": 1, "p4l": 2, "pd": 3}
 KERNEL = os.environ.get("TDL_GEMM_KERNEL", "pp")        # bf16-output products (matmul)
 WGRAD_KERNEL = os.environ.get("TDL_WGRAD_KERNEL", "p4")  # fp32 weight-gradient products
 
