@@ -1189,10 +1189,15 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
             pleft = 0;
         }
     };
+    // copy i (< 8: A piece i, else B piece i - 8): the lane's base offset in the VGPR operand, the
+    // piece's uniform offset in the SGPR one (no per-copy address arithmetic in the K loop)
     auto copy_piece = [&](char* stage, auto ic) {
         constexpr int i = decltype(ic)::value;
-        if constexpr (i < 8) sa.piece(qa, stage, w, i);
-        else sb.piece(qb, stage + TILE_BYTES, w, i - 8);
+        constexpr int j = i & 7;
+        const Stager<false, 4>& st = i < 8 ? sa : sb;
+        char* dst = stage + (i < 8 ? 0 : TILE_BYTES) + (w + 4 * j) * 1024;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 8 ? qa : qb, (lds_void_t*)dst, 16, st.base[0],
+                                                 __builtin_amdgcn_readfirstlane((uint32_t)j * st.delta), 0, 0);
     };
     auto frag_base = [&](bool isB, int buf, int ks) -> uint32_t {
         const int wb = isB ? wn : wm;
@@ -1369,7 +1374,8 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
                 case 1: gemm_pd<0, 2, 36, 6, 110><<<grid, PNTHR, 0, s>>>(p); break;
                 case 2: gemm_pd<0, 1, 20, 7, 100><<<grid, PNTHR, 0, s>>>(p); break;
                 case 3: gemm_pd<0, 2, 36, 6, 100><<<grid, PNTHR, 0, s>>>(p); break;
-                default: gemm_pd<0, 1, 24, 6, 108><<<grid, PNTHR, 0, s>>>(p); break;
+                case 4: gemm_pd<0, 1, 19, 7, 104><<<grid, PNTHR, 0, s>>>(p); break;
+                default: gemm_pd<0, 1, 20, 7, 108><<<grid, PNTHR, 0, s>>>(p); break;
             }
             TDL_LAUNCH_CHECK();
         }
