@@ -1106,14 +1106,16 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
 // the schedule of the library kernel our step profiles name for these products (its disassembly: a
 // K step = 128 MFMAs, 16 one-KiB copies spread one per ~5 MFMAs, three barriers, ONE vmcnt wait):
 //   half 0 (64 MFMAs on F0 = k-half 0 of step s, read at the end of step s - 1):
-//     T 1..31 : read F1 = k-half 1 of step s from stage cur, one fragment every 2 MFMAs
-//     T 34    : own LDS reads retired + barrier: no wave reads stage cur any more
-//     T 40..60: copies 0-4 of step s + 2 into stage cur (one every 5 MFMAs)
+//     T 0..15 : read F1 = k-half 1 of step s from stage cur, one fragment per MFMA
+//     T 18    : own LDS reads retired + barrier: no wave reads stage cur any more
+//     T 20..62: copies 0-6 of step s + 2 into stage cur, one every 7 MFMAs (spread: a copy's issue
+//               costs ~60 cycles, MI355X_MICROARCH.md; denser placements measured slower)
 //   half 1 (64 MFMAs on F1):
-//     T 1..31 : copies 5-11
-//     T 32    : vmcnt(12) — every copy of step s + 1 (issued during step s - 1) landed, the 12
+//     T 5..33 : copies 7-11
+//     T 36    : vmcnt(12) — every copy of step s + 1 (issued during step s - 1) landed, the 12
 //               issued since stay in flight — + barrier: all waves' copies of step s + 1 visible
-//     T 33..63: read F0 = k-half 0 of step s + 1 from stage nxt; copies 12-15 at T 36..51
+//     T 37..52: read F0 = k-half 0 of step s + 1 from stage nxt; copies 12-15 at T 40..61
+// (variants of these slots: TDL_PD_SCHED, profiles/r5_gemm_pd_sched_ab.jsonl)
 // So a copy has about a K step to land and the wave waits for copies once per step (gemm_p4 waits
 // for each staged register ahead of its LDS write, inside the MFMA stream: 46 % of its wave cycles).
 // NT operands only (TA = TB = false: the forward / input-gradient products).
@@ -1140,7 +1142,7 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // Schedule (global MFMA slot g = 64 half + T of a K step): RP = MFMAs per F1 fragment read at the
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
-template <int EPI, int RP = 2, int DS = 40, int DP = 5, int WG = 96>
+template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
@@ -1372,7 +1374,7 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         if (v > 0) {
             switch (v) {
                 case 1: gemm_pd<0, 2, 36, 6, 110><<<grid, PNTHR, 0, s>>>(p); break;
-                case 2: gemm_pd<0, 1, 20, 7, 100><<<grid, PNTHR, 0, s>>>(p); break;
+                case 2: gemm_pd<0, 2, 40, 5, 96><<<grid, PNTHR, 0, s>>>(p); break;
                 case 3: gemm_pd<0, 2, 36, 6, 100><<<grid, PNTHR, 0, s>>>(p); break;
                 case 4: gemm_pd<0, 1, 19, 7, 104><<<grid, PNTHR, 0, s>>>(p); break;
                 default: gemm_pd<0, 1, 20, 7, 108><<<grid, PNTHR, 0, s>>>(p); break;
