@@ -1119,15 +1119,68 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_p4(GemmParams p) {
 // So a copy has about a K step to land and the wave waits for copies once per step (gemm_p4 waits
 // for each staged register ahead of its LDS write, inside the MFMA stream: 46 % of its wave cycles).
 // NT operands only (TA = TB = false: the forward / input-gradient products).
-template <int T, bool ZERO, class Hook>
+// ORD 0: MFMA T = (A tile T / 8, B tile T % 8) — the MFMA's second source (an A fragment) held for
+// 8 MFMAs; ORD 1: (A tile T % 8, B tile T / 8) — its first source (a B fragment) held, as in the
+// library kernel.  Either way accumulator 8 i + j is tile (i, j).
+template <int T, bool ZERO, int ORD, class Hook>
 __device__ __forceinline__ void mfma_run_pd(Acc& acc, const bf16x8_t (&a)[8], const bf16x8_t (&b)[8], Hook& hook) {
     if constexpr (T < 64) {
-        if constexpr (ZERO) amfma0<T>(acc, b[T % 8], a[T / 8]);
-        else amfma<T>(acc, b[T % 8], a[T / 8]);
+        constexpr int i = ORD == 0 ? T / 8 : T % 8, j = ORD == 0 ? T % 8 : T / 8;
+        if constexpr (ZERO) amfma0<8 * i + j>(acc, b[j], a[i]);
+        else amfma<8 * i + j>(acc, b[j], a[i]);
         hook(std::integral_constant<int, T>{});
         __builtin_amdgcn_sched_barrier(0);
-        mfma_run_pd<T + 1, ZERO>(acc, a, b, hook);
+        mfma_run_pd<T + 1, ZERO, ORD>(acc, a, b, hook);
     }
+}
+
+// bf16 (+ bias) epilogue with 16-byte stores (cdna_hip_programming.md T21): the accumulator gives
+// a lane 4 consecutive columns of a 16 x 16 tile; v_permlane16_swap trades tile j's columns 4-7
+// (held by the odd 16-lane rows) for tile j + 1's columns 0-3 (held by the even rows), so every lane
+// stores 8 consecutive columns of one tile: 32 dwordx4 stores per wave instead of 64 dwordx2 (half
+// the store issue, and few enough VMEM ops that the next tile's first copy wait can count past
+// them instead of waiting for the stores, PD_X4_VMEM).  The bias values come in `braw`, loaded by
+// pd_bias_load at the start of the tile's last K step: a load inside the epilogue would make the
+// in-order vmcnt wait for every copy and store issued before it (the per-tile-row epilogue waits
+// that way once per column block).  Needs N % 8 == 0, ldc % 8 == 0.
+constexpr int PD_X4_VMEM = 32;   // VMEM instructions of pd_store_x4 per wave: 32 stores
+__device__ __forceinline__ void pd_bias_load(const GemmParams& p, int nw, int lane, u32x2_t (&braw)[8]) {
+    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int n = nw + 16 * j + 4 * (lane >> 4);
+        braw[j] = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
+    }
+}
+template <class Get>
+__device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int mw, int nw, int lane,
+                                            const u32x2_t (&braw)[8]) {
+    const int g = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const char*)p.C + (size_t)mw * p.ldc * 2, (long long)(p.M - mw) * p.ldc * 2);
+    const uint32_t lrow = (uint32_t)(lane & 15) * (uint32_t)p.ldc * 2u;
+    auto pair = [&](auto jc) {
+        constexpr int j = 2 * decltype(jc)::value;
+        float ba[4], bb[4];   // bias of this lane's columns in tiles j, j + 1
+        unpack4(make_uint2(braw[j].x, braw[j].y), ba);
+        unpack4(make_uint2(braw[j + 1].x, braw[j + 1].y), bb);
+        const int nt = nw + 16 * (j + (g & 1)) + 8 * (g >> 1);   // the 8 columns this lane stores
+        const uint32_t col = nt < p.N ? (uint32_t)nt * 2u : 0x80000000u;
+        auto row = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const f32x4 a = get(std::integral_constant<int, i>{}, std::integral_constant<int, j>{});
+            const f32x4 b = get(std::integral_constant<int, i>{}, std::integral_constant<int, j + 1>{});
+            float va[4] = {a[0] + ba[0], a[1] + ba[1], a[2] + ba[2], a[3] + ba[3]};
+            float vb[4] = {b[0] + bb[0], b[1] + bb[1], b[2] + bb[2], b[3] + bb[3]};
+            const uint2 qa = pack4(va), qb = pack4(vb);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(qa.x, qb.x, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(qa.y, qb.y, false, false);
+            const uint32_t off = col == 0x80000000u ? col : lrow + (uint32_t)(16 * i) * (uint32_t)p.ldc * 2u + col;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{s0[0], s1[0], s0[1], s1[1]}, rc, off, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for<8>(row);
+    };
+    static_for<4>(pair);
 }
 
 // s_waitcnt vmcnt(n) with expcnt / lgkmcnt at their no-wait maxima (gfx9 encoding)
@@ -1142,11 +1195,16 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // Schedule (global MFMA slot g = 64 half + T of a K step): RP = MFMAs per F1 fragment read at the
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
-template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100>
+template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
     constexpr int RP2 = 127 - WG >= 32 ? 2 : 1;          // MFMAs per F0 fragment read
+    static_assert(!X4 || EPI == EPI_BF16, "16-byte store epilogue: bf16 (+ bias) only");
+    // the first wait after an epilogue: the copies it waits for precede the epilogue's VMEM ops
+    // (>= 64 per wave for the per-tile-row epilogue, exactly PD_X4_VMEM for pd_store_x4) and the NB
+    // copies issued since; vmcnt counts in issue order, so vmcnt(that sum) retires exactly the copies
+    constexpr int NB_EPI = (X4 ? PD_X4_VMEM : 64) + NB < 63 ? (X4 ? PD_X4_VMEM : 64) + NB : 63;
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1232,20 +1290,23 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         read_f0(0);
     }
     int s = 0;
-    // after_epi: the first step after a tile's epilogue, whose >= 64 stores / loads per wave were
-    // issued between the copies this step waits for and the NB issued since: vmcnt(63) then retires
-    // those copies without waiting for the epilogue's stores (vmcnt(NB) stalled on them every tile)
+    u32x2_t braw[8];   // X4: the bias of the wave's columns (pd_bias_load)
+    int bias_n0 = 0;
+    // after_epi: the first step after a tile's epilogue, whose VMEM ops were issued between the
+    // copies this step waits for and the NB issued since: vmcnt(NB_EPI) retires those copies without
+    // waiting for all of the epilogue's stores (vmcnt(NB) stalled on them every tile)
     auto kstep = [&](auto zc, auto lc, bool after_epi) {
         constexpr bool ZERO = decltype(zc)::value, LAST = decltype(lc)::value;
         const int cur = s & 1, nxt = cur ^ 1;
         char* cstage = smem + cur * STAGE_BYTES;
+        if constexpr (X4 && LAST) pd_bias_load(p, bias_n0, lane, braw);   // ahead of this step's copies
         produce_rsrc();
         auto slot = [&](auto gc, const uint32_t* fb) {
             constexpr int g = decltype(gc)::value;
             if constexpr (g < 16 * RP && g % RP == RP - 1) {   // F1 = k-half 1 of step s (stage cur)
                 constexpr int k = g / RP;
-                if constexpr (k < 8) b1[k] = frag_at(fb[0], k);
-                else a1[k - 8] = frag_at(fb[1], k - 8);
+                if constexpr ((k < 8) == (ORD == 0)) b1[k & 7] = frag_at(fb[0], k & 7);
+                else a1[k & 7] = frag_at(fb[1], k & 7);
             }
             if constexpr (g == 16 * RP + 2) {   // own reads of stage cur retired; then all waves'
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1254,25 +1315,25 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
             if constexpr (g >= DS && (g - DS) % DP == 0 && (g - DS) / DP < 16)
                 copy_piece(cstage, std::integral_constant<int, (g - DS) / DP>{});
             if constexpr (g == WG) {   // copies of step s + 1 landed (this step's NB stay in flight)
-                if (ZERO && after_epi) __builtin_amdgcn_s_waitcnt(vmcnt_enc(63));
+                if (ZERO && after_epi) __builtin_amdgcn_s_waitcnt(vmcnt_enc(NB_EPI));
                 else __builtin_amdgcn_s_waitcnt(vmcnt_enc(NB));
                 __builtin_amdgcn_s_barrier();
             }
             if constexpr (!LAST && g > WG && (g - WG - 1) % RP2 == 0 && (g - WG - 1) / RP2 < 16) {
                 constexpr int k = (g - WG - 1) / RP2;   // F0 = k-half 0 of step s + 1 (stage nxt)
-                if constexpr (k < 8) b0[k] = frag_at(fb[2], k);
-                else a0[k - 8] = frag_at(fb[3], k - 8);
+                if constexpr ((k < 8) == (ORD == 0)) b0[k & 7] = frag_at(fb[2], k & 7);
+                else a0[k & 7] = frag_at(fb[3], k & 7);
             }
         };
         const uint32_t fb[4] = {frag_base(true, cur, 1), frag_base(false, cur, 1), frag_base(true, nxt, 0),
                                 frag_base(false, nxt, 0)};
         {
             auto hook = [&](auto tc) { slot(tc, fb); };
-            mfma_run_pd<0, ZERO>(acc, a0, b0, hook);
+            mfma_run_pd<0, ZERO, ORD>(acc, a0, b0, hook);
         }
         {
             auto hook = [&](auto tc) { slot(std::integral_constant<int, 64 + decltype(tc)::value>{}, fb); };
-            mfma_run_pd<0, false>(acc, a1, b1, hook);
+            mfma_run_pd<0, false, ORD>(acc, a1, b1, hook);
         }
         produce_advance();
         ++s;
@@ -1280,6 +1341,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     for (int ci = 0; ci < n_mine; ++ci) {
         int cm0, cn0, csp;
         coords(ci, cm0, cn0, csp);
+        bias_n0 = cn0 + wn * 128;
         kstep(std::true_type{}, std::false_type{}, ci > 0);
 #pragma clang loop unroll(disable)
         for (int ct = 1; ct < nk - 1; ++ct) kstep(std::false_type{}, std::false_type{}, false);
@@ -1292,7 +1354,8 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         acc_fence<48>(acc);
         __builtin_amdgcn_sched_barrier(0);
         auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
-        epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
+        if constexpr (X4) pd_store_x4(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+        else epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         __builtin_amdgcn_sched_barrier(0);
         read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
     }
@@ -1377,8 +1440,15 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
                 case 2: gemm_pd<0, 2, 40, 5, 96><<<grid, PNTHR, 0, s>>>(p); break;
                 case 3: gemm_pd<0, 2, 36, 6, 100><<<grid, PNTHR, 0, s>>>(p); break;
                 case 4: gemm_pd<0, 1, 19, 7, 104><<<grid, PNTHR, 0, s>>>(p); break;
+                case 6: gemm_pd<0, 1, 20, 7, 100, true, 1><<<grid, PNTHR, 0, s>>>(p); break;
                 default: gemm_pd<0, 1, 20, 7, 108><<<grid, PNTHR, 0, s>>>(p); break;
             }
+            TDL_LAUNCH_CHECK();
+        }
+        const char* xe = std::getenv("TDL_PD_X4");   // "0": per-tile-row stores (A/B)
+        const bool x4 = (N % 8 == 0) && (ldc % 8 == 0) && ((uintptr_t)C % 16 == 0) && !(xe && xe[0] == '0');
+        if (epi == EPI_BF16 && x4) {
+            gemm_pd<0, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             TDL_LAUNCH_CHECK();
         }
         switch (epi) {

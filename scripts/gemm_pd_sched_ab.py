@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--groups", default="", help="extra grouped tile orders for pd (TDL_GEMM_GROUPM)")
     args = ap.parse_args()
     M, C = 65536, 1024
     prods = [("qkv_fwd", C, 3 * C), ("o_fwd", C, C), ("fc_fwd", C, 4 * C), ("proj_fwd", 4 * C, C),
@@ -50,8 +51,23 @@ def main():
         for v in args.variants.split(","):
             def f(v=v):
                 os.environ["TDL_PD_SCHED"] = v
+                os.environ.pop("TDL_PD_X4", None)
                 gemm._launch(a, b, out, N, "none", kernel="pd")
             fns["pd" + v] = f
+
+        def f_nox4():   # default schedule, per-tile-row stores instead of the 16-byte epilogue
+            os.environ["TDL_PD_SCHED"] = "0"
+            os.environ["TDL_PD_X4"] = "0"
+            gemm._launch(a, b, out, N, "none", kernel="pd")
+        fns["pd0_nox4"] = f_nox4
+        for g in [x for x in args.groups.split(",") if x]:
+            def f_g(g=g):   # default schedule and epilogue, grouped tile order
+                os.environ["TDL_PD_SCHED"] = "0"
+                os.environ.pop("TDL_PD_X4", None)
+                os.environ["TDL_GEMM_GROUPM"] = g
+                gemm._launch(a, b, out, N, "none", kernel="pd")
+                os.environ["TDL_GEMM_GROUPM"] = "0"
+            fns["pd0_g" + g] = f_g
         ref = a.float() @ b.float()
         bad = {}
         for k, f in fns.items():
@@ -76,6 +92,7 @@ def main():
             res[k + "_tf"] = round(flops / t / 1e12, 1)
         print(json.dumps(res), flush=True)
     os.environ.pop("TDL_PD_SCHED", None)
+    os.environ.pop("TDL_PD_X4", None)
 
 
 if __name__ == "__main__":
