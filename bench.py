@@ -314,7 +314,7 @@ def run(args):
                        "detections": len(engine.attack_history),
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
-                       "native_gemm": "fc fwd+gelu, proj dgrad+dgelu, all weight gradients",
+                       "native_gemm": "fc fwd+gelu (pd), proj dgrad+dgelu (pp), all weight gradients (p4)",
                        "native_wgrad": os.environ.get("TDL_WGRAD_KERNEL", "p4"),
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        # per-rank RCCL communicators / HIP streams (compute + verification + one per

@@ -1143,7 +1143,8 @@ __device__ __forceinline__ void mfma_run_pd(Acc& acc, const bf16x8_t (&a)[8], co
 // pd_bias_load at the start of the tile's last K step: a load inside the epilogue would make the
 // in-order vmcnt wait for every copy and store issued before it (the per-tile-row epilogue waits
 // that way once per column block).  Needs N % 8 == 0, ldc % 8 == 0.
-constexpr int PD_X4_VMEM = 32;   // VMEM instructions of pd_store_x4 per wave: 32 stores
+// VMEM instructions of pd_store_x4 per wave: 32 stores (bf16), 64 (GELU: pre-activation + output)
+constexpr int pd_x4_vmem(int epi) { return epi == EPI_GELU ? 64 : 32; }
 __device__ __forceinline__ void pd_bias_load(const GemmParams& p, int nw, int lane, u32x2_t (&braw)[8]) {
     const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
 #pragma unroll
@@ -1152,11 +1153,14 @@ __device__ __forceinline__ void pd_bias_load(const GemmParams& p, int nw, int la
         braw[j] = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
     }
 }
-template <class Get>
+template <int EPI, class Get>
 __device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int mw, int nw, int lane,
                                             const u32x2_t (&braw)[8]) {
+    static_assert(EPI == EPI_BF16 || EPI == EPI_GELU, "16-byte store epilogue: bf16 (+ bias), bias + GELU");
     const int g = lane >> 4;
     const __amdgpu_buffer_rsrc_t rc = make_rsrc((const char*)p.C + (size_t)mw * p.ldc * 2, (long long)(p.M - mw) * p.ldc * 2);
+    const __amdgpu_buffer_rsrc_t rx =
+        EPI == EPI_GELU ? make_rsrc((const char*)p.aux + (size_t)mw * p.ldc * 2, (long long)(p.M - mw) * p.ldc * 2) : rc;
     const uint32_t lrow = (uint32_t)(lane & 15) * (uint32_t)p.ldc * 2u;
     auto pair = [&](auto jc) {
         constexpr int j = 2 * decltype(jc)::value;
@@ -1171,11 +1175,22 @@ __device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int m
             const f32x4 b = get(std::integral_constant<int, i>{}, std::integral_constant<int, j + 1>{});
             float va[4] = {a[0] + ba[0], a[1] + ba[1], a[2] + ba[2], a[3] + ba[3]};
             float vb[4] = {b[0] + bb[0], b[1] + bb[1], b[2] + bb[2], b[3] + bb[3]};
-            const uint2 qa = pack4(va), qb = pack4(vb);
-            const auto s0 = __builtin_amdgcn_permlane16_swap(qa.x, qb.x, false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(qa.y, qb.y, false, false);
             const uint32_t off = col == 0x80000000u ? col : lrow + (uint32_t)(16 * i) * (uint32_t)p.ldc * 2u + col;
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{s0[0], s1[0], s0[1], s1[1]}, rc, off, 0, 0);
+            auto store8 = [&](const float (&xa)[4], const float (&xb)[4], const __amdgpu_buffer_rsrc_t& r) {
+                const uint2 qa = pack4(xa), qb = pack4(xb);
+                const auto s0 = __builtin_amdgcn_permlane16_swap(qa.x, qb.x, false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(qa.y, qb.y, false, false);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{s0[0], s1[0], s0[1], s1[1]}, r, off, 0, 0);
+            };
+            if constexpr (EPI == EPI_GELU) {
+                store8(va, vb, rx);   // the pre-activation
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    va[r] = gelu_tanh(va[r]);
+                    vb[r] = gelu_tanh(vb[r]);
+                }
+            }
+            store8(va, vb, rc);
             __builtin_amdgcn_sched_barrier(0);
         };
         static_for<8>(row);
@@ -1200,11 +1215,12 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
     constexpr int RP2 = 127 - WG >= 32 ? 2 : 1;          // MFMAs per F0 fragment read
-    static_assert(!X4 || EPI == EPI_BF16, "16-byte store epilogue: bf16 (+ bias) only");
+    static_assert(!X4 || EPI == EPI_BF16 || EPI == EPI_GELU, "16-byte store epilogue: bf16 (+ bias), bias + GELU");
     // the first wait after an epilogue: the copies it waits for precede the epilogue's VMEM ops
     // (>= 64 per wave for the per-tile-row epilogue, exactly PD_X4_VMEM for pd_store_x4) and the NB
     // copies issued since; vmcnt counts in issue order, so vmcnt(that sum) retires exactly the copies
-    constexpr int NB_EPI = (X4 ? PD_X4_VMEM : 64) + NB < 63 ? (X4 ? PD_X4_VMEM : 64) + NB : 63;
+    constexpr int EV = X4 ? pd_x4_vmem(EPI) : 64;
+    constexpr int NB_EPI = EV + NB < 63 ? EV + NB : 63;
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1354,7 +1370,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         acc_fence<48>(acc);
         __builtin_amdgcn_sched_barrier(0);
         auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
-        if constexpr (X4) pd_store_x4(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+        if constexpr (X4) pd_store_x4<EPI>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
         else epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         __builtin_amdgcn_sched_barrier(0);
         read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
@@ -1447,8 +1463,9 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         }
         const char* xe = std::getenv("TDL_PD_X4");   // "0": per-tile-row stores (A/B)
         const bool x4 = (N % 8 == 0) && (ldc % 8 == 0) && ((uintptr_t)C % 16 == 0) && !(xe && xe[0] == '0');
-        if (epi == EPI_BF16 && x4) {
-            gemm_pd<0, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
+        if ((epi == EPI_BF16 || epi == EPI_GELU) && x4 && (epi != EPI_GELU || (uintptr_t)aux % 16 == 0)) {
+            if (epi == EPI_BF16) gemm_pd<EPI_BF16, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
+            else gemm_pd<EPI_GELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             TDL_LAUNCH_CHECK();
         }
         switch (epi) {
