@@ -76,7 +76,10 @@ def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_
     N = b.shape[1]
     ta, lda = _operand_a(a)
     tb, ldb = _operand_b(b)
-    kid = KERNELS[kernel or KERNEL]
+    kn = kernel or KERNEL
+    if kn == "pd" and (ta or tb):   # pd takes k-contiguous (NT) operands only
+        kn = "pp"
+    kid = KERNELS[kn]
     _lib.call("tdl_gemm", ptr(a), ptr(b), ptr(c), ptr(bias), ptr(aux), ptr(colsum), M, N, K, lda, ldb, ldc,
               ta, tb, EPI[epi] | (kid << 8), int(split), int(split_stride), stream_ptr(a.device))
 
