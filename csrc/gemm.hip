@@ -1144,7 +1144,7 @@ __device__ __forceinline__ void mfma_run_pd(Acc& acc, const bf16x8_t (&a)[8], co
 // in-order vmcnt wait for every copy and store issued before it (the per-tile-row epilogue waits
 // that way once per column block).  Needs N % 8 == 0, ldc % 8 == 0.
 // VMEM instructions of pd_store_x4 per wave: 32 stores (bf16), 64 (GELU: pre-activation + output)
-constexpr int pd_x4_vmem(int epi) { return epi == EPI_GELU ? 64 : 32; }
+constexpr int pd_x4_vmem(int epi) { return epi == EPI_GELU ? 64 : epi == EPI_DGELU ? 68 : 32; }
 __device__ __forceinline__ void pd_bias_load(const GemmParams& p, int nw, int lane, u32x2_t (&braw)[8]) {
     const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias != nullptr ? (long long)p.N * 2 : 0);
 #pragma unroll
@@ -1198,6 +1198,80 @@ __device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int m
     static_for<4>(pair);
 }
 
+// dGELU epilogue with 16-byte accesses: d = acc * gelu'(pre), pre read from aux, bias-gradient
+// column sums of d into colsum (fp32 atomics).  The accumulators are swapped in fp32 (4 swaps per
+// tile pair and row block) so each lane holds 8 consecutive columns; all 32 pre-activation loads of
+// the wave are issued before the first store (one in-order wait for them, none behind the stores).
+// VMEM per wave: 32 loads + 32 stores + 4 atomics.
+template <class Get>
+__device__ __forceinline__ void pd_store_x4_dgelu(const GemmParams& p, Get& get, int mw, int nw, int lane) {
+    const int g = lane >> 4;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc((const char*)p.C + (size_t)mw * p.ldc * 2, (long long)(p.M - mw) * p.ldc * 2);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc((const char*)p.aux + (size_t)mw * p.ldc * 2, (long long)(p.M - mw) * p.ldc * 2);
+    const uint32_t lrow = (uint32_t)(lane & 15) * (uint32_t)p.ldc * 2u;
+    auto coloff = [&](int j) -> uint32_t {   // this lane's 8 columns of tile pair (j, j + 1)
+        const int nt = nw + 16 * (j + (g & 1)) + 8 * (g >> 1);
+        return nt < p.N ? (uint32_t)nt * 2u : 0x80000000u;
+    };
+    auto offset = [&](uint32_t col, int i) -> uint32_t {
+        return col == 0x80000000u ? col : lrow + (uint32_t)(16 * i) * (uint32_t)p.ldc * 2u + col;
+    };
+    u32x4_t pre[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) pre[q] = __builtin_amdgcn_raw_buffer_load_b128(rx, offset(coloff(2 * (q >> 3)), q & 7), 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    auto pair = [&](auto jc) {
+        constexpr int j = 2 * decltype(jc)::value;
+        const uint32_t col = coloff(j);
+        float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        auto row = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            const f32x4 a = get(std::integral_constant<int, i>{}, std::integral_constant<int, j>{});
+            const f32x4 b = get(std::integral_constant<int, i>{}, std::integral_constant<int, j + 1>{});
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[k]), __float_as_uint(b[k]), false, false);
+                v[k] = __uint_as_float(sw[0]);       // columns 0-3 of the lane's 8
+                v[4 + k] = __uint_as_float(sw[1]);   // columns 4-7
+            }
+            const u32x4_t u = pre[4 * j + i];   // (j / 2) * 8 + i
+            float pu[8];
+            unpack4(make_uint2(u.x, u.y), pu);
+            unpack4(make_uint2(u.z, u.w), pu + 4);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                v[c] *= gelu_tanh_grad(pu[c]);
+                cs[c] += v[c];
+            }
+            const uint2 lo = pack4(v), hi = pack4(v + 4);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{lo.x, lo.y, hi.x, hi.y}, rc, offset(col, i), 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for<8>(row);
+        if (p.colsum != nullptr) {
+            // the 16 lanes of a row group hold the same 8 columns for 16 rows: sum over them
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                float t = cs[c];
+                t += __shfl_xor(t, 1, 64);
+                t += __shfl_xor(t, 2, 64);
+                t += __shfl_xor(t, 4, 64);
+                t += __shfl_xor(t, 8, 64);
+                cs[c] = t;
+            }
+            const int c = lane & 7;
+            float t = cs[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) t = c == k ? cs[k] : t;
+            const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.colsum, (long long)p.N * 4);
+            const bool writer = (lane & 15) < 8 && col != 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(t, rs, writer ? col * 2u + (uint32_t)c * 4u : 0x80000000u, 0, 0);
+        }
+    };
+    static_for<4>(pair);
+}
+
 // s_waitcnt vmcnt(n) with expcnt / lgkmcnt at their no-wait maxima (gfx9 encoding)
 constexpr int vmcnt_enc(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 // copies of a step issued before global MFMA slot wg (slots ds + dp i, i < 16)
@@ -1215,7 +1289,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
     constexpr int RP2 = 127 - WG >= 32 ? 2 : 1;          // MFMAs per F0 fragment read
-    static_assert(!X4 || EPI == EPI_BF16 || EPI == EPI_GELU, "16-byte store epilogue: bf16 (+ bias), bias + GELU");
+    static_assert(!X4 || EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU, "16-byte epilogues: bf16, GELU, dGELU");
     // the first wait after an epilogue: the copies it waits for precede the epilogue's VMEM ops
     // (>= 64 per wave for the per-tile-row epilogue, exactly PD_X4_VMEM for pd_store_x4) and the NB
     // copies issued since; vmcnt counts in issue order, so vmcnt(that sum) retires exactly the copies
@@ -1315,7 +1389,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         constexpr bool ZERO = decltype(zc)::value, LAST = decltype(lc)::value;
         const int cur = s & 1, nxt = cur ^ 1;
         char* cstage = smem + cur * STAGE_BYTES;
-        if constexpr (X4 && LAST) pd_bias_load(p, bias_n0, lane, braw);   // ahead of this step's copies
+        if constexpr (X4 && LAST && EPI != EPI_DGELU) pd_bias_load(p, bias_n0, lane, braw);   // ahead of this step's copies
         produce_rsrc();
         auto slot = [&](auto gc, const uint32_t* fb) {
             constexpr int g = decltype(gc)::value;
@@ -1370,7 +1444,8 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         acc_fence<48>(acc);
         __builtin_amdgcn_sched_barrier(0);
         auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
-        if constexpr (X4) pd_store_x4<EPI>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+        if constexpr (X4 && EPI == EPI_DGELU) pd_store_x4_dgelu(p, get, cm0 + wm * 128, cn0 + wn * 128, lane);
+        else if constexpr (X4) pd_store_x4<EPI>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
         else epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         __builtin_amdgcn_sched_barrier(0);
         read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
@@ -1463,9 +1538,10 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         }
         const char* xe = std::getenv("TDL_PD_X4");   // "0": per-tile-row stores (A/B)
         const bool x4 = (N % 8 == 0) && (ldc % 8 == 0) && ((uintptr_t)C % 16 == 0) && !(xe && xe[0] == '0');
-        if ((epi == EPI_BF16 || epi == EPI_GELU) && x4 && (epi != EPI_GELU || (uintptr_t)aux % 16 == 0)) {
+        if ((epi == EPI_BF16 || epi == EPI_GELU || epi == EPI_DGELU) && x4 && (epi == EPI_BF16 || (uintptr_t)aux % 16 == 0)) {
             if (epi == EPI_BF16) gemm_pd<EPI_BF16, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
-            else gemm_pd<EPI_GELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
+            else if (epi == EPI_GELU) gemm_pd<EPI_GELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
+            else gemm_pd<EPI_DGELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             TDL_LAUNCH_CHECK();
         }
         switch (epi) {

@@ -34,6 +34,7 @@ KERNEL = os.environ.get("TDL_GEMM_KERNEL", "pp")        # bf16-output products (
 # the bias + GELU product (the MLP fc forward) on the LDS-DMA kernel's 16-byte-store epilogue: +0.4 %
 # per step over the ping-pong kernel, 3 of 3 interleaved rounds (profiles/r5_gemm_pd_gelu_ab.txt)
 GELU_KERNEL = os.environ.get("TDL_GEMM_GELU_KERNEL", "pd")
+DGELU_KERNEL = os.environ.get("TDL_GEMM_DGELU_KERNEL", "")   # the dGELU product (proj dgrad); "" = KERNEL
 WGRAD_KERNEL = os.environ.get("TDL_WGRAD_KERNEL", "p4")  # fp32 weight-gradient products
 
 
@@ -102,7 +103,7 @@ def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None
     if epi == "dgelu" and _operand_a(a)[0]:
         raise ValueError("dgelu needs a row-major A (rows past M must read as zero for the column sums)")
     _launch(a, b, out, out.stride(0), epi, bias=bias, aux=aux, colsum=colsum,
-            kernel=(GELU_KERNEL or None) if epi == "gelu" else None)
+            kernel=(GELU_KERNEL or None) if epi == "gelu" else (DGELU_KERNEL or None) if epi == "dgelu" else None)
     return out
 
 
