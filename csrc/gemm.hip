@@ -1284,9 +1284,9 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // Schedule (global MFMA slot g = 64 half + T of a K step): RP = MFMAs per F1 fragment read at the
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
-template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0>
+template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
-    static_assert(DS > 16 * RP + 2 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
+    static_assert(B1 >= 16 * RP + 2 && DS > B1 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
     constexpr int RP2 = 127 - WG >= 32 ? 2 : 1;          // MFMAs per F0 fragment read
     static_assert(!X4 || EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_DGELU, "16-byte epilogues: bf16, GELU, dGELU");
@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
                 if constexpr ((k < 8) == (ORD == 0)) b1[k & 7] = frag_at(fb[0], k & 7);
                 else a1[k & 7] = frag_at(fb[1], k & 7);
             }
-            if constexpr (g == 16 * RP + 2) {   // own reads of stage cur retired; then all waves'
+            if constexpr (g == B1) {   // own reads of stage cur retired; then all waves'
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
             }
@@ -1532,6 +1532,9 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
                 case 3: gemm_pd<0, 2, 36, 6, 100><<<grid, PNTHR, 0, s>>>(p); break;
                 case 4: gemm_pd<0, 1, 19, 7, 104><<<grid, PNTHR, 0, s>>>(p); break;
                 case 6: gemm_pd<0, 1, 20, 7, 100, true, 1><<<grid, PNTHR, 0, s>>>(p); break;
+                case 7: gemm_pd<0, 1, 26, 6, 100, true, 0, 24><<<grid, PNTHR, 0, s>>>(p); break;
+                case 8: gemm_pd<0, 1, 24, 6, 100, true, 0, 22><<<grid, PNTHR, 0, s>>>(p); break;
+                case 9: gemm_pd<0, 1, 30, 6, 104, true, 0, 28><<<grid, PNTHR, 0, s>>>(p); break;
                 default: gemm_pd<0, 1, 20, 7, 108><<<grid, PNTHR, 0, s>>>(p); break;
             }
             TDL_LAUNCH_CHECK();
