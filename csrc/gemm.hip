@@ -1284,7 +1284,8 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // Schedule (global MFMA slot g = 64 half + T of a K step): RP = MFMAs per F1 fragment read at the
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
-template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2>
+template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2,
+          bool TA = false, bool TB = false>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(B1 >= 16 * RP + 2 && DS > B1 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
@@ -1319,7 +1320,10 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     // step it repeats that step (into a stage nobody reads any more)
     int pi = 0, pt = 0, pm0, pn0, psp, pleft = total;
     coords(0, pm0, pn0, psp);
-    Stager<false, 4> sa, sb;   // k-contiguous images: the lane offsets do not depend on the tile
+    // k-contiguous images: lane offsets independent of the tile; row-contiguous (TA / TB: the weight
+    // gradients) ones clamp ragged columns per tile, so the producer re-inits them with each tile
+    Stager<TA, 4> sa;
+    Stager<TB, 4> sb;
     sa.init(p.lda, pm0, p.M, w, lane);
     sb.init(p.ldb, pn0, p.N, w, lane);
     __amdgpu_buffer_rsrc_t qa, qb;
@@ -1334,6 +1338,8 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
                 pt = 0;
                 ++pi;
                 coords(pi, pm0, pn0, psp);
+                if constexpr (TA) sa.init(p.lda, pm0, p.M, w, lane);
+                if constexpr (TB) sb.init(p.ldb, pn0, p.N, w, lane);
             }
         } else {
             pleft = 0;
@@ -1344,10 +1350,12 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     auto copy_piece = [&](char* stage, auto ic) {
         constexpr int i = decltype(ic)::value;
         constexpr int j = i & 7;
-        const Stager<false, 4>& st = i < 8 ? sa : sb;
+        constexpr bool TR = i < 8 ? TA : TB;
+        const uint32_t vo = i < 8 ? sa.base[TR ? (j & 1) : 0] : sb.base[TR ? (j & 1) : 0];
+        const uint32_t dl = i < 8 ? sa.delta : sb.delta;
         char* dst = stage + (i < 8 ? 0 : TILE_BYTES) + (w + 4 * j) * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 8 ? qa : qb, (lds_void_t*)dst, 16, st.base[0],
-                                                 __builtin_amdgcn_readfirstlane((uint32_t)j * st.delta), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 8 ? qa : qb, (lds_void_t*)dst, 16, vo,
+                                                 __builtin_amdgcn_readfirstlane((uint32_t)j * dl), 0, 0);
     };
     auto frag_base = [&](bool isB, int buf, int ks) -> uint32_t {
         const int wb = isB ? wn : wm;
@@ -1357,15 +1365,23 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         return v;
     };
     auto frag_at = [&](uint32_t base, int t) -> bf16x8_t { return *(const bf16x8_t*)(smem + base + t * 16 * 128); };
+    // fragment t of operand B (isB) / A, k-half ks, stage buf: the k-contiguous image through a
+    // per-lane base + immediate offsets, the row-contiguous one through the transposing read
+    auto frag_x = [&](bool isB, uint32_t base, int buf, int t, int ks) -> bf16x8_t {
+        if (isB ? TB : TA)
+            return isB ? frag<TB>(smem + buf * STAGE_BYTES + TILE_BYTES, wn * 128 + 16 * t, ks, lane)
+                       : frag<TA>(smem + buf * STAGE_BYTES, wm * 128 + 16 * t, ks, lane);
+        return frag_at(base, t);
+    };
 
     bf16x8_t a0[8], b0[8], a1[8], b1[8];
     Acc acc;
     auto read_f0 = [&](int buf) {
         const uint32_t bb = frag_base(true, buf, 0), ba = frag_base(false, buf, 0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b0[j] = frag_at(bb, j);
+        for (int j = 0; j < 8; ++j) b0[j] = frag_x(true, bb, buf, j, 0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) a0[i] = frag_at(ba, i);
+        for (int i = 0; i < 8; ++i) a0[i] = frag_x(false, ba, buf, i, 0);
     };
     {   // prologue: steps 0 and 1 -> stages 0 and 1; F0 = step 0's k-half 0
         produce_rsrc();
@@ -1395,8 +1411,8 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
             constexpr int g = decltype(gc)::value;
             if constexpr (g < 16 * RP && g % RP == RP - 1) {   // F1 = k-half 1 of step s (stage cur)
                 constexpr int k = g / RP;
-                if constexpr ((k < 8) == (ORD == 0)) b1[k & 7] = frag_at(fb[0], k & 7);
-                else a1[k & 7] = frag_at(fb[1], k & 7);
+                if constexpr ((k < 8) == (ORD == 0)) b1[k & 7] = frag_x(true, fb[0], cur, k & 7, 1);
+                else a1[k & 7] = frag_x(false, fb[1], cur, k & 7, 1);
             }
             if constexpr (g == B1) {   // own reads of stage cur retired; then all waves'
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1411,8 +1427,8 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
             }
             if constexpr (!LAST && g > WG && (g - WG - 1) % RP2 == 0 && (g - WG - 1) / RP2 < 16) {
                 constexpr int k = (g - WG - 1) / RP2;   // F0 = k-half 0 of step s + 1 (stage nxt)
-                if constexpr ((k < 8) == (ORD == 0)) b0[k & 7] = frag_at(fb[2], k & 7);
-                else a0[k & 7] = frag_at(fb[3], k & 7);
+                if constexpr ((k < 8) == (ORD == 0)) b0[k & 7] = frag_x(true, fb[2], nxt, k & 7, 0);
+                else a0[k & 7] = frag_x(false, fb[3], nxt, k & 7, 0);
             }
         };
         const uint32_t fb[4] = {frag_base(true, cur, 1), frag_base(false, cur, 1), frag_base(true, nxt, 0),
@@ -1518,10 +1534,18 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     gemm_p4<P4_TA, P4_TB, P4_EPI, P4_LEPI><<<256, PNTHR, 0, s>>>(p);
     TDL_LAUNCH_CHECK();
 #else
-    if (kernel == 3) {  // gemm_pd: NT operands only
-        if (ta || tb || kps / BK < 2) return (int)hipErrorInvalidValue;
+    if (kernel == 3) {  // gemm_pd: NT operands, or TT (the weight gradients) with fp32 outputs
+        if (ta != tb || kps / BK < 2 || (ta && epi < EPI_F32)) return (int)hipErrorInvalidValue;
         const int items = p.tiles * split;
         const int grid = items < num_cus() ? items : num_cus();
+        if (ta) {
+            switch (epi) {
+                case EPI_F32: gemm_pd<EPI_F32, 1, 20, 7, 100, false, 0, 18, true, true><<<grid, PNTHR, 0, s>>>(p); break;
+                case EPI_F32ACC: gemm_pd<EPI_F32ACC, 1, 20, 7, 100, false, 0, 18, true, true><<<grid, PNTHR, 0, s>>>(p); break;
+                default: gemm_pd<EPI_F32ATOM, 1, 20, 7, 100, false, 0, 18, true, true><<<grid, PNTHR, 0, s>>>(p); break;
+            }
+            TDL_LAUNCH_CHECK();
+        }
         // schedule variants (plain bf16 epilogue only): TDL_PD_SCHED, read per launch (in-process A/B)
         const char* sv = std::getenv("TDL_PD_SCHED");
         const int v = (sv && epi == EPI_BF16) ? std::atoi(sv) : 0;

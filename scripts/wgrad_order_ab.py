@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--only", default="")
+    ap.add_argument("--kernels", default="p4", help="weight-gradient kernels to compare (p4, pd)")
     args = ap.parse_args()
     T, C = args.tokens, 1024
     prods = [("qkv_wgrad", C, 3 * C), ("o_wgrad", C, C), ("fc_wgrad", C, 4 * C), ("proj_wgrad", 4 * C, C)]
@@ -49,12 +50,13 @@ def main():
         auto = gemm.wgrad_split(T, cin, cout)
         splits = sorted({auto if s == "auto" else int(s) for s in args.splits.split(",")})
         fns = {}
-        for sp in splits:
-            for g in groups:
-                def f(g=g, sp=sp):
-                    os.environ["TDL_GEMM_GROUPM"] = str(g)
-                    gemm.matmul_f32_acc(acc, x.t(), dy, split=sp)
-                fns[f"s{sp}_g{g}"] = f
+        for kn in args.kernels.split(","):
+            for sp in splits:
+                for g in groups:
+                    def f(g=g, sp=sp, kn=kn):
+                        os.environ["TDL_GEMM_GROUPM"] = str(g)
+                        gemm.matmul_f32_acc(acc, x.t(), dy, split=sp, kernel=kn)
+                    fns[f"{kn}_s{sp}_g{g}"] = f
         # correctness of every variant: one accumulation from zero against fp32
         ref = x.float().t() @ dy.float()
         bad = {}

@@ -78,7 +78,7 @@ def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_
     ta, lda = _operand_a(a)
     tb, ldb = _operand_b(b)
     kn = kernel or KERNEL
-    if kn == "pd" and (ta or tb):   # pd takes k-contiguous (NT) operands only
+    if kn == "pd" and (ta != tb or (ta and not epi.startswith("f32"))):   # pd: NT, or TT with fp32 out
         kn = "pp"
     kid = KERNELS[kn]
     _lib.call("tdl_gemm", ptr(a), ptr(b), ptr(c), ptr(bias), ptr(aux), ptr(colsum), M, N, K, lda, ldb, ldc,
