@@ -1,22 +1,190 @@
-// Backward-audit primitives for the commit-then-reveal gradient check (security/grad_audit.py,
-// parallel/commitments.py).  Reference: the gradient check there is a host z-score
-// (/root/reference/attack_detector.py:109-141) that a sign flip passes; r4's replacement sampled
-// 1/16 of the gradient under sign patterns derived from public values, which an adaptive adversary
-// can evade by perturbing only the unsampled coordinates or the null space of the public signs.
+// Backward-audit primitives of the commit / key / open gradient protocol (security/grad_audit.py,
+// parallel/commitments.py, parallel/audit.py).  Reference: the gradient check there is a host
+// z-score (/root/reference/attack_detector.py:109-141) that a sign flip passes, and the optimizer
+// step it is meant to guard (/root/reference/distributed_trainer.py:197-205, :441-446) applies
+// whatever gradient the node holds.
 //
-//  * word hash   — exact, order-independent 64-bit hash of a range of 32-bit words:
-//                  H = sum_j mix(w_j ^ mix(j ^ seed))  (mod 2^64, integer atomics: any launch order
-//                  gives the same bits), optionally copying the range into a snapshot in the same
-//                  pass.  Commits the running gradient after every micro-batch and the applied one.
-//  * keyed sketch — K = 4 full-coverage random-sign projections sum_j s_k(key, j) (a_j - b_j) with
-//                  the signs derived from a PRIVATE per-step key revealed only after the
-//                  commitments were sent; two-pass, fixed-order reduction (deterministic).
-// The mixing function is the same 32-bit integer mix as the CPU reference in grad_audit.py, so CPU
-// and GPU give identical hashes and signs (constants < 2^31: the CPU path multiplies in int64).
+//  * BLAKE2s Merkle hash — a collision-resistant 256-bit commitment to a range of 32-bit words:
+//      leaf j   = BLAKE2s(words [256 j, 256 j + 256) ; node_offset = j, node_depth = 0)
+//      node l,j = BLAKE2s(child digests [32 j, 32 j + 32) of level l - 1 ; node_offset = j, node_depth = l)
+//    up to one root per segment (at least one node level), then one combine over the segments'
+//    roots (node_depth = 255, last_node).  Bit-identical to Python's hashlib.blake2s with the same
+//    node parameters (the CPU path and the GPU tests use it as the oracle).  One thread per leaf /
+//    node: 16 compressions of 10 rounds each, integer VALU only; a batch dimension (grid.y) hashes
+//    the M per-micro-batch contributions of a step in one launch per tree level.
+//  * keyed sketch — K = 4 full-coverage random-sign projections sum_j s_k(key, j) a_j with the
+//    signs derived from a PRIVATE per-step key revealed only after the commitments were received;
+//    two-pass, fixed-order reduction (deterministic: the auditor recomputes the auditee's value
+//    bit for bit).  Batched over contributions (grid.y).
+//  * contribution snapshot — c_i = g - prev, prev = g after micro-batch i's weight gradients.
+//
+// (r5 used an additive mix32 word hash: a sum of invertible 32-bit mixes, so a second preimage
+// cost O(1) — set one word to mix^-1 of the difference — and it travelled folded to 32 bits.)
 #include "common.h"
 
 namespace {
 
+// ============================================================================ BLAKE2s
+__constant__ uint32_t kIV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                                0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+
+constexpr uint8_t kSigma[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+constexpr int LEAF_WORDS = 256;   // 1 KiB leaves: 16 compressions per thread
+constexpr int FANOUT = 32;        // 32 child digests (1 KiB) per internal node
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+template <int R>
+__device__ __forceinline__ void b2s_round(uint32_t* v, const uint32_t* m) {
+#define B2S_G(a, b, c, d, x, y)                 \
+    v[a] = v[a] + v[b] + (x);                   \
+    v[d] = rotr(v[d] ^ v[a], 16);               \
+    v[c] = v[c] + v[d];                         \
+    v[b] = rotr(v[b] ^ v[c], 12);               \
+    v[a] = v[a] + v[b] + (y);                   \
+    v[d] = rotr(v[d] ^ v[a], 8);                \
+    v[c] = v[c] + v[d];                         \
+    v[b] = rotr(v[b] ^ v[c], 7);
+    B2S_G(0, 4, 8, 12, m[kSigma[R][0]], m[kSigma[R][1]]);
+    B2S_G(1, 5, 9, 13, m[kSigma[R][2]], m[kSigma[R][3]]);
+    B2S_G(2, 6, 10, 14, m[kSigma[R][4]], m[kSigma[R][5]]);
+    B2S_G(3, 7, 11, 15, m[kSigma[R][6]], m[kSigma[R][7]]);
+    B2S_G(0, 5, 10, 15, m[kSigma[R][8]], m[kSigma[R][9]]);
+    B2S_G(1, 6, 11, 12, m[kSigma[R][10]], m[kSigma[R][11]]);
+    B2S_G(2, 7, 8, 13, m[kSigma[R][12]], m[kSigma[R][13]]);
+    B2S_G(3, 4, 9, 14, m[kSigma[R][14]], m[kSigma[R][15]]);
+#undef B2S_G
+}
+
+// one compression of block m (t: bytes hashed so far including this block; last: final block)
+__device__ __forceinline__ void b2s_compress(uint32_t* h, const uint32_t* m, uint32_t t, bool last, bool last_node) {
+    uint32_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        v[i] = h[i];
+        v[i + 8] = kIV[i];
+    }
+    v[12] ^= t;
+    v[14] ^= last ? 0xFFFFFFFFu : 0u;
+    v[15] ^= last_node ? 0xFFFFFFFFu : 0u;
+    b2s_round<0>(v, m);
+    b2s_round<1>(v, m);
+    b2s_round<2>(v, m);
+    b2s_round<3>(v, m);
+    b2s_round<4>(v, m);
+    b2s_round<5>(v, m);
+    b2s_round<6>(v, m);
+    b2s_round<7>(v, m);
+    b2s_round<8>(v, m);
+    b2s_round<9>(v, m);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
+}
+
+// parameter block of a 32-byte, unkeyed digest with fanout 1, depth 1 (hashlib's defaults) and the
+// given node offset (< 2^32 here) / node depth
+__device__ __forceinline__ void b2s_init(uint32_t* h, uint32_t node_offset, uint32_t node_depth) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kIV[i];
+    h[0] ^= 32u | (1u << 16) | (1u << 24);
+    h[2] ^= node_offset;
+    h[3] ^= node_depth << 16;
+}
+
+// hash `nw` >= 1 words read by `load(block, m)` (block b: words [16 b, 16 b + 16), zero padded)
+template <class Load>
+__device__ __forceinline__ void b2s_words(uint32_t* h, int nw, bool last_node, Load load) {
+    const int nblk = (nw + 15) >> 4;
+    uint32_t m[16];
+    for (int b = 0; b < nblk; ++b) {
+        load(b, m);
+        const bool last = b == nblk - 1;
+        const uint32_t t = last ? (uint32_t)nw * 4u : (uint32_t)(b + 1) * 64u;
+        b2s_compress(h, m, t, last, last_node);
+    }
+}
+
+// leaves: out[y][j] = leaf digest j of x[y * stride + lo : y * stride + hi)
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void b2s_leaf_kernel(const uint32_t* __restrict__ x, long long stride, long long lo,
+                                                      long long hi, long long nleaf, uint32_t* __restrict__ out,
+                                                      long long out_stride) {
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nleaf) return;
+    const uint32_t* src = x + (long long)blockIdx.y * stride + lo + j * LEAF_WORDS;
+    const long long rem = hi - lo - j * LEAF_WORDS;
+    const int nw = rem < LEAF_WORDS ? (int)rem : LEAF_WORDS;
+    uint32_t h[8];
+    b2s_init(h, (uint32_t)j, 0u);
+    b2s_words(h, nw, false, [&](int b, uint32_t* m) {
+        const int w0 = b * 16;
+        if (ALIGNED && w0 + 16 <= nw) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src + w0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 u = s4[q];
+                m[4 * q] = u.x;
+                m[4 * q + 1] = u.y;
+                m[4 * q + 2] = u.z;
+                m[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) m[q] = w0 + q < nw ? src[w0 + q] : 0u;
+        }
+    });
+    uint32_t* o = out + (long long)blockIdx.y * out_stride + j * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = h[i];
+}
+
+// internal nodes: out[y][j] = node j over children [F j, F j + F) of in[y] (n_in digests)
+__global__ __launch_bounds__(256) void b2s_node_kernel(const uint32_t* __restrict__ in, long long in_stride,
+                                                      long long n_in, int fan, uint32_t depth, int last_node,
+                                                      uint32_t* __restrict__ out, long long out_stride,
+                                                      long long n_out) {
+    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n_out) return;
+    const uint32_t* src = in + (long long)blockIdx.y * in_stride + j * fan * 8;
+    const long long rem = n_in - j * fan;
+    const int nch = rem < fan ? (int)rem : fan;
+    uint32_t h[8];
+    b2s_init(h, (uint32_t)j, depth);
+    b2s_words(h, nch * 8, last_node != 0, [&](int b, uint32_t* m) {
+        const int w0 = b * 16;
+        const int nw = nch * 8;
+        if (w0 + 16 <= nw) {
+            const uint4* s4 = reinterpret_cast<const uint4*>(src + w0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 u = s4[q];
+                m[4 * q] = u.x;
+                m[4 * q + 1] = u.y;
+                m[4 * q + 2] = u.z;
+                m[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) m[q] = w0 + q < nw ? src[w0 + q] : 0u;
+        }
+    });
+    uint32_t* o = out + (long long)blockIdx.y * out_stride + j * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = h[i];
+}
+
+// ============================================================================ keyed sketch
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -26,45 +194,19 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
 constexpr int HB = 256;
 
-// acc += sum over j in [lo, hi) of mix(x[j] ^ mix(j ^ seed)); dst (nullable): dst[j] = x[j]
-__global__ __launch_bounds__(HB) void word_hash_kernel(const uint32_t* __restrict__ x, uint32_t* __restrict__ dst,
-                                                      long long lo, long long hi, uint32_t seed,
-                                                      unsigned long long* __restrict__ acc) {
-    __shared__ unsigned long long red[HB / 64];
-    unsigned long long s = 0;
-    const long long stride = (long long)gridDim.x * HB;
-    for (long long j = lo + (long long)blockIdx.x * HB + threadIdx.x; j < hi; j += stride) {
-        const uint32_t w = x[j];
-        if (dst != nullptr) dst[j] = w;
-        s += mix32(w ^ mix32((uint32_t)j ^ seed));
-    }
-    s = wave_sum_u64(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long t = 0;
-#pragma unroll
-        for (int i = 0; i < HB / 64; ++i) t += red[i];
-        atomicAdd(acc, t);   // integer add: exact and order-independent
-    }
-}
-
-// part[block][k] = sum over this block's j of s_k(key, j) * (a[j] - b[j])   (b nullable)
-__global__ __launch_bounds__(HB) void keyed_sketch_partial_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                                 long long lo, long long hi, uint32_t k0, uint32_t k1,
+// part[y][block][k] = sum over this block's j of s_k(key, j) * (a[y][j] - b[j])   (b nullable)
+__global__ __launch_bounds__(HB) void keyed_sketch_partial_kernel(const float* __restrict__ a, long long stride,
+                                                                 const float* __restrict__ b, long long lo,
+                                                                 long long hi, uint32_t k0, uint32_t k1,
                                                                  float* __restrict__ part) {
     __shared__ float red[HB / 64][4];
+    a += (long long)blockIdx.y * stride;
+    part += (long long)blockIdx.y * gridDim.x * 4;
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    const long long stride = (long long)gridDim.x * HB;
-    for (long long j = lo + (long long)blockIdx.x * HB + threadIdx.x; j < hi; j += stride) {
+    const long long step = (long long)gridDim.x * HB;
+    for (long long j = lo + (long long)blockIdx.x * HB + threadIdx.x; j < hi; j += step) {
         const float v = b != nullptr ? a[j] - b[j] : a[j];
         const uint32_t h = mix32(mix32((uint32_t)j ^ k0) ^ k1);
 #pragma unroll
@@ -85,10 +227,12 @@ __global__ __launch_bounds__(HB) void keyed_sketch_partial_kernel(const float* _
     }
 }
 
-// out[k] (+)= sum over blocks of part[.][k], in block order (one wave per k)
-__global__ __launch_bounds__(256) void keyed_sketch_final_kernel(const float* __restrict__ part, int nb, float* __restrict__ out,
-                                                                int accumulate) {
+// out[y][k] (+)= sum over blocks of part[y][.][k], in block order (one wave per k, one block per y)
+__global__ __launch_bounds__(256) void keyed_sketch_final_kernel(const float* __restrict__ part, int nb,
+                                                                float* __restrict__ out, int accumulate) {
     const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    part += (long long)blockIdx.x * nb * 4;
+    out += blockIdx.x * 4;
     float t = 0.f;
     for (int i = lane; i < nb; i += 64) t += part[i * 4 + k];
     t = wave_sum(t);
@@ -100,28 +244,72 @@ int grid_for(long long n, int cap) {
     return (int)(b < 1 ? 1 : b > cap ? cap : b);
 }
 
+// ============================================================================ contribution snapshot
+// c = g - prev ; prev = g   (fp32, elementwise; the subtraction the CPU path does in torch)
+__global__ __launch_bounds__(256) void contrib_snap_kernel(const float* __restrict__ g, float* __restrict__ prev,
+                                                          float* __restrict__ c, long long n) {
+    const long long step = (long long)gridDim.x * 256;
+    for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < n; j += step) {
+        const float v = g[j];
+        c[j] = v - prev[j];
+        prev[j] = v;
+    }
+}
+
 }  // namespace
 
-// acc (device uint64, caller-zeroed) += word hash of x[lo:hi) (32-bit words); dst (nullable) gets a copy
-TDL_API int tdl_word_hash(const void* x, void* dst, long long lo, long long hi, unsigned int seed,
-                          unsigned long long* acc, hipStream_t s) {
-    if (hi <= lo) return 0;
-    word_hash_kernel<<<grid_for(hi - lo, 2048), HB, 0, s>>>((const uint32_t*)x, (uint32_t*)dst, lo, hi, seed, acc);
+// ---- BLAKE2s Merkle levels (the Python side walks the tree: grad_audit.merkle_roots)
+TDL_API long long tdl_b2s_leaf_words() { return LEAF_WORDS; }
+TDL_API long long tdl_b2s_fanout() { return FANOUT; }
+
+// out[y][0..nleaf) digests of x[y * stride + lo : ... + hi), y < batch
+TDL_API int tdl_b2s_leaves(const void* x, long long stride, int batch, long long lo, long long hi, void* out,
+                           long long out_stride, hipStream_t s) {
+    if (hi <= lo || batch <= 0) return 0;
+    const long long nleaf = (hi - lo + LEAF_WORDS - 1) / LEAF_WORDS;
+    const dim3 grid((unsigned)((nleaf + 255) / 256), (unsigned)batch);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && ((lo & 3) == 0) && ((stride & 3) == 0);
+    if (aligned)
+        b2s_leaf_kernel<true><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out, out_stride);
+    else
+        b2s_leaf_kernel<false><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out, out_stride);
     TDL_LAUNCH_CHECK();
 }
 
-// number of partial rows the keyed sketch uses (workspace: 4 floats each)
+// out[y][0..n_out) = nodes over in[y][0..n_in), fan children each (in / out strides in uint32 words)
+TDL_API int tdl_b2s_nodes(const void* in, long long in_stride, long long n_in, int batch, int fan, int depth,
+                          int last_node, void* out, long long out_stride, hipStream_t s) {
+    if (n_in <= 0 || batch <= 0) return 0;
+    const long long n_out = (n_in + fan - 1) / fan;
+    const dim3 grid((unsigned)((n_out + 255) / 256), (unsigned)batch);
+    b2s_node_kernel<<<grid, 256, 0, s>>>((const uint32_t*)in, in_stride, n_in, fan, (uint32_t)depth, last_node,
+                                         (uint32_t*)out, out_stride, n_out);
+    TDL_LAUNCH_CHECK();
+}
+
+// number of partial rows the keyed sketch uses per batch entry (workspace: 4 floats each)
 TDL_API long long tdl_keyed_sketch_ws_floats(long long n) { return 4LL * grid_for(n, 1024); }
 
-// out[0..3] (+)= keyed sketch of (a - b)[lo:hi) (b nullable) under key (k0, k1); ws >= ws_floats
-TDL_API int tdl_keyed_sketch(const float* a, const float* b, long long lo, long long hi, unsigned int k0,
-                             unsigned int k1, float* ws, float* out, int accumulate, hipStream_t s) {
+// out[y][0..3] (+)= keyed sketch of (a[y] - b)[lo:hi) (b nullable) under key (k0, k1), y < batch;
+// ws >= batch * ws_floats(hi - lo)
+TDL_API int tdl_keyed_sketch(const float* a, long long stride, int batch, const float* b, long long lo, long long hi,
+                             unsigned int k0, unsigned int k1, float* ws, float* out, int accumulate, hipStream_t s) {
+    if (batch <= 0) return 0;
     if (hi <= lo) {
-        if (!accumulate) hipMemsetAsync(out, 0, 4 * sizeof(float), s);
+        if (!accumulate) hipMemsetAsync(out, 0, 4 * sizeof(float) * batch, s);
         TDL_LAUNCH_CHECK();
     }
     const int nb = grid_for(hi - lo, 1024);
-    keyed_sketch_partial_kernel<<<nb, HB, 0, s>>>(a, b, lo, hi, k0, k1, ws);
-    keyed_sketch_final_kernel<<<1, 256, 0, s>>>(ws, nb, out, accumulate);
+    keyed_sketch_partial_kernel<<<dim3(nb, batch), HB, 0, s>>>(a, stride, b, lo, hi, k0, k1, ws);
+    keyed_sketch_final_kernel<<<batch, 256, 0, s>>>(ws, nb, out, accumulate);
+    TDL_LAUNCH_CHECK();
+}
+
+// c = g - prev; prev = g  (n fp32)
+TDL_API int tdl_contrib_snap(const float* g, float* prev, float* c, long long n, hipStream_t s) {
+    if (n <= 0) return 0;
+    long long nb = (n + 256 * 8 - 1) / (256 * 8);
+    if (nb > 4096) nb = 4096;
+    contrib_snap_kernel<<<(int)nb, 256, 0, s>>>(g, prev, c, n);
     TDL_LAUNCH_CHECK();
 }

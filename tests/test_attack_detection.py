@@ -113,3 +113,17 @@ def test_ground_truth_counters():
     det.detect_output_anomaly(torch.randn(512, generator=g) * 5 + 3, 0, 30, ground_truth=True)
     st = det.get_detection_statistics()
     assert st["precision"] == 1.0 and st["recall"] == 1.0
+
+
+def test_quantiles_propagate_nan_like_numpy():
+    """the one-partition quantiles must return NaN for an input holding a NaN, as
+    np.median / np.percentile (the reference definitions, attack_detector.py:192-196) do."""
+    import numpy as np
+    from trustworthy_dl.security.attack_detection import _quantiles, numpy_tensor_statistics
+    x = np.random.default_rng(0).standard_normal(1001).astype(np.float32)
+    ref = [float(np.percentile(x, 25)), float(np.median(x)), float(np.percentile(x, 75))]
+    assert np.allclose(_quantiles(x, (0.25, 0.5, 0.75)), ref)
+    x[17] = np.nan
+    got = _quantiles(x, (0.25, 0.5, 0.75))
+    assert all(np.isnan(v) for v in got) and np.isnan(np.median(x))
+    assert np.isnan(numpy_tensor_statistics(x)["median"])

@@ -219,10 +219,10 @@ def _worker(rank, world, port, out_path, attack, targets, atk_kw, micro, cfg=Non
     ("byzantine_backward", (2,), None, "gradient_tampering"),                      # the loss stage
     ("gradient_poisoning", (0,), {"gradient_mode": "sign_flip"}, "gradient_poisoning"),
     ("model_poisoning", (1,), {"lie_integrity": True}, "model_poisoning"),         # lies about its checksum
-    # rewrites its gradient after the backward and reports, in its own row, a last commitment equal
-    # to what it applies: its auditor holds the commitment it really sent (D_GCOM_RECV_*)
-    pytest.param("gradient_poisoning", (1,), {"gradient_mode": "sign_flip", "lie_commitment": True},
-                 "gradient_poisoning", id="lie_commitment"),
+    # rewrites its gradient after the backward (a rank that also lies in its reports is in
+    # tests/test_lying_rank.py): the applied gradient is not the sum of the committed contributions
+    pytest.param("gradient_poisoning", (1,), {"gradient_mode": "sign_flip"}, "gradient_poisoning",
+                 id="post_backward_rewrite"),
     (None, (), None, None)])
 @pytest.mark.slow
 def test_distributed_backward_audit(attack, targets, atk_kw, kind):

@@ -4,9 +4,10 @@ r4's gradient commitments were sketches under PUBLIC sign patterns over a public
 the gradient (security/grad_audit.GradSketch): an adversary that knows the job seed, the step and
 the stage's layer range tampers only the coordinates the sketch does not read, and both checks —
 applied-vs-committed and the audited micro-batch's recomputed contribution — pass.  The binding
-checks are now an exact hash of the running gradient (every coordinate) and a keyed full-coverage
-sketch under a key the auditor reveals only after the commitments (csrc/audit.hip).  CPU, local
-mode and gloo ranks; tiny GPT-2."""
+checks are now BLAKE2s Merkle commitments of every micro-batch's contribution and of the applied
+gradient (every coordinate), keyed full-coverage sketches under a key the auditor reveals only after
+it received the commitments, and a live optimizer mirror (csrc/audit.hip, parallel/commitments.py).
+CPU, local mode; tiny GPT-2."""
 import pytest
 import torch
 
@@ -54,7 +55,7 @@ def test_adaptive_tamper_is_invisible_to_the_public_sketch():
     t = g + delta
     assert torch.equal(sk(g, off), sk(t, off))                      # r4's commitment: no difference
     segs = ga._segments(n)
-    assert int(ga.word_hash(g, segs)) != int(ga.word_hash(t, segs))
+    assert not torch.equal(ga.merkle_root(g, segs), ga.merkle_root(t, segs))
     key = 0x1234_5678_9ABC
     a, b = ga.keyed_sketch(g, segs, key), ga.keyed_sketch(t, segs, key)
     assert float((a - b).abs().max()) > 0.5 * float(delta.norm())   # ~ ||delta|| per sign vector
@@ -72,13 +73,13 @@ def test_keyed_sketch_linear_and_masked():
     a2 = a.clone()
     a2[1500] += 100.0
     assert torch.equal(ga.keyed_sketch(a2, segs, k), ga.keyed_sketch(a, segs, k))
-    assert int(ga.word_hash(a2, segs)) == int(ga.word_hash(a, segs))
+    assert torch.equal(ga.merkle_root(a2, segs), ga.merkle_root(a, segs))
     assert not torch.allclose(ga.keyed_sketch(a, segs, k), ga.keyed_sketch(a, segs, k + 1))
 
 
 def test_local_adaptive_post_backward_caught_every_step():
-    """Adaptive tamper between backward and optimizer: the applied gradient's exact hash differs
-    from the last committed one on every tampered step; only the target is blamed."""
+    """Adaptive tamper between backward and optimizer: the applied gradient's keyed sketch is no
+    longer the sum of the committed contributions' on every tampered step; only the target is blamed."""
     eng, att = _engine(3, targets=(1,), start=4, micro=2)
     for b in _batches(8):
         eng.train_step(b)

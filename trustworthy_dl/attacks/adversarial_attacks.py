@@ -71,8 +71,6 @@ class AttackConfig:
     label_flip_fraction: Optional[float] = None  # default intensity
     micro_batches: Optional[int] = None  # tamper only this many of the step's micro-batches (None: all)
     lie_integrity: bool = False          # the target reports its weight-integrity check as passing
-    lie_commitment: bool = False         # the target reports its last gradient commitment as equal to
-                                         # the (tampered) gradient it applies, in its own digest row
     adaptive: bool = False               # gradient tampers avoid everything the public sketch samples
     seed: int = 1234
 
@@ -139,9 +137,6 @@ class AdversarialAttacker:
 
     def lies_about_integrity(self, node: int, step: int) -> bool:
         return self.config.lie_integrity and self.active and node in self.config.target_nodes
-
-    def lies_about_commitment(self, node: int, step: int) -> bool:
-        return self.config.lie_commitment and self.active and node in self.config.target_nodes
 
     def _log(self, kind: str, node: int, step: int, **info):
         self.injections.append({"type": kind, "node": node, "step": step, "timestamp": time.time(), **info})

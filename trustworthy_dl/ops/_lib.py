@@ -146,9 +146,11 @@ _SIGNATURES = {
     "tdl_gemm": [_P] * 6 + [_I] * 10 + [_L, _P],
     "tdl_gemm_set_timestamps": [_P],
     # audit.hip
-    "tdl_word_hash": [_P, _P, _L, _L, ctypes.c_uint32, _P, _P],
+    "tdl_b2s_leaves": [_P, _L, _I, _L, _L, _P, _L, _P],
+    "tdl_b2s_nodes": [_P, _L, _L, _I, _I, _I, _I, _P, _L, _P],
     "tdl_keyed_sketch_ws_floats": [_L],
-    "tdl_keyed_sketch": [_P, _P, _L, _L, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I, _P],
+    "tdl_keyed_sketch": [_P, _L, _I, _P, _L, _L, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I, _P],
+    "tdl_contrib_snap": [_P, _P, _P, _L, _P],
     # conv.hip / bn.hip
     "tdl_conv_nt": [_P] * 5 + [_I] * 12 + [_P],
     "tdl_conv_stats_ws_floats": [_I, _I],

@@ -64,13 +64,13 @@ class AttributionMixin:
         blame = torch.zeros_like(of)
         evidence = torch.zeros_like(of)
         self.t_taint.copy_(torch.maximum(self.t_taint, (pf > 0).float()))
-        audited = self._audit_now
+        audited = self._audit_now or self._gsk_on
         akind = torch.zeros_like(of)
         if audited:
             akind, _ = self._audit_vectors(D)
         abad = (akind > 0).float()
-        # applied gradient != committed backward contributions: rewritten after the backward
-        gbad = self._gsk_mismatch(D) if self.cfg.audit and self.cfg.audit_backward else torch.zeros_like(of)
+        # a tied-weight member applying something else than the sum of the members' contributions
+        gbad = self._tied_mismatch(D) if self._gsk_on else torch.zeros_like(of)
         # proof of tampering (not a statistic): compromises at once (compromise_on_proof)
         self._proof = torch.maximum(torch.maximum((pf > 0).float(), abad), gbad)
         self._proof_kind = akind + gbad * 32.0
@@ -248,6 +248,6 @@ class AttributionMixin:
             return "output_tampering"
         if kind & (SV.AK_DX | SV.AK_DXHASH):
             return "gradient_tampering"
-        if kind & (SV.AK_DW | 32):
+        if kind & (SV.AK_DW | SV.AK_GAPP):
             return "gradient_poisoning"
         return "output_anomaly" if out_flag and not self.cfg.audit else "gradient_poisoning"

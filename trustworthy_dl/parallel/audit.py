@@ -1,14 +1,17 @@
-"""Deterministic recompute audit of ``PipelineEngine``: every stage is audited by the stage that
-received its output (the loss stage by its predecessor) on privately chosen micro-batches —
-forward output, input gradient and weight-gradient contribution are recomputed on the auditor.
-Local mode here; the distributed protocol is in ``audit_dist.py``.
+"""Deterministic recompute audit of ``PipelineEngine``, auditor side: every stage is audited by the
+stage that received its output (the loss stage by its predecessor) on privately chosen
+micro-batches — forward output, input gradient and weight-gradient contribution recomputed on a
+LIVE OPTIMIZER MIRROR of the audited stage — and, every step, its applied gradient and weights are
+checked against its commitments (parallel/commitments.py describes the protocol).  Local mode
+here; the distributed message flow is in ``audit_dist.py``.
 
 Reference: Byzantine detection by cosine of DIFFERENT stages' outputs (attack_detector.py:143-162),
-which over-flags every node.
+which over-flags every node; the optimizer step it should guard
+(distributed_trainer.py:197-205, :441-446).
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -19,9 +22,12 @@ from .stage import Stage
 
 
 class AuditMixin:
-    """Recompute audit, local mode + shared helpers (mixed into ``PipelineEngine``)."""
+    """Recompute audit + optimizer mirrors, local mode + shared helpers (mixed into ``PipelineEngine``)."""
 
-    # ================================================================== deterministic stage cross-check
+    audit_sum_tol = 2e-4    # relative error of sketch(G) vs the sum of the M committed sketches (fp32
+    #                         rounding of the ring differences and of the sketch sums: ~1e-6 x M)
+
+    # ================================================================== recompute
     def _recompute(self, st: Stage, x: torch.Tensor, dy: Optional[torch.Tensor] = None,
                    labels: Optional[torch.Tensor] = None, M: int = 1, backward: bool = False):
         """``st``'s forward of one micro-batch as in training (BatchNorm in batch-statistics mode),
@@ -56,6 +62,7 @@ class AuditMixin:
                 for b, v in zip(st.module.buffers(), bufs):
                     b.copy_(v)
 
+    # ================================================================== targeting
     @staticmethod
     @torch.no_grad()
     def _output_stat(y: torch.Tensor):
@@ -68,7 +75,7 @@ class AuditMixin:
     def _target_scores(self, ystats, run) -> Optional[torch.Tensor]:
         """Robust |z| per micro-batch (max over the statistics) of: the output's log RMS, the cosine of
         its token-mean vector with the other micro-batches' (a sign flip or a large perturbation
-        drives it toward -1 / 0) and the norm of its committed weight-gradient sketch contribution."""
+        drives it toward -1 / 0) and the norm of its public weight-gradient sketch contribution."""
         terms = []
         if ystats:
             lr = torch.cat([a for a, _ in ystats])
@@ -115,6 +122,74 @@ class AuditMixin:
         self._target_log.extend((self.global_step, p, m) for p, m in picks.items())
         return picks
 
+    # ================================================================== optimizer mirrors
+    def _audit_mirror(self, rng: Tuple[int, int], sid: int, device=None) -> Stage:
+        """The audited stage's layers on this GPU: the auditor's live optimizer mirror of it (its
+        own fp32 master + AdamW moments, advanced with the verified gradient every step), or in
+        weight-shipping mode a module whose weights every audit overwrites.  One per audited layer
+        range and plan (the stage before the loss stage audits two stages)."""
+        key = (self.plan.version, tuple(rng))
+        cache = self._mirrors
+        if key not in cache:
+            for k in [k for k in cache if k[0] != self.plan.version]:
+                del cache[k]
+            # (its gradient-folding hooks stay: the backward audit recomputes weight gradients on it)
+            cache[key] = Stage(self.model, rng, sid, self.plan.num_stages, device or self.device, self.dtype,
+                               {"output_detection": False, "gradient_verification": False, "serialize_streams": True})
+        return cache[key]
+
+    def _invalidate_mirrors(self):
+        """Every rank, at the same step: the mirrors' state no longer follows their stages (a step
+        they did not see, a checkpoint load); each is re-seeded from its stage before its next use."""
+        self._mirror_epoch += 1
+
+    def _mirror_seeded(self, mir: Stage) -> bool:
+        return getattr(mir, "_seed_epoch", None) == self._mirror_epoch
+
+    @torch.no_grad()
+    def _seed_mirror(self, mir: Stage, master, exp_avg, exp_avg_sq, step: int):
+        """Start a mirror from its stage's optimizer state (once per plan / after a load: the one
+        point where the auditor takes the auditee's word — the state came from a migration or a
+        checkpoint; every update after it is verified)."""
+        f = mir.flat
+        if master is not None:
+            f.master.copy_(master.to(f.device))
+            f.exp_avg.copy_(exp_avg.to(f.device))
+            f.exp_avg_sq.copy_(exp_avg_sq.to(f.device))
+        if f.data is not f.master:
+            f.data.copy_(f.master)
+        f.step_count = int(step)
+        from ..ops.layers import bump_weight_generation
+        bump_weight_generation()
+        mir._seed_epoch = self._mirror_epoch
+        self._audit_cost["seeds"] += 1
+
+    def _skip_decision(self, D: torch.Tensor, evidence: torch.Tensor, node: int) -> torch.Tensor:
+        """[1] 1.0 when ``node``'s update is skipped this step — derived from the all-gathered digest
+        only, so the stage and its auditor's mirror take the same decision: its own gradient flag
+        or non-finite gradient (quarantine), or tampering evidence in its pipeline replica."""
+        z = torch.zeros(1, dtype=torch.float32, device=D.device)
+        q = torch.maximum((D[node, SV.D_GRAD_FLAG] > 0).float(), (D[node, SV.D_NONFINITE] > 0).float()).reshape(1) \
+            if self.cfg.quarantine else z
+        e = evidence[node:node + 1].float() if self.quarantine_on_evidence else z
+        return torch.maximum(q, e)
+
+    @torch.no_grad()
+    def _mirror_update(self, D: torch.Tensor, evidence: torch.Tensor, total_sumsq: torch.Tensor):
+        """Advance every mirror this rank holds with the gradient its stage shipped (verified this
+        step) under the clip scale and skip decision every rank derives from the digest."""
+        for mir, G, node in self._mirror_pending:
+            ctrl = mir.verifier.ctrl
+            mir.verifier.set_clip_scale(total_sumsq.to(mir.device), self.cfg.adamw.max_grad_norm)
+            ctrl[1:2].copy_(self._skip_decision(D, evidence, node).to(mir.device))
+            saved = mir.flat.set_grad_buffer(G)
+            try:
+                mir.flat.adamw_step(self.cfg.adamw, ctrl=ctrl, zero_grad=False)
+            finally:
+                mir.flat.set_grad_buffer(saved)
+        self._mirror_pending = []
+
+    # ================================================================== checks
     def _audit_verdict(self, y_seen: torch.Tensor, y_ref: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(mismatch flag, relative max error) of a received output against its recomputation —
         device tensors, no host sync.  Non-finite values count as a mismatch."""
@@ -123,26 +198,33 @@ class AuditMixin:
         err = torch.nan_to_num(err, nan=1e30, posinf=1e30)
         return (err > self.cfg.audit_tol).float().reshape(1), err.reshape(1)
 
-    def _audit_one(self, st: Stage, x: torch.Tensor, m: int, M: int, y_seen=None, dy=None, labels=None,
-                   dx_seen=None, answer=None, committed=None, key: Optional[int] = None, whash=None):
-        """All checks of one audited micro-batch ``m`` of stage ``st`` (its own modules in local mode,
-        a mirror holding its shipped weights in distributed mode).  Returns device tensors
+    @staticmethod
+    def _seg_rel_err(a: torch.Tensor, ref: torch.Tensor, segs) -> torch.Tensor:
+        """max |a - ref| / max |ref| over the segments (device scalar; non-finite -> 1e30)."""
+        if not segs:
+            return torch.zeros((), device=ref.device)
+        num = torch.stack([(a[lo:hi] - ref[lo:hi]).abs().amax() for lo, hi in segs]).amax()
+        den = torch.stack([ref[lo:hi].abs().amax() for lo, hi in segs]).amax().clamp_min(1e-30)
+        return torch.nan_to_num(num / den, nan=1e30, posinf=1e30)
+
+    def _audit_one(self, mir: Stage, x: torch.Tensor, m: int, M: int, y_seen=None, dy=None, labels=None,
+                   dx_seen=None, c_m: Optional[torch.Tensor] = None, C: Optional[torch.Tensor] = None,
+                   s: Optional[torch.Tensor] = None, key: Optional[int] = None):
+        """Checks of one opened micro-batch ``m``, recomputed on ``mir`` (the live mirror, or the
+        stage's own modules / shipped weights outside mirror mode).  Returns device tensors
         (mismatch flag [1], failed-check bitmask [1], worst relative error [1]).
 
         * forward (AK_FWD): the output the next stage received == f(x; W);
         * input gradient (AK_DX): the gradient sent upstream == the recomputed one for the output
           gradient the audited stage received;
-        * weight gradient (AK_DW): the auditee's ``answer`` (CommitmentMixin._answer_challenge) —
-          the keyed sketch, under the key revealed only now, of micro-batch m's committed
-          contribution — equals the keyed sketch of the recomputed contribution, and the two
-          snapshots it was taken from still hash to the ``committed`` values sent before the reveal;
-        * weights (AK_WHASH, local mode): the weights in use == the stage's post-update commitment."""
-        from ..security.grad_audit import K_KEYED, fold_hash64, keyed_sketch
-        bwd = self.cfg.audit_backward and (st.computes_loss or dy is not None)
-        y_ref, dx_ref, g_ref = self._recompute(st, x, dy, labels, M, backward=bwd)
-        z = torch.zeros(1, dtype=torch.float32, device=st.device)
+        * contribution (AK_DW): the opened c_m hashes to its commitment, its keyed sketch equals
+          the committed s_m bit for bit, and it equals the recomputed contribution."""
+        from ..security.grad_audit import keyed_sketch, merkle_root, roots_differ
+        bwd = self.cfg.audit_backward and (mir.computes_loss or dy is not None)
+        y_ref, dx_ref, g_ref = self._recompute(mir, x, dy, labels, M, backward=bwd)
+        z = torch.zeros(1, dtype=torch.float32, device=mir.device)
         kind, err = z.clone(), z.clone()
-        if y_seen is not None and not st.computes_loss:
+        if y_seen is not None and not mir.computes_loss:
             f, e = self._audit_verdict(y_seen, y_ref)
             kind += f * SV.AK_FWD
             err = torch.maximum(err, e)
@@ -150,46 +232,78 @@ class AuditMixin:
             f, e = self._audit_verdict(dx_seen, dx_ref)
             kind += f * SV.AK_DX
             err = torch.maximum(err, e)
-        if bwd and answer is not None and g_ref is not None and key is not None and committed is not None \
-                and 0 <= m < committed.shape[0] - 1:
-            segs = self._commit_segments(st)
-            ref = keyed_sketch(g_ref, segs, key)
-            # scale: the sketch itself, floored at a quarter of the recomputed contribution's norm
-            # (a random-sign projection of v has magnitude ~ ||v||): a perturbation of >~ tol x the
-            # micro-batch's own gradient fails whatever its direction
-            nrm = torch.stack([g_ref[lo:hi].float().square().sum() for lo, hi in segs]).sum().sqrt() \
-                if segs else torch.zeros((), device=g_ref.device)
-            ans = answer.to(ref.device)
-            scale = torch.maximum(ref.abs().amax(), 0.25 * nrm).clamp_min(1e-30)
-            e = torch.nan_to_num((ans[:K_KEYED] - ref).abs().amax() / scale, nan=1e30, posinf=1e30).reshape(1)
-            hbad = torch.cat([ans[K_KEYED:K_KEYED + 2] != fold_hash64(committed[m]).to(ref.device),
-                              ans[K_KEYED + 2:K_KEYED + 4] != fold_hash64(committed[m + 1]).to(ref.device)]).any()
-            f = torch.maximum((e > self.cfg.audit_grad_tol).float(), hbad.float().reshape(1))
+        if bwd and c_m is not None and g_ref is not None and C is not None and s is not None and 0 <= m < s.shape[0]:
+            segs = self._commit_segments(mir)
+            c = c_m.to(mir.device)
+            hbad = roots_differ(merkle_root(c, segs), C[m])
+            sbad = (keyed_sketch(c, segs, key) != s[m].to(mir.device)).any().float().reshape(1)
+            e = self._seg_rel_err(c, g_ref, segs).reshape(1)
+            f = torch.maximum(torch.maximum(hbad, sbad), (e > self.cfg.audit_grad_tol).float())
             kind += f * SV.AK_DW
             err = torch.maximum(err, e)
-        if whash is not None:
-            kind += whash * SV.AK_WHASH
         return (kind > 0).float(), kind, err
 
-    def _audit(self, rows: Dict[int, torch.Tensor]):
-        """Recompute audit of one privately chosen micro-batch per stage and step.
+    @torch.no_grad()
+    def _verify_applied(self, mir: Stage, C: torch.Tensor, G: torch.Tensor, s: torch.Tensor, key: int):
+        """Every step, on data the auditor holds: (AK_GAPP) the shipped gradient hashes to its
+        commitment and its keyed sketch equals the sum of the M committed contribution sketches;
+        (AK_WHASH) the committed master weights equal this mirror's.  Returns (kind [1], err [1])."""
+        from ..security.grad_audit import keyed_sketch, merkle_root, roots_differ
+        dev = mir.device
+        M = s.shape[0]
+        if C.shape[0] != M + 2:
+            one = torch.ones(1, device=dev)
+            return one * (SV.AK_GAPP + SV.AK_WHASH), one * 1e30
+        segs = self._commit_segments(mir)
+        G = G.to(dev)
+        gbad = roots_differ(merkle_root(G, segs), C[M])
+        sg = keyed_sketch(G, segs, key)
+        ssum = s.to(dev).float().sum(0)
+        nrm = torch.stack([G[lo:hi].float().square().sum() for lo, hi in segs]).sum().sqrt() if segs \
+            else torch.zeros((), device=dev)
+        scale = torch.maximum(sg.abs().amax(), 0.25 * nrm).clamp_min(1e-30)
+        e = torch.nan_to_num((sg - ssum).abs().amax() / scale, nan=1e30, posinf=1e30).reshape(1)
+        abad = torch.maximum(gbad, (e > self.audit_sum_tol).float())
+        wbad = roots_differ(merkle_root(mir.flat.master), C[M + 1])
+        return abad * SV.AK_GAPP + wbad * SV.AK_WHASH, e
 
-        Every non-loss stage is audited by the NEXT stage (it received the output and sent back the
-        output gradient), the loss stage by its predecessor (which received its input gradient).
-        Forward (the output equals f(input; weights)) and, with ``audit_backward``, backward (the
-        input gradient sent upstream and the micro-batch's weight-gradient contribution equal their
-        recomputation) — see ``_audit_one``.  Local mode: the engine holds every stage and computes
-        each verdict right here.  Distributed: see ``_audit_dist``.  A verdict rides in its
-        auditor's digest row (``D_AUDIT_PREV`` / ``D_AUDIT_NEXT``), so no collective is added; a
-        tampered activation or gradient mismatches deterministically, a weight perturbation
-        recomputes consistently but fails the weight commitment, a clean stage always matches."""
+    @staticmethod
+    def _combine(acc, res):
+        if acc is None:
+            return res
+        (f0, k0, e0), (f1, k1, e1) = acc, res
+        return (torch.maximum(f0, f1), torch.bitwise_or(k0.long(), k1.long()).float(), torch.maximum(e0, e1))
+
+    def _write_verdict(self, d: torch.Tensor, res, next_slot: bool):
+        flag, kind, err = res
+        base = (SV.D_AUDIT_NEXT, SV.D_AUDITED_NEXT, SV.D_AUDIT_KIND_NEXT) if next_slot else \
+            (SV.D_AUDIT_PREV, SV.D_AUDITED_PREV, SV.D_AUDIT_KIND_PREV)
+        d[base[0]:base[0] + 1].copy_(flag.to(d.device))
+        d[base[1]:base[1] + 1].fill_(1.0)
+        d[base[2]:base[2] + 1].copy_(kind.to(d.device))
+        d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1],
+                                                                err.to(d.device)))
+
+    # ================================================================== local protocol
+    def _audit(self, rows: Dict[int, torch.Tensor]):
+        """Audit of every stage by its auditor (the next stage; the loss stage by its predecessor).
+
+        Mirror mode (backward audit with commitments): every step, commitments -> private key ->
+        keyed sketches -> private choice of the opened micro-batches -> opened contributions, all
+        through the auditee-side methods of CommitmentMixin (which a lying subclass overrides); the
+        auditor checks the applied gradient and the weights every step and recomputes the opened
+        micro-batches on its mirror.  Forward-only mode: the opened micro-batches are recomputed on
+        the stage's own modules and its weights checked against its post-update checksum.  A verdict
+        rides in its auditor's digest row (``D_AUDIT_PREV`` / ``D_AUDIT_NEXT``), so no collective is
+        added; a tampered activation or gradient mismatches deterministically, a clean stage
+        always matches."""
         if self.distributed:
             self._audit_dist(rows)
             return
-        from ..security.grad_audit import fold_hash
         order = list(self.plan.ranks)
         S = len(order)
         M = len(self._audit_batch)
+        mirror = self._gsk_on
         picks = self._target_picks(order) if self._targeted else {}
         for k in range(S):
             p = order[k]
@@ -197,51 +311,60 @@ class AuditMixin:
             if last and not self.cfg.audit_backward:
                 continue
             aud = order[k + 1] if not last else order[k - 1]
-            recs = self._audit_rec.get(p, {})
-            chosen = [m for m in dict.fromkeys(list(self._audit_ms) + [picks.get(p, -1)])
-                      if m >= 0 and "x" in recs.get(m, {})]
-            if not chosen or aud not in rows:
+            if aud not in rows:
                 continue
             st = self.stages[p]
-            wh = None
-            cur, ref = st._cur_checksum, st.param_checksum
-            if cur is not None and ref is not None and cur is not ref:
-                wh = (fold_hash(cur) != fold_hash(ref)).any().float().reshape(1)
-            flag = kind = err = None
-            # the key is drawn now, after every commitment of the step was taken (private RNG)
-            key = self._mon_rng.getrandbits(64)
-            for m in chosen:
+            recs = self._audit_rec.get(p, {})
+            chosen = [m for m in dict.fromkeys(list(self._audit_ms) + [picks.get(p, -1)])
+                      if m >= 0 and "x" in recs.get(m, {})] if self._audit_now else []
+            res = None
+            C = s = key = None
+            opened: List[torch.Tensor] = []
+            if mirror:
+                dev = self.stages[aud].device
+                mir = self._audit_mirror(st.layer_range, st.stage_id, dev)
+                if not self._mirror_seeded(mir):
+                    self._seed_mirror(mir, *self._optimizer_state(p, st))
+                # the key is drawn only after the commitments exist, the opened set only after the
+                # sketches (private RNG; a lying auditee-side method sees them in that order)
+                C = self._contrib_commitments(p, st).to(dev)
+                G = self._applied_gradient(p, st).to(dev)
+                key = self._mon_rng.getrandbits(63)
+                s = self._contrib_sketches(p, st, key).to(dev)
+                opened = self._open_contributions(p, st, chosen)
+                kd, e = self._verify_applied(mir, C, G, s, key)
+                res = ((kd > 0).float(), kd, e)
+                self._mirror_pending.append((mir, G, p))
+                rows[aud][SV.D_MIRROR:SV.D_MIRROR + 1].fill_(1.0)
+            else:
+                if not chosen:
+                    continue
+                mir = st
+                cur, ref = st._cur_checksum, st.param_checksum
+                if cur is not None and ref is not None and cur is not ref:
+                    wh = (cur != ref).any().float().reshape(1)
+                    res = ((wh > 0).float(), wh * SV.AK_WHASH, torch.zeros(1, device=st.device))
+            for j, m in enumerate(chosen):
                 rec = recs[m]
-                ans = self._answer_challenge(p, st, m, key) if p in self._gcom else None
-                f1, k1, e1 = self._audit_one(st, rec["x"], m, M, y_seen=rec.get("y"),
-                                             dy=None if last else rec.get("dy"), labels=rec.get("labels"),
-                                             dx_seen=rec.get("dx"), answer=ans, committed=self._gcom.get(p),
-                                             key=key, whash=wh)
-                if flag is None:
-                    flag, kind, err = f1, k1, e1
-                else:   # failed-check bits of both audited micro-batches
-                    flag, err = torch.maximum(flag, f1), torch.maximum(err, e1)
-                    kind = torch.bitwise_or(kind.long(), k1.long()).float()
-            d = rows[aud]
-            base = (SV.D_AUDIT_NEXT, SV.D_AUDITED_NEXT, SV.D_AUDIT_KIND_NEXT) if last else \
-                (SV.D_AUDIT_PREV, SV.D_AUDITED_PREV, SV.D_AUDIT_KIND_PREV)
-            d[base[0]:base[0] + 1].copy_(flag.to(d.device))
-            d[base[1]:base[1] + 1].fill_(1.0)
-            d[base[2]:base[2] + 1].copy_(kind.to(d.device))
-            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1],
-                                                                    err.to(d.device)))
+                res = self._combine(res, self._audit_one(
+                    mir, rec["x"].to(mir.device), m, M, y_seen=rec.get("y"), dy=None if last else rec.get("dy"),
+                    labels=rec.get("labels"), dx_seen=rec.get("dx"), c_m=opened[j] if opened else None,
+                    C=C, s=s, key=key))
+            if res is not None:
+                self._write_verdict(rows[aud], res, next_slot=last)
 
+    # ================================================================== weight shipping (no mirror)
     def _audit_early_ship(self, st: Stage):
-        """Distributed audit, weights part, posted BEFORE the 1F1B schedule on the audit
-        communicator so the transfer overlaps the step instead of sitting in its tail (a stage of
-        GPT-2-medium at 8 stages ships 75-180 MB of bf16 weights per step).  The weights sent are
-        those of the step (posted after the attacker's parameter hook, nothing writes them before
-        the optimizer, which runs after the audit waited for the transfer); shipping every step
-        reveals nothing about the private choice, so this runs only when every step is audited
-        (``audit_prob`` = 1).  ``_audit_dist`` waits for it and skips its own weight transfer."""
+        """Distributed audit without optimizer mirrors (data-parallel replicas, or the forward-only
+        audit), weights part: posted BEFORE the 1F1B schedule on the audit communicator so the
+        transfer overlaps the step.  The weights sent are those of the step (posted after the
+        attacker's parameter hook, nothing writes them before the optimizer, which runs after the
+        audit waited for the transfer); shipping every step reveals nothing about the private
+        choice, so this runs only when every step is audited (``audit_prob`` = 1).  In mirror mode
+        nothing is shipped: the auditor holds its own verified copy."""
         self._early_ship = None
         if not (self.distributed and self._audit_now and self.cfg.audit_prob >= 1.0
-                and self._audit_pg is not None):
+                and self._audit_pg is not None) or self._gsk_on:
             return
         s, S = st.stage_id, self.plan.num_stages
         prev, nxt = self.comm.prev, self.comm.next
@@ -265,6 +388,7 @@ class AuditMixin:
         a["bytes"] += sum(t.numel() * t.element_size() for t, _ in sends + recvs)
         self._early_ship = (dist.batch_isend_irecv(ops), mirrors)
 
+    # ================================================================== accounting
     def _note_audit_cost(self, host_s: float, ev):
         a = self._audit_cost
         a["steps"] += 1
@@ -275,18 +399,20 @@ class AuditMixin:
                 del a["events"][:256]
 
     def audit_summary(self) -> Dict[str, float]:
-        """Per-step cost of the recompute audit on this rank (call after a device sync): P2P bytes
-        it sent + received (commitments, weights, inputs, gradients), host wall time of the audit
-        phase, and device time between its first and last kernel (HIP events)."""
+        """Per-step cost of the audit protocol on this rank (call after a device sync): P2P bytes
+        it sent + received (applied gradients, opened contributions, inputs, input gradients; the
+        one-off mirror seeds), host wall time of the audit phase, device time between its first and
+        last kernel (HIP events), device memory it holds (contribution rings + mirrors)."""
         a = self._audit_cost
         tl = self._target_log
         if not a or not a["steps"]:
             return {"steps": 0, "targeted_extra": len(tl)}
         gpu = [e0.elapsed_time(e1) for e0, e1 in a["events"] if e1.query()]
         return {"steps": a["steps"], "bytes_per_step": a["bytes"] / a["steps"],
+                "seed_bytes": a["seed_bytes"], "mirror_seeds": a["seeds"],
                 "host_ms_per_step": 1e3 * a["host_s"] / a["steps"],
                 "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None,
-                "targeted_extra": len(tl)}
+                "memory_bytes": self.audit_memory_bytes(), "targeted_extra": len(tl)}
 
     def _audit_transfer(self, sends, recvs, prev, nxt, act_g, grad_g):
         """Audit traffic: toward the next stage on the activation communicator, toward the
@@ -302,29 +428,23 @@ class AuditMixin:
             self._note_peers(ss, rr, "dir" if g is not None else "default")
             batched_transfer(ss, rr, group=g)
 
-    def _audit_mirror(self, rng: Tuple[int, int], sid: int) -> Stage:
-        """The audited stage's layers on this GPU (weights overwritten by every audit); one mirror
-        per audited layer range (the stage before the loss stage audits two stages)."""
-        key = (self.plan.version, tuple(rng))
-        cache = self._mirrors
-        if key not in cache:
-            for k in [k for k in cache if k[0] != self.plan.version]:
-                del cache[k]
-            # (its gradient-folding hooks stay: the backward audit recomputes weight gradients on it)
-            cache[key] = Stage(self.model, rng, sid, self.plan.num_stages, self.device, self.dtype,
-                               {"output_detection": False, "gradient_verification": False, "serialize_streams": True})
-        return cache[key]
-
     def _audit_vectors(self, D: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Per-node (failed-check bitmask, audited) from the digest, identical on every rank: a
         stage's verdict sits in the row of its auditor (the next stage of its pipeline replica; the
-        loss stage's in its predecessor's ``*_NEXT`` slots), plus the hash cross-checks — the
-        weights its auditor received vs its own post-update commitment, and the input gradient it
-        shipped to its auditor vs what the upstream stage received."""
+        loss stage's in its predecessor's ``*_NEXT`` slots), plus the cross-party hash checks, each
+        comparing what two OTHER ranks hold: the input gradients a stage shipped to its auditor vs
+        those its upstream stage received, its shipped inputs vs the outputs its upstream stage
+        sent, and (weight-shipping mode) the weights its auditor received vs its post-update
+        commitment."""
+        R = 8
         N = D.shape[0]
         kind = torch.zeros(N, dtype=torch.float32, device=D.device)
         done = torch.zeros_like(kind)
         bwd = self.cfg.audit_backward
+
+        def differ(a, b):
+            both = ((a[..., 0] >= 0) & (b[..., 0] >= 0)).float()
+            return both * (a != b).any(-1).float()
         for idx in self._replica_orders():
             n = idx.numel()
             if n < 2:
@@ -334,22 +454,20 @@ class AuditMixin:
                 (D[a, SV.D_AUDIT_KIND_PREV] <= 0).float() * SV.AK_FWD
             done[p] = D[a, SV.D_AUDITED_PREV]
             if self.distributed:
-                wh_c, wh_s = D[p, SV.D_WHASH:SV.D_WHASH + 2], D[a, SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2]
-                both = ((wh_c[:, 0] >= 0) & (wh_s[:, 0] >= 0)).float()
-                kind[p] += both * (wh_c != wh_s).any(1).float() * SV.AK_WHASH
+                kind[p] += differ(D[p, SV.D_WHASH:SV.D_WHASH + R], D[a, SV.D_WHASH_PREV:SV.D_WHASH_PREV + R]) \
+                    * SV.AK_WHASH
                 if n >= 3:
-                    # stage j (1 <= j <= n-2) shipped its dx to idx[j+1]; idx[j-1] received it
-                    q = idx[1:-1]
-                    recv, ship = D[idx[:-2], SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2], \
-                        D[idx[2:], SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2]
-                    both = ((recv[:, 0] >= 0) & (ship[:, 0] >= 0)).float()
-                    kind[q] += both * (recv != ship).any(1).float() * SV.AK_DXHASH
+                    # stage j (1 <= j <= n-2) shipped its x / dx to idx[j+1]; idx[j-1] sent / received them
+                    q, up, au = idx[1:-1], idx[:-2], idx[2:]
+                    bad = torch.maximum(
+                        differ(D[up, SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + R], D[au, SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + R]),
+                        differ(D[up, SV.D_XHASH_SENT:SV.D_XHASH_SENT + R], D[au, SV.D_XHASH_SHIP:SV.D_XHASH_SHIP + R]))
+                    kind[q] += bad * SV.AK_DXHASH
             if bwd:
                 L, A = idx[-1], idx[-2]
                 kind[L] = D[A, SV.D_AUDIT_KIND_NEXT]
                 done[L] = D[A, SV.D_AUDITED_NEXT]
                 if self.distributed:
-                    wh_c, wh_s = D[L, SV.D_WHASH:SV.D_WHASH + 2], D[A, SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2]
-                    both = float(1.0) * ((wh_c[0] >= 0) & (wh_s[0] >= 0)).float()
-                    kind[L] += both * (wh_c != wh_s).any().float() * SV.AK_WHASH
+                    kind[L] += differ(D[L, SV.D_WHASH:SV.D_WHASH + R], D[A, SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + R]) \
+                        * SV.AK_WHASH
         return kind, done

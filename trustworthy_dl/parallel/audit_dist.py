@@ -1,10 +1,20 @@
-"""Distributed recompute-audit protocol of ``PipelineEngine`` (one process per stage): commit,
-private reveal through the c10d store, ship, verify on a mirror of the audited stage.
+"""Distributed audit protocol of ``PipelineEngine`` (one process per stage): commit, private key,
+sketches, private opening through the c10d store; applied gradient, opened contributions, inputs
+and input gradients over P2P; verification on the auditor's live optimizer mirror.
+
+Ordering is what makes it binding, so the small messages go host to host through the store: an
+auditor reveals its key only after ``store.get`` returned the commitments, and its opened set only
+after it returned the sketches — nothing the auditee sends after a reveal can change what it had
+committed before it (a P2P send is only enqueued when the host posts it; the auditor could not tell
+when it landed without a device sync).  Store payloads are JSON (an auditee's bytes are never
+unpickled).  Every rank runs the phases in the same order — all auditee "commit" posts, then all
+auditor "key" posts, ... — so no store read waits on a phase that waits on it.
 """
 from __future__ import annotations
 
+import json
 import os
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -13,244 +23,301 @@ from ..runtime.commcheck import note_host_sync
 from ..security import stage_verifier as SV
 
 
+def _enc_json(obj) -> str:
+    return json.dumps(obj, separators=(",", ":"))
+
+
 class DistAuditMixin:
     """Distributed audit protocol (mixed into ``PipelineEngine``)."""
 
-    def _audit_dist(self, rows: Dict[int, torch.Tensor]):
-        """Distributed audit protocol of one rank (stage s of S):
+    def _tensor_root(self, t: torch.Tensor) -> torch.Tensor:
+        """Merkle root of a tensor's bytes (16-bit tensors hashed as pairs of elements)."""
+        from ..security.grad_audit import merkle_root
+        t = t.detach().contiguous().reshape(-1)
+        if t.element_size() == 4:
+            return merkle_root(t)
+        if t.element_size() == 2 and t.numel() % 2 == 0:
+            return merkle_root(t.view(torch.int32))
+        return merkle_root(t.float())
 
-        1. commit: every audited stage sends the exact hashes of its running gradient after every
-           micro-batch (one [M+1] int64 tensor; CommitmentMixin) to its auditor BEFORE any choice is
-           revealed;
-        2. reveal: each auditor draws privately whether to audit, which ``audit_micro_k``
-           micro-batches and a 63-bit sketch key, and posts them in the c10d store (host to host, no
-           device sync); the auditee reads them only now, after every output and gradient of the
-           step reached its peers and its commitments went out;
-        3. ship: the auditee sends its bf16 weights, (non-first, non-loss stages) its input and the
-           input gradient it sent upstream for those micro-batches, and its answers: the keyed
-           sketch of each audited micro-batch's committed contribution plus the re-computed hashes of
-           the snapshots it came from (``_answer_challenge``); the loss stage ships only its weights
-           and answers (its auditor holds its input, the labels and the gradient it sent);
-        4. verify on a mirror of the audited stage (``_audit_one``); the hash of the weights
-           received (vs the auditee's post-update commitment ``D_WHASH``) and of the input gradient
-           shipped (vs what the upstream stage received, ``D_DXHASH_RECV``) go into the auditor's
-           row and are compared on every rank in ``_attribute`` — so a rank that lies about its own
-           integrity check, or ships a different gradient than it sent, is still caught."""
-        from ..security.grad_audit import hash2
+    def _list_row(self, ts: List[torch.Tensor]) -> torch.Tensor:
+        """hash_row of the root over the roots of a list of tensors (digest cross-checks)."""
+        from ..security.grad_audit import hash_row, merkle_root
+        roots = torch.stack([self._tensor_root(t) for t in ts])
+        return hash_row(merkle_root(roots.reshape(-1)))
+
+    def _audit_dist(self, rows: Dict[int, torch.Tensor]):
+        """One rank's part of the step's audit (stage s of S; auditee of its auditor, auditor of its
+        previous stage and — as the stage before the loss stage — of the loss stage).
+
+        Mirror mode (backward audit, commitments on):
+          1. commit   (auditee) store: Merkle roots of the M contributions, the applied gradient and
+                      the master weights (+ public running sketches for the targeted audit); P2P on
+                      the audit communicator: the applied gradient (and, when its auditor's mirror
+                      is not seeded for this plan, the optimizer state);
+          2. key      (auditor) after reading the commitments: a private 63-bit sketch key;
+          3. sketches (auditee) the M keyed contribution sketches;
+          4. open     (auditor) after reading the sketches: whether to audit (``audit_prob``) and
+                      which ``audit_micro_k`` micro-batches (+ the targeted one, opt-in);
+          5. ship     (auditee, P2P) the opened contributions; for non-first, non-loss stages also
+                      the inputs and the input gradients it sent upstream for them;
+          6. verify   (auditor, on its mirror) ``_verify_applied`` every step, ``_audit_one`` per
+                      opened micro-batch; its upstream neighbour and it put the roots of the
+                      inputs / input gradients sent, received and shipped into the digest, compared
+                      on every rank (``_audit_vectors``).
+        Weight-shipping mode (data-parallel replicas, forward-only audit): 4-6 with the stage's
+        bf16 weights shipped (``_audit_early_ship``) instead of a mirror."""
         st = self.my_stage()
         if st is None:
             return
+        me = self.rank
         s, S = st.stage_id, self.plan.num_stages
         prev, nxt = self.comm.prev, self.comm.next
         bwd = self.cfg.audit_backward
         act_g, grad_g = (self._dir_groups if self.p2p_mode == "async" else (None, None))
         M = len(self._audit_batch)
-        d = rows[self.rank]
+        d = rows[me]
+        mirror = bool(self._gsk_on)
         if self._audit_rng is None:
             seed = self.cfg.monitor_seed
             self._audit_rng = __import__("random").Random(
-                int.from_bytes(os.urandom(8), "little") if seed is None else seed * 7919 + self.rank)
+                int.from_bytes(os.urandom(8), "little") if seed is None else seed * 7919 + me)
         store = dist.distributed_c10d._get_default_store()
         tag = f"tdl_audit/{self.plan.version}/{self.global_step}"
         # my auditees: prev (I am its next stage), and nxt when it is the loss stage
-        audit_prev = prev is not None
-        audit_next = bwd and nxt is not None and s + 1 == S - 1
+        peers = []
+        if prev is not None:
+            peers.append((prev, s - 1, False))
+        if bwd and nxt is not None and s + 1 == S - 1:
+            peers.append((nxt, s + 1, True))
         # my auditor: nxt, or prev when I am the loss stage
         my_auditor = nxt if nxt is not None else (prev if bwd and s == S - 1 and prev is not None else None)
-        # ---- 1. commitments: exact running-gradient hashes (and, for targeting, the public running
-        # sketches) to my auditor before any reveal
-        runs_in: Dict[int, torch.Tensor] = {}
-        coms_in: Dict[int, torch.Tensor] = {}
-        keyed = bool(bwd and self._gsk_on)
-        if keyed:
-            c_send, c_recv = [], []
-            if my_auditor is not None:
-                c_send.append((self._gcom[self.rank], my_auditor))
-                if self._targeted:
-                    c_send.append((self._gsk_run[self.rank], my_auditor))
-            for peer, on in ((prev, audit_prev), (nxt, audit_next)):
-                if on:
-                    coms_in[peer] = torch.empty(M + 1, dtype=torch.int64, device=self.device)
-                    c_recv.append((coms_in[peer], peer))
-                    if self._targeted:
-                        runs_in[peer] = torch.empty(M + 1, 2, dtype=torch.float32, device=self.device)
-                        c_recv.append((runs_in[peer], peer))
-            self._audit_transfer(c_send, c_recv, prev, nxt, act_g, grad_g)
-        # the auditees' last commitments as received here: compared on every rank with what each
-        # auditee reports for itself (``_gsk_mismatch``)
-        from ..security.grad_audit import fold_hash64
-        for peer, slot in ((prev, SV.D_GCOM_RECV_PREV), (nxt, SV.D_GCOM_RECV_NEXT)):
-            com = coms_in.get(peer) if peer is not None else None
-            if com is not None:   # + 1: a zeroed slot (no audit this step) reads as "none"
-                d[slot:slot + 2].copy_(fold_hash64(com[-1]) + 1.0)
-            else:
-                d[slot:slot + 2].fill_(0.0)
+        mirs = {p: self._audit_mirror(tuple(self.plan.ranges[sid]), sid) for p, sid, _ in peers}
+        a_cost = self._audit_cost
 
-        # ---- 2. reveal: private choices (whether + which micro-batches).  The uniform draw, plus
-        # with ``audit_targeted`` the micro-batch whose received output / committed sketch norm stands
-        # out (one host read of the scores: the choice needs them)
-        tgt_prev = tgt_next = -1
-        if self._targeted:
-            zs = []
-            if audit_prev:
-                ys = [self._output_stat(self._audit_inputs[m]) for m in range(M)] if s - 1 >= 0 else None
-                zs.append(self._target_scores(ys, runs_in.get(prev)))
-            if audit_next:
-                zs.append(self._target_scores(None, runs_in.get(nxt)))
-            got = [torch.stack([z.max(), z.argmax().float()]) if z is not None else
-                   torch.tensor([-1.0, -1.0], device=self.device) for z in zs]
+        # ---- 1. commit (auditee): roots through the store, the applied gradient over P2P
+        p2p_ops = []
+        if mirror and my_auditor is not None:
+            C = self._contrib_commitments(me, st)
+            G = self._applied_gradient(me, st)
+            run = self._gsk_run.get(me) if self._targeted else None
+            mark = (self.plan.version, tuple(st.layer_range), self._mirror_epoch)
+            seed_state = self._seed_mark != mark
             note_host_sync()
-            vals = torch.stack(got).tolist() if got else []
-            thr = self.cfg.audit_target_z
-            picks = [int(i) if zm > thr else -1 for zm, i in vals]
-            if audit_prev:
-                tgt_prev = picks.pop(0)
-            if audit_next:
-                tgt_next = picks.pop(0)
-            self._target_log.extend((self.global_step, n, m) for n, m in ((prev, tgt_prev), (nxt, tgt_next)) if m >= 0)
+            payload = {"C": C.cpu().tolist(), "step_count": st.flat.step_count,
+                       "run": run.cpu().tolist() if run is not None else None}
+            store.set(f"{tag}/com/{me}", _enc_json(payload))
+            p2p_ops.append(("send", G.contiguous(), my_auditor))
+            if seed_state:
+                master, m1, m2, _ = self._optimizer_state(me, st)
+                p2p_ops += [("send", t.contiguous(), my_auditor) for t in (master, m1, m2)]
+                self._seed_mark = mark
+        seeding: Dict[int, bool] = {}
+        if mirror:
+            for p, _, _ in peers:
+                mir = mirs[p]
+                g_in = getattr(mir, "_g_in", None)
+                if g_in is None or g_in.numel() != mir.flat.numel:
+                    g_in = mir._g_in = torch.empty(mir.flat.numel, dtype=torch.float32, device=self.device)
+                p2p_ops.append(("recv", g_in, p))
+                seeding[p] = not self._mirror_seeded(mir)
+                if seeding[p]:
+                    p2p_ops += [("recv", t, p) for t in (mir.flat.master, mir.flat.exp_avg, mir.flat.exp_avg_sq)]
+        work = None
+        if p2p_ops:
+            g = self._audit_pg
+            ops = [dist.P2POp(dist.isend if k == "send" else dist.irecv, t, r, g) for k, t, r in p2p_ops]
+            nb = sum(t.numel() * t.element_size() for _, t, _ in p2p_ops)
+            a_cost["bytes"] += nb
+            self._note_peers([(t, r) for k, t, r in p2p_ops if k == "send"],
+                             [(t, r) for k, t, r in p2p_ops if k == "recv"], "audit")
+            work = dist.batch_isend_irecv(ops)
+
+        # ---- 2. key (auditor): only after the commitments were read
+        got: Dict[int, dict] = {}
+        keys: Dict[int, int] = {}
+        if mirror:
+            for p, _, _ in peers:
+                k = f"{tag}/com/{p}"
+                got[p] = json.loads(store.get(k).decode())
+                store.delete_key(k)
+                keys[p] = self._audit_rng.getrandbits(63)
+                store.set(f"{tag}/key/{p}", str(keys[p]))
+
+        # ---- 3. sketches (auditee)
+        if mirror and my_auditor is not None:
+            k = f"{tag}/key/{me}"
+            key_req = int(store.get(k).decode())
+            store.delete_key(k)
+            note_host_sync()
+            sk = self._contrib_sketches(me, st, key_req).cpu().tolist()
+            store.set(f"{tag}/sk/{me}", _enc_json(sk))
+
+        # ---- 4. open (auditor): only after the sketches were read
+        sketches: Dict[int, Optional[torch.Tensor]] = {}
+        if mirror:
+            for p, _, _ in peers:
+                k = f"{tag}/sk/{p}"
+                sketches[p] = self._as_tensor(json.loads(store.get(k).decode()), torch.float32)
+                store.delete_key(k)
+        tgt: Dict[int, int] = {}
+        if self._targeted and peers:
+            zs = []
+            for p, sid, nxt_peer in peers:
+                ys = [self._output_stat(self._audit_inputs[m]) for m in range(M)] if (not nxt_peer and sid >= 0) else None
+                run = got.get(p, {}).get("run") if mirror else None
+                run = self._as_tensor(run, torch.float32) if run is not None else None
+                zs.append(self._target_scores(ys, run))
+            vals = [torch.stack([z.max(), z.argmax().float()]) if z is not None else
+                    torch.tensor([-1.0, -1.0], device=self.device) for z in zs]
+            note_host_sync()
+            vals = torch.stack(vals).tolist()
+            for (p, _, _), (zm, i) in zip(peers, vals):
+                tgt[p] = int(i) if zm > self.cfg.audit_target_z else -1
+            self._target_log.extend((self.global_step, p, m) for p, m in tgt.items() if m >= 0)
 
         def choose(extra):
             if self.cfg.audit_prob < 1.0 and self._audit_rng.random() >= self.cfg.audit_prob:
                 return [extra] if extra >= 0 else []
-            k = max(1, min(int(self.cfg.audit_micro_k), M))
-            return list(dict.fromkeys(self._audit_rng.sample(range(M), k) + ([extra] if extra >= 0 else [])))
-        ms_prev = choose(tgt_prev) if audit_prev else []
-        ms_next = choose(tgt_next) if audit_next else []
-        key_prev, key_next = self._audit_rng.getrandbits(63), self._audit_rng.getrandbits(63)
+            kk = max(1, min(int(self.cfg.audit_micro_k), M))
+            return list(dict.fromkeys(self._audit_rng.sample(range(M), kk) + ([extra] if extra >= 0 else [])))
 
-        def enc(ms, key=None):
-            v = ",".join(str(m) for m in ms) if ms else "-1"
-            return v if key is None else f"{v};{key}"
+        def enc(ms):
+            return ",".join(str(m) for m in ms) if ms else "-1"
 
         def dec(v):
-            return [int(t) for t in v.decode().split(";")[0].split(",") if int(t) >= 0]
-        if audit_prev:
-            store.set(f"{tag}/req/{prev}", enc(ms_prev, key_prev))
-            if s - 1 > 0 and bwd:
-                store.set(f"{tag}/reqh/{prev}", enc(ms_prev))   # for the stage before prev: dx hash
-        if audit_next:
-            store.set(f"{tag}/req/{nxt}", enc(ms_next, key_next))
+            return [int(t) for t in v.decode().split(",") if int(t) >= 0]
+        opened: Dict[int, List[int]] = {}
+        for p, sid, nxt_peer in peers:
+            opened[p] = choose(tgt.get(p, -1)) if self._audit_now else []
+            store.set(f"{tag}/req/{p}", enc(opened[p]))
+            if not nxt_peer and sid > 0 and bwd:
+                store.set(f"{tag}/reqh/{p}", enc(opened[p]))   # for p's upstream stage: x / dx roots
         ms_req: List[int] = []
-        key_req = 0
         if my_auditor is not None:
-            k = f"{tag}/req/{self.rank}"
-            v = store.get(k)
-            ms_req = dec(v)
-            key_req = int(v.decode().split(";")[1])
+            k = f"{tag}/req/{me}"
+            ms_req = dec(store.get(k))
             store.delete_key(k)
-
-        def hsum(ts):
-            """Combined hash of several tensors (sum of the 16-bit halves mod 2^16, exact in fp32)."""
-            h = hash2(ts[0])
-            for t in ts[1:]:
-                h = torch.remainder(h + hash2(t), 65536.0)
-            return h
-        # as the upstream recipient of nxt's input gradient: hash what I received for nxt's audited micro-batches
+        # as the upstream neighbour of nxt (when nxt is not the loss stage): roots of the outputs I
+        # sent it and of the input gradients I received from it, for the micro-batches its auditor opened
+        for slot in (SV.D_DXHASH_RECV, SV.D_XHASH_SENT):
+            d[slot:slot + 8].fill_(-1.0)
         if bwd and nxt is not None and s + 1 < S - 1:
             k = f"{tag}/reqh/{nxt}"
             mh = dec(store.get(k))
             store.delete_key(k)
             if mh and all(m in self._audit_recv_dy for m in mh):
-                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].copy_(hsum([self._audit_recv_dy[m] for m in mh]))
-            else:
-                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
-        else:
-            d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 2].fill_(-1.0)
+                d[SV.D_DXHASH_RECV:SV.D_DXHASH_RECV + 8].copy_(self._list_row([self._audit_recv_dy[m] for m in mh]))
+            if mh and all(m in self._audit_outputs for m in mh):
+                d[SV.D_XHASH_SENT:SV.D_XHASH_SENT + 8].copy_(self._list_row([self._audit_outputs[m] for m in mh]))
+
+        # ---- 5. ship (auditee) / receive (auditor)
         x_send, dx_send = [], []
-        if ms_req and s > 0 and s < S - 1:
+        if ms_req and 0 < s < S - 1:
             x_send = [self._audit_inputs[m].contiguous() for m in ms_req]
             if bwd and all(m in self._audit_sent_dx for m in ms_req):
                 dx_send = [self._audit_sent_dx[m].contiguous() for m in ms_req]
-            store.set(f"{tag}/shape/{self.rank}", ",".join(str(v) for v in x_send[0].shape))
-        # ---- 3. ship (the weights went out before the schedule when ``_audit_early_ship`` ran)
+            store.set(f"{tag}/shape/{me}", ",".join(str(v) for v in x_send[0].shape))
         early = self._early_ship
         self._early_ship = None
         sends, recvs = [], []
         if ms_req:
-            if early is None:
+            if not mirror and early is None:
                 sends.append((st.flat.data, my_auditor))
             sends += [(t, my_auditor) for t in x_send]
             sends += [(t, my_auditor) for t in dx_send]
-            if keyed:   # answers to the revealed key, after every commitment went out
-                sends.append((torch.stack([self._answer_challenge(self.rank, st, m, key_req) for m in ms_req]),
-                              my_auditor))
-        mir_p = mir_n = None
-        x_prev, dx_prev = [], []
-        if audit_prev and ms_prev:
-            mir_p = self._audit_mirror(tuple(self.plan.ranges[s - 1]), s - 1)
-            if early is None:
-                recvs.append((mir_p.flat.data, prev))
-            if s - 1 > 0:
-                k = f"{tag}/shape/{prev}"
+            if mirror:
+                sends += [(t.contiguous(), my_auditor) for t in self._open_contributions(me, st, ms_req)]
+        inbound: Dict[int, dict] = {}
+        for p, sid, nxt_peer in peers:
+            ms = opened[p]
+            ib = inbound[p] = {"x": [], "dx": [], "c": []}
+            if not ms:
+                continue
+            mir = mirs[p]
+            if not mirror and early is None:
+                recvs.append((mir.flat.data, p))
+            if not nxt_peer and sid > 0:
+                k = f"{tag}/shape/{p}"
                 shape = torch.Size([int(v) for v in store.get(k).decode().split(",")])
                 store.delete_key(k)
-                x_prev = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms_prev]
-                recvs += [(t, prev) for t in x_prev]
+                ib["x"] = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms]
+                recvs += [(t, p) for t in ib["x"]]
                 if bwd:
-                    dx_prev = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms_prev]
-                    recvs += [(t, prev) for t in dx_prev]
-        from ..security.grad_audit import K_KEYED
-        ans_prev = ans_next = None
-        if audit_prev and ms_prev and keyed:
-            ans_prev = torch.empty(len(ms_prev), K_KEYED + 4, dtype=torch.float32, device=self.device)
-            recvs.append((ans_prev, prev))
-        if audit_next and ms_next:
-            mir_n = self._audit_mirror(tuple(self.plan.ranges[s + 1]), s + 1)
-            if early is None:
-                recvs.append((mir_n.flat.data, nxt))
-            if keyed:
-                ans_next = torch.empty(len(ms_next), K_KEYED + 4, dtype=torch.float32, device=self.device)
-                recvs.append((ans_next, nxt))
+                    ib["dx"] = [torch.empty(shape, dtype=self.dtype, device=self.device) for _ in ms]
+                    recvs += [(t, p) for t in ib["dx"]]
+            if mirror:
+                ib["c"] = [torch.empty(mir.flat.numel, dtype=torch.float32, device=self.device) for _ in ms]
+                recvs += [(t, p) for t in ib["c"]]
         self._audit_transfer(sends, recvs, prev, nxt, act_g, grad_g)
+        if work is not None:
+            for w in work:
+                w.wait()
         if early is not None:
             for w in early[0]:
                 w.wait()
 
-        def combine(acc, res):
-            if acc is None:
-                return res
-            (f0, k0, e0), (f1, k1, e1) = acc, res
-            return (torch.maximum(f0, f1), torch.bitwise_or(k0.long(), k1.long()).float(), torch.maximum(e0, e1))
-        # ---- 4. verify
-        if mir_p is not None:
+        # ---- 6. verify (auditor)
+        d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 8].fill_(-1.0)
+        d[SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 8].fill_(-1.0)
+        d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 8].fill_(-1.0)
+        d[SV.D_XHASH_SHIP:SV.D_XHASH_SHIP + 8].fill_(-1.0)
+        from ..security.grad_audit import hash_row, merkle_root
+        for p, sid, nxt_peer in peers:
+            mir = mirs[p]
+            ms, ib = opened[p], inbound[p]
             res = None
-            for j, m in enumerate(ms_prev):
-                xp = x_prev[j] if x_prev else self._stage_input(self._audit_batch[m], mir_p)
-                dy = self._audit_sent_dx.get(m) if bwd else None
-                res = combine(res, self._audit_one(mir_p, xp, m, M, y_seen=self._audit_inputs[m], dy=dy,
-                                                   dx_seen=dx_prev[j] if dx_prev else None,
-                                                   answer=None if ans_prev is None else ans_prev[j],
-                                                   committed=coms_in.get(prev), key=key_prev))
-            flag, kind, err = res
-            d[SV.D_AUDIT_PREV:SV.D_AUDIT_PREV + 1].copy_(flag)
-            d[SV.D_AUDITED_PREV:SV.D_AUDITED_PREV + 1].fill_(1.0)
-            d[SV.D_AUDIT_KIND_PREV:SV.D_AUDIT_KIND_PREV + 1].copy_(kind)
-            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(err)
-            d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].copy_(hash2(mir_p.flat.data))
-            if dx_prev:
-                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].copy_(hsum(dx_prev))
-            else:
-                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
-        else:
-            d[SV.D_WHASH_PREV:SV.D_WHASH_PREV + 2].fill_(-1.0)
-            d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 2].fill_(-1.0)
-        if mir_n is not None:
-            res = None
-            for j, m in enumerate(ms_next):
-                labels = self._audit_targets[m].to(self.device, non_blocking=True)
-                res = combine(res, self._audit_one(mir_n, self._audit_outputs.get(m), m, M, labels=labels,
-                                                   dx_seen=self._audit_recv_dy.get(m),
-                                                   answer=None if ans_next is None else ans_next[j],
-                                                   committed=coms_in.get(nxt), key=key_next))
-            flag, kind, err = res
-            d[SV.D_AUDIT_NEXT:SV.D_AUDIT_NEXT + 1].copy_(flag)
-            d[SV.D_AUDITED_NEXT:SV.D_AUDITED_NEXT + 1].fill_(1.0)
-            d[SV.D_AUDIT_KIND_NEXT:SV.D_AUDIT_KIND_NEXT + 1].copy_(kind)
-            d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1].copy_(torch.maximum(d[SV.D_AUDIT_ERR:SV.D_AUDIT_ERR + 1], err))
-            d[SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2].copy_(hash2(mir_n.flat.data))
-        else:
-            d[SV.D_WHASH_NEXT:SV.D_WHASH_NEXT + 2].fill_(-1.0)
+            C = s_p = key = None
+            if mirror:
+                if seeding[p]:
+                    a_cost["seed_bytes"] += 3 * mir.flat.numel * 4
+                    self._seed_mirror(mir, None, None, None, int(got[p].get("step_count", 0)))
+                C = self._as_tensor(got[p]["C"], torch.int32)
+                s_p, key = sketches[p], keys[p]
+                if C is None or s_p is None or s_p.dim() != 2 or s_p.shape[0] != M:
+                    one = torch.ones(1, device=self.device)
+                    res = (one, one * (SV.AK_GAPP + SV.AK_WHASH), one * 1e30)
+                    C = s_p = None
+                else:
+                    kd, e = self._verify_applied(mir, C, mir._g_in, s_p, key)
+                    res = ((kd > 0).float(), kd, e)
+                self._mirror_pending.append((mir, mir._g_in, p))
+                d[SV.D_MIRROR:SV.D_MIRROR + 1].fill_(1.0)
+            for j, m in enumerate(ms):
+                if nxt_peer:
+                    labels = self._audit_targets[m].to(self.device, non_blocking=True)
+                    r1 = self._audit_one(mir, self._audit_outputs.get(m), m, M, labels=labels,
+                                         dx_seen=self._audit_recv_dy.get(m), c_m=ib["c"][j] if ib["c"] else None,
+                                         C=C, s=s_p, key=key)
+                else:
+                    xp = ib["x"][j] if ib["x"] else self._stage_input(self._audit_batch[m], mir)
+                    dy = self._audit_sent_dx.get(m) if bwd else None
+                    r1 = self._audit_one(mir, xp, m, M, y_seen=self._audit_inputs[m], dy=dy,
+                                         dx_seen=ib["dx"][j] if ib["dx"] else None,
+                                         c_m=ib["c"][j] if ib["c"] else None, C=C, s=s_p, key=key)
+                res = self._combine(res, r1)
+            if res is not None:
+                self._write_verdict(d, res, next_slot=nxt_peer)
+            if not mirror and ms:
+                slot = SV.D_WHASH_NEXT if nxt_peer else SV.D_WHASH_PREV
+                d[slot:slot + 8].copy_(hash_row(merkle_root(mir.flat.data.view(torch.int32)
+                                                            if mir.flat.data.element_size() == 2 and mir.flat.numel % 2 == 0
+                                                            else mir.flat.data.float())))
+            if not nxt_peer and ib["x"]:
+                d[SV.D_XHASH_SHIP:SV.D_XHASH_SHIP + 8].copy_(self._list_row(ib["x"]))
+            if not nxt_peer and ib["dx"]:
+                d[SV.D_DXHASH_SHIP:SV.D_DXHASH_SHIP + 8].copy_(self._list_row(ib["dx"]))
         self._audit_inputs = {}
         self._audit_sent_dx = {}
         self._audit_recv_dy = {}
         self._audit_outputs = {}
+
+    def _as_tensor(self, v, dtype) -> Optional[torch.Tensor]:
+        """A JSON payload from a peer as a device tensor (None if it is not a rectangular number list)."""
+        try:
+            t = torch.tensor(v, dtype=torch.int64 if dtype == torch.int32 else dtype)
+        except (TypeError, ValueError, RuntimeError):
+            return None
+        if dtype == torch.int32:
+            t = ((t & 0xFFFFFFFF) - ((t & 0x80000000) << 1)).to(torch.int32)
+        return t.to(self.device)

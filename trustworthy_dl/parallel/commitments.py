@@ -1,21 +1,33 @@
-"""Per-micro-batch gradient commitments of ``PipelineEngine`` (security/grad_audit.py).
+"""Auditee side of the gradient protocol of ``PipelineEngine`` (security/grad_audit.py; the
+auditor side is parallel/audit.py and audit_dist.py).
 
-Commit-then-reveal: after every micro-batch's backward each stage commits the
-EXACT hash of its running flat gradient (the tied weight's elements excluded: the tied all-reduce
-adds to them) and keeps a snapshot of it; at the step tail it commits the hash of the gradient it is
-about to apply.  Only then does its auditor reveal a private per-step key (and which micro-batches
-it audits): the stage answers with the keyed full-coverage sketch of the audited micro-batch's
-committed contribution (snapshot i+1 - snapshot i, re-hashed against the commitment first), which
-the auditor compares with the sketch of its own recomputation (parallel/audit.py).  Every rank
-checks applied-hash == last committed hash exactly (``_gsk_mismatch``).
+Per step, every audited stage A (its auditor V: the next stage, or the previous one for the loss
+stage):
 
-r4 committed sketches under public sign patterns over a public 1/16 sample of the gradient: a
-perturbation in the unsampled coordinates or in the null space of the two public sign vectors
-passed both checks (attacks/adversarial_attacks.py ``adaptive``, tests/test_keyed_audit.py).  The
-public sketch is kept only to rank micro-batches for the targeted audit.
+1. during the backward, after micro-batch i's weight gradients: c_i = g - prev, prev = g into a
+   ring of M contributions (the tied weight's elements excluded from everything below: the tied
+   all-reduce adds to them; they have their own cross-stage check, ``_tied_mismatch``);
+2. **commit**: A sends V the BLAKE2s Merkle roots of c_0..c_{M-1}, of the gradient G it applies and
+   of its fp32 master weights (``_contrib_commitments``), and ships G itself;
+3. **key**: only after V RECEIVED the commitments does it reveal a private sketch key; A answers
+   with the keyed sketches s_i of all M contributions (``_contrib_sketches``);
+4. **open**: only after V received the sketches does it reveal which k micro-batches it audits; A
+   ships those c_m (``_open_contributions``);
+5. V checks with data it hashes itself: root(c_m) == commitment, sketch(c_m) == s_m (bit exact),
+   c_m == V's recomputation of micro-batch m; root(G) == commitment, sketch(G) == sum_i s_i; the
+   committed master == V's LIVE OPTIMIZER MIRROR of A (fp32 master + AdamW moments, advanced every
+   step with the verified G under the clip scale / quarantine decision every rank derives from the
+   all-gathered digest).  So A cannot apply anything but sum_i c_i (a lie in any s_i or c_i is
+   opened with probability >= k/M per step), cannot apply something else than the G it shipped
+   (the mirror diverges: caught at the next step's weight check), and cannot rewrite its weights
+   outside the optimizer.
+
+Every auditee-side answer is a method a lying rank can override (tests/test_lying_rank.py runs
+such subclasses as gloo ranks); no check trusts a value the audited rank reports about itself.
 
 Reference: the gradient check is a host z-score (attack_detector.py:109-141) that cannot see a
-sign flip; the phantom ``GradientVerifier`` (distributed_trainer.py:199-205).
+sign flip; the phantom ``GradientVerifier`` (distributed_trainer.py:199-205); the optimizer step
+that should only apply verified gradients (distributed_trainer.py:197-205, :441-446).
 """
 from __future__ import annotations
 
@@ -28,7 +40,7 @@ from .stage import Stage
 
 
 class CommitmentMixin:
-    """Gradient commitments (mixed into ``PipelineEngine``)."""
+    """Gradient commitments, auditee side (mixed into ``PipelineEngine``)."""
 
     # ------------------------------------------------------------------ layout helpers
     def _tied_ids(self, st: Stage) -> List[int]:
@@ -63,18 +75,28 @@ class CommitmentMixin:
             segs = self._gsk_cache[key] = _segments(st.flat.numel, tied_ranges(st.flat, self._tied_ids(st)))
         return segs
 
-    def _hash_seed(self, st: Stage) -> int:
-        a, b = st.layer_range
-        return (self.cfg.seed * 1_000_003 + self.global_step * 7919 + a * 31 + b) & 0xFFFFFFFF
-
-    def _snap_buffer(self, node: int, st: Stage, M: int) -> torch.Tensor:
-        """[M + 1, numel] fp32 snapshot ring of the stage's running gradient (reused across steps)."""
+    def _ring_buffers(self, node: int, st: Stage, M: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        """([M, numel] contribution ring, [numel] previous running gradient), fp32, reused across
+        steps: (M + 1) x the stage's gradient memory (``audit_memory_bytes``)."""
         key = (node, M, st.flat.numel, str(st.device))
-        buf = self._gsnap_cache.get(key)
+        buf = self._gring_cache.get(key)
         if buf is None:
-            self._gsnap_cache = {k: v for k, v in self._gsnap_cache.items() if k[0] != node}
-            buf = self._gsnap_cache[key] = torch.empty(M + 1, st.flat.numel, dtype=torch.float32, device=st.device)
+            self._gring_cache = {k: v for k, v in self._gring_cache.items() if k[0] != node}
+            buf = self._gring_cache[key] = (torch.empty(M, st.flat.numel, dtype=torch.float32, device=st.device),
+                                            torch.empty(st.flat.numel, dtype=torch.float32, device=st.device))
         return buf
+
+    def audit_memory_bytes(self) -> int:
+        """Device bytes the protocol holds on this rank: contribution rings + optimizer mirrors."""
+        n = sum(r.numel() * 4 + p.numel() * 4 for r, p in self._gring_cache.values())
+        for mir in self._mirrors.values():
+            f = mir.flat
+            n += sum(t.numel() * t.element_size() for t in {id(t): t for t in (f.master, f.data, f.exp_avg,
+                                                                             f.exp_avg_sq, f.grad)}.values())
+            g_in = getattr(mir, "_g_in", None)
+            if g_in is not None:
+                n += g_in.numel() * 4
+        return n
 
     # ------------------------------------------------------------------ tied weight (public sketch)
     def _tied_param(self, st: Stage) -> Optional[torch.Tensor]:
@@ -107,82 +129,88 @@ class CommitmentMixin:
             if t is not None:
                 self._tsk_pre[st.stage_id] = t
 
-    # ------------------------------------------------------------------ per-micro-batch commitments
+    # ------------------------------------------------------------------ per-micro-batch contributions
     def _begin_commitments(self, M: int):
-        """Commit state 0 of every local stage (the flat gradient before the first micro-batch's
-        backward): its exact hash and snapshot; the public running sketch for targeting."""
+        """Open the step's contribution rings (prev := the running gradient before the first
+        micro-batch's backward) and, for the targeted audit, the public running sketches."""
         self._gsk_on = bool(self.cfg.audit and self.cfg.audit_backward and self.plan.num_stages > 1 and self.dp == 1)
+        self._gring: Dict[int, torch.Tensor] = {}
+        self._gprev: Dict[int, torch.Tensor] = {}
         self._gsk_run: Dict[int, torch.Tensor] = {}
-        self._gcom: Dict[int, torch.Tensor] = {}
-        self._gsnap: Dict[int, torch.Tensor] = {}
         self._tsk_pre: Dict[int, torch.Tensor] = {}
+        self._mirror_pending = []
         if not self._gsk_on:
+            # a step whose gradients no mirror sees: every mirror must be re-seeded before it is used
+            self._invalidate_mirrors()
             return
         for node, st in self.stages.items():
-            self._gcom[node] = torch.zeros(M + 1, dtype=torch.int64, device=st.device)
-            self._gsnap[node] = self._snap_buffer(node, st, M)
-            self._commit_state(node, st, 0)
+            ring, prev = self._ring_buffers(node, st, M)
+            prev.copy_(st.flat.grad)
+            self._gring[node], self._gprev[node] = ring, prev
             if self._targeted:
                 sk = self._sketch_for(st)
                 r = torch.zeros(M + 1, 2, dtype=torch.float32, device=st.device)
                 r[0].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
                 self._gsk_run[node] = r
 
-    def _commit_state(self, node: int, st: Stage, k: int):
-        """Commitment k of the running gradient: exact hash + snapshot in one pass."""
-        from ..security.grad_audit import word_hash
-        word_hash(st.flat.grad, self._commit_segments(st), self._hash_seed(st), snapshot=self._gsnap[node][k],
-                  out=self._gcom[node][k:k + 1])
-
     def _commit_micro(self, node: int, st: Stage, i: int):
         """Micro-batch ``i``'s weight gradients of ``node`` are accumulated: (attack hook, then)
-        commit the running gradient."""
+        its contribution into the ring."""
+        from ..security.grad_audit import contrib_snap
         M = len(self._audit_batch)
         if self.attacker is not None and hasattr(self.attacker, "after_micro_backward"):
             if self.attacker.after_micro_backward(node, st.flat.grad, self.global_step, i, M):
                 self._truth_now[node] = True
-        if node in self._gcom:
-            self._commit_state(node, st, i + 1)
+        ring = self._gring.get(node)
+        if ring is not None:
+            contrib_snap(st.flat.grad, self._gprev[node], ring[i])
         r = self._gsk_run.get(node)
         if r is not None:
             sk = self._sketch_for(st)
             r[i + 1].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
 
-    @torch.no_grad()
-    def _answer_challenge(self, node: int, st: Stage, m: int, key: int) -> torch.Tensor:
-        """The audited stage's answer for micro-batch ``m`` under the revealed key: [K_KEYED + 4]
-        = keyed sketch of snapshot m+1 - snapshot m, then the two snapshots' hashes recomputed NOW
-        (each folded to two fp32 halves: the auditor compares them with the commitments it received
-        before the reveal, so a snapshot rewritten after committing fails)."""
-        from ..security.grad_audit import K_KEYED, fold_hash64, keyed_sketch, word_hash
-        segs = self._commit_segments(st)
-        snap = self._gsnap[node]
-        seed = self._hash_seed(st)
-        out = torch.empty(K_KEYED + 4, dtype=torch.float32, device=st.device)
-        out[:K_KEYED].copy_(keyed_sketch(snap[m + 1], segs, key, b=snap[m]))
-        out[K_KEYED:K_KEYED + 2].copy_(fold_hash64(word_hash(snap[m], segs, seed)))
-        out[K_KEYED + 2:K_KEYED + 4].copy_(fold_hash64(word_hash(snap[m + 1], segs, seed)))
-        return out
+    # ------------------------------------------------------------------ auditee answers (overridable)
+    def _applied_gradient(self, node: int, st: Stage) -> torch.Tensor:
+        """The flat gradient this stage applies (and ships to its auditor's mirror)."""
+        return st.flat.grad
 
+    @torch.no_grad()
+    def _contrib_commitments(self, node: int, st: Stage) -> torch.Tensor:
+        """[M + 2, 8] int32 roots: the M contributions, the applied gradient, the fp32 master
+        weights (before this step's update = after the previous one)."""
+        from ..security.grad_audit import merkle_root, merkle_roots
+        segs = self._commit_segments(st)
+        ring = self._gring[node]
+        M, n = ring.shape
+        C = torch.empty(M + 2, 8, dtype=torch.int32, device=st.device)
+        C[:M].copy_(merkle_roots(ring, segs, batch=M, stride=n))
+        C[M].copy_(merkle_root(self._applied_gradient(node, st), segs))
+        C[M + 1].copy_(merkle_root(st.flat.master))
+        return C
+
+    @torch.no_grad()
+    def _contrib_sketches(self, node: int, st: Stage, key: int) -> torch.Tensor:
+        """[M, K_KEYED] keyed sketches of the M committed contributions under the revealed key."""
+        from ..security.grad_audit import keyed_sketch
+        ring = self._gring[node]
+        M, n = ring.shape
+        return keyed_sketch(ring, self._commit_segments(st), key, batch=M, stride=n)
+
+    def _open_contributions(self, node: int, st: Stage, ms: List[int]) -> List[torch.Tensor]:
+        """The contributions of the opened micro-batches (views into the ring)."""
+        ring = self._gring[node]
+        return [ring[m] for m in ms]
+
+    def _optimizer_state(self, node: int, st: Stage) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, int]:
+        """(master, exp_avg, exp_avg_sq, step count): seeds the auditor's mirror once per plan."""
+        f = st.flat
+        return f.master, f.exp_avg, f.exp_avg_sq, f.step_count
+
+    # ------------------------------------------------------------------ digest slots + tied check
     def _write_commitments(self, node: int, st: Stage, d: torch.Tensor):
-        """Digest slots of the gradient commitments: the exact hash of the gradient about to be
-        applied (after the tied all-reduce and every hook) and of the committed running gradient
-        after the last micro-batch's backward.  They differ when the gradient was rewritten in
-        between, on any coordinate."""
-        from ..security.grad_audit import fold_hash64, word_hash
-        com = self._gcom.get(node) if self._gsk_on else None
-        if com is None:
-            d[SV.D_GSK_ON:SV.D_GSK_ON + 1].fill_(0.0)
-            return
-        d[SV.D_GSK_APP:SV.D_GSK_APP + 2].copy_(fold_hash64(word_hash(st.flat.grad, self._commit_segments(st),
-                                                                     self._hash_seed(st))))
-        d[SV.D_GSK_BWD:SV.D_GSK_BWD + 2].copy_(fold_hash64(com[-1]))
-        att = self.attacker
-        if att is not None and hasattr(att, "lies_about_commitment") and att.lies_about_commitment(node, self.global_step):
-            # simulated liar: its own row claims it committed what it applies
-            d[SV.D_GSK_BWD:SV.D_GSK_BWD + 2].copy_(d[SV.D_GSK_APP:SV.D_GSK_APP + 2])
-        d[SV.D_GSK_ON:SV.D_GSK_ON + 1].fill_(1.0)
-        pre = self._tsk_pre.get(st.stage_id)
+        """Digest slots of the tied-weight cross check: this stage's own contribution to the tied
+        gradient (before the all-reduce) and the tied gradient it applies."""
+        pre = self._tsk_pre.get(st.stage_id) if self._gsk_on else None
         if pre is not None:
             d[SV.D_TSK_PRE:SV.D_TSK_PRE + 2].copy_(pre)
             d[SV.D_TSK_APP:SV.D_TSK_APP + 2].copy_(self._tied_sketch(st))
@@ -190,32 +218,11 @@ class CommitmentMixin:
         else:
             d[SV.D_TSK_ON:SV.D_TSK_ON + 1].fill_(0.0)
 
-    def _gsk_mismatch(self, D: torch.Tensor) -> torch.Tensor:
-        """Per-node 1.0 where the applied gradient's hash differs from the committed running
-        gradient's (a gradient rewritten after the backward: exact, every coordinate), or (distributed)
-        where the last commitment a node reports differs from the one its auditor received.  The
-        applied hash itself is the node's own report: a rank that also lies about it is outside what
-        this check sees (the recompute audit of its committed contributions still applies)."""
+    def _tied_mismatch(self, D: torch.Tensor) -> torch.Tensor:
+        """Per-node 1.0 where a member of the tied weight's group applies a tied gradient that is not
+        the sum of the members' own contributions (public sketches, as reported by the members)."""
         from ..security.grad_audit import K_SKETCH
-        app = D[:, SV.D_GSK_APP:SV.D_GSK_APP + 2]
-        com = D[:, SV.D_GSK_BWD:SV.D_GSK_BWD + 2]
-        on = (D[:, SV.D_GSK_ON] > 0).float()
-        bad = on * (app != com).any(1).float()
-        if self.distributed and self.cfg.audit_backward:
-            for idx in self._replica_orders():
-                S = idx.numel()
-                for j in range(S):
-                    # the auditor of stage j: stage j + 1, or stage j - 1 for the loss stage
-                    if j + 1 < S:
-                        rec = D[idx[j + 1], SV.D_GCOM_RECV_PREV:SV.D_GCOM_RECV_PREV + 2]
-                    elif j > 0:
-                        rec = D[idx[j - 1], SV.D_GCOM_RECV_NEXT:SV.D_GCOM_RECV_NEXT + 2]
-                    else:
-                        continue
-                    n = idx[j]
-                    held = (rec > 0).all().float() * on[n]
-                    bad[n] = torch.maximum(bad[n], held * (rec - 1.0 != com[n]).any().float())
-        # the tied weight: every member must apply the sum of the members' own contributions
+        bad = torch.zeros(D.shape[0], dtype=torch.float32, device=D.device)
         ton = (D[:, SV.D_TSK_ON] > 0).float()
         pre, tapp = D[:, SV.D_TSK_PRE:SV.D_TSK_PRE + K_SKETCH], D[:, SV.D_TSK_APP:SV.D_TSK_APP + K_SKETCH]
         for idx in self._replica_orders():

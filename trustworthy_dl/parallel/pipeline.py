@@ -170,15 +170,18 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._audit_outputs: Dict[int, torch.Tensor] = {}
         self._early_ship = None                  # (P2P works, mirrors) of the early weight shipment
         self._audit_rng = None                   # distributed auditor's private RNG (audit_dist.py)
-        self._audit_cost = {"steps": 0, "host_s": 0.0, "bytes": 0, "events": []}
+        self._audit_cost = {"steps": 0, "host_s": 0.0, "bytes": 0, "events": [], "seeds": 0, "seed_bytes": 0}
         self._target_log: List[Tuple[int, int, int]] = []
         self._mirrors: Dict[Tuple[int, Tuple[int, int]], Stage] = {}
-        # gradient commitments (commitments.py)
+        # gradient commitments (commitments.py) and optimizer mirrors (audit.py)
         self._gsk_on = False
         self._gsk_run: Dict[int, torch.Tensor] = {}      # public running sketches (targeting)
-        self._gcom: Dict[int, torch.Tensor] = {}         # exact hashes of the running gradient [M+1]
-        self._gsnap: Dict[int, torch.Tensor] = {}        # snapshots of the running gradient [M+1, n]
-        self._gsnap_cache: Dict[tuple, torch.Tensor] = {}
+        self._gring: Dict[int, torch.Tensor] = {}        # [M, n] per-micro-batch contributions
+        self._gprev: Dict[int, torch.Tensor] = {}        # [n] running gradient before the next one
+        self._gring_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._mirror_epoch = 0                           # bumped on every rank when mirrors go stale
+        self._mirror_pending: List = []                  # (mirror, verified gradient, node) to apply
+        self._seed_mark = None                           # (plan, range, epoch) my auditor's mirror was seeded for
         self._tsk_pre: Dict[int, torch.Tensor] = {}
         self._gsk_cache: Dict[tuple, object] = {}
         self._tsk_cache: Dict[tuple, object] = {}
@@ -602,14 +605,6 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._step_time = time.perf_counter() - t0
         return self.last_loss
 
-
-
-
-
-
-
-
-
     def begin_step(self) -> int:
         """Open an optimizer step (``train_step`` does this itself; the reference per-phase API —
         DistributedTrainer.forward_pass / backward_pass / optimizer_step — calls it explicitly)."""
@@ -627,16 +622,14 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
     def end_step(self, loss: Optional[torch.Tensor], truth: Optional[Dict[int, bool]] = None) -> Optional[float]:
         """Close a step whose gradients are already accumulated in the stages' flat buffers (by an
         external ``loss.backward()``): tied all-reduce, verification digest, attribution, trust
-        update, global-norm clipping + quarantine, fused AdamW — the same tail as ``train_step``."""
+        update, global-norm clipping + quarantine, fused AdamW — the same tail as ``train_step``.
+        No gradient commitments are taken on this path, so the auditors' mirrors go stale."""
+        self._invalidate_mirrors()
+        self._mirror_pending = []
         self._finish_step(None if loss is None else loss.detach(), dict(truth or {}))
         self.tracer.end_step(self.global_step)
         self.tracer.resolve()
         return self.last_loss
-
-
-
-
-
 
 
 
@@ -729,14 +722,13 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
             hm = self._host_metric_row(node)
             d = st.verifier.finish_step(st.flat.grad, loss if st.computes_loss else None, hm,
                                         truth.get(node, False), st.stage_id)
-            # the weight commitment made after this stage's last update (before anything of this
-            # step could touch the weights): the auditor checks the weights it receives against it
-            pc = st.param_checksum
-            if pc is not None and self.cfg.audit and self.plan.num_stages > 1:
-                from ..security.grad_audit import fold_hash
-                d[SV.D_WHASH:SV.D_WHASH + 2].copy_(fold_hash(pc))
+            # weight-shipping mode (no mirror): the root of the weights in use this step (= after the
+            # last update); the auditor hashes the weights it receives and every rank compares
+            if self.distributed and self._audit_now and not self._gsk_on:
+                from ..security.grad_audit import hash_row
+                d[SV.D_WHASH:SV.D_WHASH + 8].copy_(hash_row(self._tensor_root(st.flat.data)))
             else:
-                d[SV.D_WHASH:SV.D_WHASH + 2].fill_(-1.0)
+                d[SV.D_WHASH:SV.D_WHASH + 8].fill_(-1.0)
             if self.cfg.param_integrity:
                 d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].copy_(self._integrity_flag(st))
                 if self.attacker is not None and getattr(self.attacker, "lies_about_integrity", None) \
@@ -744,7 +736,7 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
                     d[SV.D_PARAM_FLAG:SV.D_PARAM_FLAG + 1].fill_(0.0)   # a rank lying about its own check
             self._write_commitments(node, st, d)
             rows.append((node, d))
-        if self._audit_now:
+        if self._audit_now or self._gsk_on:
             ta = self.tracer.begin("audit")
             progress.mark(f"step {self.global_step}: recompute audit")
             t_a = time.perf_counter()
@@ -771,7 +763,12 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
             for node, d in rows:
                 D[node].copy_(d.to(self.device))
         blame, evidence = self._attribute(D)
-        if self.quarantine_on_evidence:
+        if self._gsk_on:
+            # mirror mode: the skip decision comes from the digest alone (its auditor's mirror takes
+            # the same one: audit.py _skip_decision)
+            for node, st in self.stages.items():
+                st.verifier.ctrl[1:2].copy_(self._skip_decision(D, evidence, node).to(st.device))
+        elif self.quarantine_on_evidence:
             # a tampered forward (output anomaly / failed integrity check anywhere in the pipeline)
             # taints every gradient of the step: skip the update on all of the replica's stages, so
             # the damage does not echo into the next step's outputs
@@ -817,6 +814,9 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self.tracer.end(tv)
         progress.mark(f"step {self.global_step}: optimizer")
         to = self.tracer.begin("optimizer")
+        if self._mirror_pending:
+            # before the stages' own updates: in local mode a mirror reads its stage's gradient buffer
+            self._mirror_update(D, evidence, total_sumsq)
         for node, st in self.stages.items():
             st.verifier.set_clip_scale(total_sumsq.to(st.device), self.cfg.adamw.max_grad_norm)
             cur = st._cur_checksum
@@ -832,7 +832,7 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         if self.dp > 1 and self.cfg.param_audit_interval and self.global_step % self.cfg.param_audit_interval == 0:
             self._audit_params()
         # queue the host report (pinned, non-blocking)
-        if self._audit_now:
+        if self._audit_now or self._gsk_on:
             _, adone = self._audit_vectors(D)
         else:
             adone = torch.zeros(N, dtype=torch.float32, device=self.device)
@@ -847,59 +847,10 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
             host, ev = rep.clone(), None
         self._pending.append((self.global_step, self.epoch, host, ev, dict(truth), list(self.last_ranks())))
 
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
     def close(self):
         if self.heartbeat is not None:
             self.heartbeat.stop()
             self.heartbeat = None
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
-
 
 
 
@@ -938,10 +889,3 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
                     self.comm.exchange(send_next=y)
         dist.all_reduce(total)
         return float(total) / self.dp
-
-
-
-
-
-
-

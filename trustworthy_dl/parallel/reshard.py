@@ -226,7 +226,15 @@ class ReshardMixin:
         since = max([r["step"] for r in self.reassignment_history if "step" in r] + [-1])
         blames = [a["step"] for a in self.attack_history if a.get("node_id") == c and a["step"] > since]
         first = min(blames) if blames else self.global_step
-        cands = [(p, st) for p, st in self._checkpoints if st < first and os.path.exists(p)]
+        cands = [(p, st) for p, st in self._checkpoints if st < first]
+        seen = torch.tensor([1.0 if os.path.exists(p) else 0.0 for p, _ in cands] or [0.0], device=self.device)
+        if self.distributed:
+            # every rank must restore from the same source: only a checkpoint visible on ALL ranks
+            # counts (a non-shared filesystem would otherwise split the re-shard)
+            dist.all_reduce(seen, op=dist.ReduceOp.MIN)
+        note_host_sync()
+        ok = seen.tolist()
+        cands = [c for c, v in zip(cands, ok) if v > 0]
         return max(cands, key=lambda x: x[1]) if cands else None
 
     def _pack_from_checkpoint(self, layers: Dict[int, Dict], li: int, device) -> torch.Tensor:
@@ -443,6 +451,7 @@ class ReshardMixin:
         ph["unpack_s"] = time.perf_counter() - t3
         self._shape_cache = {}
         self._gsk_cache = {}
+        self._gring_cache = {}               # contribution rings of the old layout
         self.refresh_shadows()               # the snapshot ring follows the plan: a fresh committed copy now
         ph["transfer_bytes"] = xfer_bytes
         ph["local_bytes"] = sum(self._packed_numel(li) * 4 for li in range(self.num_layers)

@@ -159,7 +159,7 @@ class ScheduleMixin:
         out_q: deque = deque()
         total = [None]
         waited0 = comm.wait_seconds
-        keep_out = self._audit_now and self.cfg.audit_backward and s == S - 2
+        keep_out = self._audit_now and self.cfg.audit_backward and not last   # loss-stage inputs + x cross-check
         self._audit_outputs: Dict[int, torch.Tensor] = {}
 
         def get_input(i):
@@ -301,8 +301,9 @@ class ScheduleMixin:
         total = [None]
         waited = [0.0]
         defer_w = self.cfg.defer_wgrad and not first
-        # the stage before the loss stage audits it and needs its own outputs (the loss stage's inputs)
-        keep_out = self._audit_now and self.cfg.audit_backward and s == S - 2
+        # my outputs stay referenced until the audit: the loss stage's inputs (I audit it) and the next
+        # stage's inputs (its auditor compares the copies it receives with what I sent)
+        keep_out = self._audit_now and self.cfg.audit_backward and not last   # loss-stage inputs + x cross-check
         self._audit_outputs: Dict[int, torch.Tensor] = {}
 
         step = self.global_step

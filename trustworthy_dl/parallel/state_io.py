@@ -83,6 +83,7 @@ class StateIOMixin:
                 st.flat.data.copy_(st.flat.master)
             st.param_checksum = None
         bump_weight_generation()
+        self._invalidate_mirrors()   # every rank loads: mirrors are re-seeded from the loaded state
         self.refresh_shadows()    # the loaded weights are the new trusted copy
 
     def load_stage_states(self, model_sd: Dict[int, Dict], optim_sd: Dict[int, Dict],
@@ -107,4 +108,5 @@ class StateIOMixin:
             if verifier_sd and node in verifier_sd:
                 st.verifier.load_state_dict(verifier_sd[node])
             st.param_checksum = None  # weights legitimately replaced
+        self._invalidate_mirrors()
         self.refresh_shadows()        # the loaded weights are the new trusted copy

@@ -41,6 +41,8 @@ def lib() -> ctypes.CDLL:
                 L.tdl_loader_num_tokens.restype = L64
                 L.tdl_loader_destroy.argtypes = [P]
                 L.tdl_loader_destroy.restype = None
+                L.tdl_host_merkle.argtypes = [P, L64, I, P, P, I, I, P]
+                L.tdl_host_merkle.restype = I
                 _lib = L
     return _lib
 

@@ -77,6 +77,8 @@ def _quantiles(x: np.ndarray, ps: Sequence[float]) -> List[float]:
     n = x.size
     if n == 0:
         return [0.0 for _ in ps]
+    if np.isnan(x).any():   # np.median / np.percentile propagate NaN; a partition would sort it to the end
+        return [float("nan") for _ in ps]
     pos = [(n - 1) * p for p in ps]
     lo = [int(np.floor(v)) for v in pos]
     hi = [min(l + 1, n - 1) for l in lo]

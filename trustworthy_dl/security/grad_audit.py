@@ -1,52 +1,43 @@
-"""Backward-pass audit primitives: gradient sketches and exact tensor hashes.
+"""Backward-pass audit primitives: collision-resistant commitments, keyed sketches, contributions.
 
 The reference's gradient check is a z-score over host statistics (attack_detector.py:109-141) that
-cannot see a sign-flipped gradient (its F1 is 0.0) and its Byzantine check
-compares outputs of DIFFERENT stages (attack_detector.py:143-162, 225-239).  Here the backward is
-audited the way the forward is (parallel/pipeline.py ``_audit``): by recomputation.
+cannot see a sign-flipped gradient (its F1 is 0.0), and its optimizer step
+(distributed_trainer.py:197-205, :441-446) applies whatever gradient a node holds.  Here a stage's
+gradient is bound by a commit / key / open protocol that its auditor verifies on data it hashes
+itself (parallel/commitments.py, parallel/audit.py):
 
-* ``GradSketch`` — K random-sign projections of a sampled subset of a stage's flat fp32 gradient:
-  from every block of ``block`` elements a window of ``win`` elements at a per-step offset (so each
-  sketch reads ~1/16 of the buffer in whole cache lines), times a fixed +-1 pattern.  Linear, so
-  the sketch of one micro-batch's weight-gradient contribution is the difference of two running
-  sketches taken around its backward.  A stage COMMITS the running sketch after every
-  micro-batch's backward and the sketch of the gradient it finally applies; its auditor recomputes
-  one privately chosen micro-batch's backward and compares that contribution's sketch, and every
-  rank checks that the applied gradient equals the sum of the committed contributions (a gradient
-  rewritten between backward and optimizer — scaled, noised, zeroed or sign-flipped — fails this
-  deterministically).  Blocks that hold a tied weight (whose gradient the tied all-reduce adds to)
-  carry zero signs.
-* ``hash2`` — an exact 32-bit fold of ``ops.stats.checksum`` (float64 sum / sum of squares /
-  position-weighted sum), split into two 16-bit halves that an fp32 digest row carries exactly.
-
-``GradSketch``'s sampling offset and sign patterns are public (derived from the job seed, the step
-and the stage's layer range): an adaptive adversary that knows them hides a perturbation in the
-unsampled coordinates or in the null space of the public signs (attacks/adversarial_attacks.py
-``adaptive``; tests/test_keyed_audit.py shows it passes that sketch).  It now only ranks micro-batches
-for the targeted audit.  The binding checks use
-
-* ``word_hash`` — an EXACT, order-independent 64-bit hash of a buffer's 32-bit words
-  (csrc/audit.hip): the running gradient after every micro-batch and the applied gradient are
-  committed by hash, so a gradient rewritten between backward and optimizer fails bit-exactly, on
-  every coordinate;
+* ``merkle_roots`` — BLAKE2s Merkle root (256 bits) of a buffer's 32-bit words over a list of
+  segments: leaves of 256 words (node_offset = leaf index, node_depth = 0), internal nodes over 32
+  child digests (node_depth = level), one root per segment, then a combine node over the segment
+  roots (node_depth = 255, last_node).  GPU: csrc/audit.hip, one thread per leaf / node, batched over
+  the step's M contributions; CPU: ``hashlib.blake2s`` with the same node parameters, which is also
+  the oracle of the GPU test.  Collision resistant, so an auditee cannot open a commitment to two
+  different vectors (r5's additive mix32 hash had O(1) second preimages: scripts/lying_rank_before.py).
 * ``keyed_sketch`` — K = 4 full-coverage random-sign projections whose signs come from a PRIVATE
-  per-step key the auditor reveals only after the auditee's commitments were sent: the auditee
-  answers with the keyed sketch of the audited micro-batch's committed contribution (the difference
-  of two snapshots whose hashes it committed), the auditor compares it with the sketch of its
-  recomputation.  A perturbation chosen before the key is known cannot avoid the signs.
+  per-step key the auditor reveals only after it RECEIVED the commitments; linear, so the sketch of
+  the applied gradient must equal the sum of the contributions' sketches.
+* ``contrib_snap`` — after micro-batch i's weight gradients: c_i = g - prev, prev = g.
+* ``GradSketch`` — K = 2 PUBLIC sketches of a 1/16 sample (job seed, step, layer range): only used
+  to rank micro-batches for the targeted audit, never as a commitment (an adaptive adversary hides
+  in its unsampled coordinates: tests/test_keyed_audit.py).
+* ``hash_row`` — the first 128 bits of a root as eight exact fp32 16-bit halves for a digest row
+  (cross-party comparisons: what one honest rank received vs what the auditee shipped).
 """
 from __future__ import annotations
 
 import hashlib
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Iterable, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
-
-from ..ops import stats as dstats
 
 K_SKETCH = 2
 K_KEYED = 4
 M32 = 0xFFFFFFFF
+LEAF_WORDS = 256
+FANOUT = 32
+DIGEST_WORDS = 8
+ROW_WORDS = 8          # digest-row floats per hash (128 bits as 16-bit halves)
 
 
 def _mix32(x: torch.Tensor) -> torch.Tensor:
@@ -70,90 +61,181 @@ def _segments(n: int, masked: Sequence[Tuple[int, int]] = ()) -> List[Tuple[int,
     return segs
 
 
-_pmix: Dict[Tuple[int, int, int], torch.Tensor] = {}
+# ====================================================================== BLAKE2s Merkle commitment
+def _b2s(data, off: int, depth: int, last: bool = False) -> bytes:
+    return hashlib.blake2s(data, digest_size=32, node_offset=off, node_depth=depth, last_node=last).digest()
 
 
-def _position_mix(lo: int, hi: int, seed: int) -> torch.Tensor:
-    """CPU path: mix(j ^ seed) over [lo, hi) (one seed serves every commitment of a step)."""
-    key = (lo, hi, seed)
-    t = _pmix.get(key)
-    if t is None:
-        if len(_pmix) > 16:
-            _pmix.clear()
-        t = _pmix[key] = _mix32((torch.arange(lo, hi, dtype=torch.int64) & M32) ^ seed)
-    return t
+def _tree_cpu(words: np.ndarray) -> bytes:
+    """Root of one segment (uint32 words, >= 1): leaves, then >= 1 level of internal nodes."""
+    buf = memoryview(np.ascontiguousarray(words, dtype="<u4").tobytes())
+    lb = LEAF_WORDS * 4
+    level = [_b2s(buf[j * lb:(j + 1) * lb], j, 0) for j in range((len(buf) + lb - 1) // lb)]
+    depth = 1
+    while True:
+        level = [_b2s(b"".join(level[j * FANOUT:(j + 1) * FANOUT]), j, depth)
+                 for j in range((len(level) + FANOUT - 1) // FANOUT)]
+        depth += 1
+        if len(level) == 1:
+            return level[0]
 
 
-@torch.no_grad()
-def word_hash(x: torch.Tensor, segments: Sequence[Tuple[int, int]], seed: int = 0,
-              snapshot: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Exact 64-bit hash (int64 device tensor [1]) of the 32-bit words of flat ``x`` over
-    ``segments`` (global word indices); with ``snapshot`` the same pass copies those words into it.
-    No host sync.  Identical bits give identical hashes on CPU and GPU."""
-    x = x.reshape(-1)
-    if x.element_size() != 4:
-        raise ValueError("word_hash works on 32-bit words")
-    if out is None:
-        out = torch.zeros(1, dtype=torch.int64, device=x.device)
-    else:
-        out.zero_()
-    if x.is_cuda:
-        from ..ops import _lib
-        from ..ops._lib import ptr, stream_ptr
-        for lo, hi in segments:
-            _lib.call("tdl_word_hash", ptr(x), ptr(snapshot), int(lo), int(hi), int(seed) & M32, ptr(out),
-                      stream_ptr(x.device))
-        return out
-    w = x.view(torch.int32).to(torch.int64) & M32
-    tot = torch.zeros((), dtype=torch.int64)
-    for lo, hi in segments:
-        tot = tot + _mix32(w[lo:hi] ^ _position_mix(lo, hi, int(seed) & M32)).sum()
-        if snapshot is not None:
-            snapshot.reshape(-1)[lo:hi].copy_(x[lo:hi])
-    out.copy_(tot.reshape(1))
+def _combine_cpu(roots: Sequence[bytes]) -> bytes:
+    return _b2s(b"".join(roots), 0, 255, last=True)
+
+
+def _root_bytes_to_tensor(b: bytes) -> torch.Tensor:
+    return torch.from_numpy(np.frombuffer(b, dtype="<u4").astype(np.int64)).to(torch.int32)
+
+
+def merkle_roots_hashlib(x: torch.Tensor, segments: Sequence[Tuple[int, int]], batch: int = 1,
+                         stride: int = 0) -> torch.Tensor:
+    """The same roots with Python's hashlib.blake2s: the oracle of the native paths' tests."""
+    w = x.reshape(-1).contiguous().view(torch.int32).numpy().view(np.uint32)
+    segs = [(int(lo), int(hi)) for lo, hi in segments if hi > lo]
+    out = [_root_bytes_to_tensor(_combine_cpu([_tree_cpu(w[y * stride + lo:y * stride + hi]) for lo, hi in segs]))
+           for y in range(batch)]
+    return torch.stack(out) if out else torch.zeros(0, DIGEST_WORDS, dtype=torch.int32)
+
+
+def _merkle_host(flat: torch.Tensor, segs, batch: int, stride: int) -> torch.Tensor:
+    """CPU tensors: the C++ host runtime (csrc/runtime/merkle.cpp, threads over leaves)."""
+    import ctypes
+    import os
+    from ..runtime import native
+    x = flat.contiguous()
+    out = torch.empty(batch, DIGEST_WORDS, dtype=torch.int32)
+    lo = (ctypes.c_longlong * max(1, len(segs)))(*[a for a, _ in segs])
+    hi = (ctypes.c_longlong * max(1, len(segs)))(*[b for _, b in segs])
+    threads = max(1, min(8, torch.get_num_threads(), os.cpu_count() or 1))
+    rc = native.lib().tdl_host_merkle(ctypes.c_void_p(x.data_ptr()), stride, batch, lo, hi, len(segs), threads,
+                                      ctypes.c_void_p(out.data_ptr()))
+    if rc != 0:
+        raise RuntimeError(f"tdl_host_merkle failed ({rc})")
     return out
 
 
-def fold_hash64(h: torch.Tensor) -> torch.Tensor:
-    """A ``word_hash`` as two fp32 values in [0, 65536) (its 32-bit fold) for a digest row."""
-    h = h.reshape(())
-    f = (h ^ (h >> 32)) & M32
-    return torch.stack([(f & 0xFFFF).float(), ((f >> 16) & 0xFFFF).float()])
+@torch.no_grad()
+def merkle_roots(x: torch.Tensor, segments: Sequence[Tuple[int, int]], batch: int = 1,
+                 stride: Optional[int] = None) -> torch.Tensor:
+    """[batch, 8] int32 (raw uint32 bits) BLAKE2s Merkle roots of the 32-bit words of
+    ``x.reshape(-1)[y * stride + lo : y * stride + hi]`` over ``segments``, y < batch.  Device
+    tensors stay on the device (no host sync); identical bits on CPU and GPU."""
+    flat = x.reshape(-1)
+    if flat.element_size() != 4:
+        raise ValueError("merkle_roots hashes 32-bit words")
+    stride = int(stride if stride is not None else 0)
+    segs = [(int(lo), int(hi)) for lo, hi in segments if hi > lo]
+    if not flat.is_cuda:
+        return _merkle_host(flat, segs, batch, stride)
+    from ..ops import _lib
+    from ..ops._lib import ptr, stream_ptr
+    dev = flat.device
+    sp = stream_ptr(dev)
+    final = torch.empty(batch, DIGEST_WORDS, dtype=torch.int32, device=dev)
+    if not segs:
+        final.copy_(_root_bytes_to_tensor(_combine_cpu([])).expand(batch, -1))
+        return final
+    nseg = len(segs)
+    roots = torch.empty(batch, nseg, DIGEST_WORDS, dtype=torch.int32, device=dev)
+    for k, (lo, hi) in enumerate(segs):
+        n = (hi - lo + LEAF_WORDS - 1) // LEAF_WORDS
+        cur = torch.empty(batch, n * DIGEST_WORDS, dtype=torch.int32, device=dev)
+        _lib.call("tdl_b2s_leaves", ptr(flat), stride, batch, lo, hi, ptr(cur), n * DIGEST_WORDS, sp)
+        depth = 1
+        while True:
+            n_out = (n + FANOUT - 1) // FANOUT
+            if n_out == 1:
+                dst, dstride = roots[:, k], nseg * DIGEST_WORDS
+            else:
+                dst = torch.empty(batch, n_out * DIGEST_WORDS, dtype=torch.int32, device=dev)
+                dstride = n_out * DIGEST_WORDS
+            _lib.call("tdl_b2s_nodes", ptr(cur), n * DIGEST_WORDS, n, batch, FANOUT, depth, 0, ptr(dst), dstride, sp)
+            if n_out == 1:
+                break
+            cur, n, depth = dst, n_out, depth + 1
+    _lib.call("tdl_b2s_nodes", ptr(roots), nseg * DIGEST_WORDS, nseg, batch, nseg, 255, 1, ptr(final),
+              DIGEST_WORDS, sp)
+    return final
 
 
+def merkle_root(x: torch.Tensor, segments: Optional[Sequence[Tuple[int, int]]] = None) -> torch.Tensor:
+    """[8] int32 Merkle root of one buffer (all of it when ``segments`` is None)."""
+    if segments is None:
+        segments = [(0, x.numel())]
+    return merkle_roots(x, segments)[0]
+
+
+def roots_differ(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """[1] float 1.0 where two roots (or [n, 8] root lists, compared row by row and OR-ed) differ."""
+    return (a.to(b.device) != b).any().float().reshape(1)
+
+
+def hash_row(root: torch.Tensor) -> torch.Tensor:
+    """First 128 bits of a root as 8 fp32 values in [0, 65536) (exact) for a digest row."""
+    h = root.reshape(-1)[:4].to(torch.int64) & M32
+    return torch.stack([h & 0xFFFF, h >> 16], dim=1).reshape(-1).float()
+
+
+def root_hex(root: torch.Tensor) -> str:
+    return np.asarray(root.detach().cpu().to(torch.int64) & M32, dtype="<u4").tobytes().hex()
+
+
+# ====================================================================== keyed sketch
 def key_words(key: int) -> Tuple[int, int]:
     return int(key) & M32, (int(key) >> 32) & M32
 
 
 @torch.no_grad()
 def keyed_sketch(a: torch.Tensor, segments: Sequence[Tuple[int, int]], key: int,
-                 b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[K_KEYED] fp32 keyed random-sign sketch of flat ``a`` (minus ``b``) over ``segments``: sign
-    k of word j is bit 28 + k of mix(mix(j ^ k0) ^ k1), key = (k0, k1).  Device, no host sync."""
+                 b: Optional[torch.Tensor] = None, batch: Optional[int] = None,
+                 stride: Optional[int] = None) -> torch.Tensor:
+    """Keyed random-sign sketch of flat ``a`` (minus ``b``) over ``segments``: sign k of word j is
+    bit 28 + k of mix(mix(j ^ k0) ^ k1), key = (k0, k1).  [K_KEYED] fp32, or [batch, K_KEYED] for
+    ``a.reshape(-1)[y * stride + j]``.  Device, no host sync; fixed-order reductions, so the
+    auditee's and the auditor's values of the same bits are identical."""
+    single = batch is None
+    batch = 1 if single else int(batch)
+    stride = int(stride if stride is not None else 0)
     a = a.reshape(-1)
     k0, k1 = key_words(key)
-    out = torch.zeros(K_KEYED, dtype=torch.float32, device=a.device)
+    out = torch.zeros(batch, K_KEYED, dtype=torch.float32, device=a.device)
     if a.is_cuda:
         from ..ops import _lib
         from ..ops._lib import ptr, stream_ptr
         n = max((hi - lo for lo, hi in segments), default=0)
-        ws = torch.empty(max(4, int(_lib.lib().tdl_keyed_sketch_ws_floats(max(1, n)))), dtype=torch.float32,
-                         device=a.device)
+        per = int(_lib.lib().tdl_keyed_sketch_ws_floats(max(1, n)))
+        ws = torch.empty(max(4, per * batch), dtype=torch.float32, device=a.device)
         for i, (lo, hi) in enumerate(segments):
-            _lib.call("tdl_keyed_sketch", ptr(a), ptr(None if b is None else b.reshape(-1)), int(lo), int(hi),
-                      k0, k1, ptr(ws), ptr(out), 1 if i else 0, stream_ptr(a.device))
-        return out
+            _lib.call("tdl_keyed_sketch", ptr(a), stride, batch, ptr(None if b is None else b.reshape(-1)), int(lo),
+                      int(hi), k0, k1, ptr(ws), ptr(out), 1 if i else 0, stream_ptr(a.device))
+        return out[0] if single else out
     bf = None if b is None else b.reshape(-1)
     for lo, hi in segments:
         j = torch.arange(lo, hi, dtype=torch.int64) & M32
         h = _mix32(_mix32(j ^ k0) ^ k1)
-        v = a[lo:hi].float() if bf is None else a[lo:hi].float() - bf[lo:hi].float()
-        for k in range(K_KEYED):
-            s = 1.0 - 2.0 * ((h >> (28 + k)) & 1).float()
-            out[k] += (s * v).sum()
-    return out
+        signs = torch.stack([1.0 - 2.0 * ((h >> (28 + k)) & 1).float() for k in range(K_KEYED)])
+        for y in range(batch):
+            v = a[y * stride + lo:y * stride + hi].float()
+            if bf is not None:
+                v = v - bf[lo:hi].float()
+            out[y] += (signs * v).sum(1)
+    return out[0] if single else out
 
 
+@torch.no_grad()
+def contrib_snap(g: torch.Tensor, prev: torch.Tensor, c: torch.Tensor) -> None:
+    """c = g - prev; prev = g (one micro-batch's weight-gradient contribution, fp32)."""
+    if g.is_cuda:
+        from ..ops import _lib
+        from ..ops._lib import ptr, stream_ptr
+        _lib.call("tdl_contrib_snap", ptr(g), ptr(prev), ptr(c), g.numel(), stream_ptr(g.device))
+        return
+    torch.sub(g, prev, out=c)
+    prev.copy_(g)
+
+
+# ====================================================================== public sketch (targeting only)
 def _block_for(n: int) -> int:
     b = 4096
     while b > 64 and n < 64 * b:
@@ -162,6 +244,8 @@ def _block_for(n: int) -> int:
 
 
 class GradSketch:
+    """K_SKETCH random-sign projections of a public 1/16 sample of a flat gradient (targeting)."""
+
     def __init__(self, numel: int, device, seed: int, masked: Iterable[Tuple[int, int]] = ()):
         self.numel = int(numel)
         self.block = _block_for(self.numel)
@@ -172,8 +256,6 @@ class GradSketch:
         if self.nblk == 0:
             signs.zero_()
         # elements of a tied weight do not count: every block a tied range touches gets zero signs
-        # (a block only partly covered used to add the tied elements in one kernel and
-        # subtract them in a second, so a tied all-reduce writing in between skewed the sketch)
         for lo, hi in masked:
             b0, b1 = lo // self.block, min(self.nblk, (hi + self.block - 1) // self.block)
             if b1 > b0:
@@ -203,23 +285,8 @@ def sketch_mismatch(seen: torch.Tensor, ref: torch.Tensor, tol: float, floor: Op
     return (err > tol).float().reshape(1), err.reshape(1)
 
 
-@torch.no_grad()
-def hash2(x: torch.Tensor) -> torch.Tensor:
-    """Exact 32-bit hash of a tensor's bytes as two fp32 values in [0, 65536) (device)."""
-    return fold_hash(dstats.checksum(x.reshape(-1)))
-
-
-def fold_hash(c: torch.Tensor) -> torch.Tensor:
-    bits = c.double().contiguous().view(torch.int64)
-    h = torch.zeros((), dtype=torch.int64, device=c.device)
-    for i in range(bits.numel()):
-        h = (h * 1000003) ^ bits[i]
-    h = h ^ (h >> 32)
-    h = h & 0xFFFFFFFF
-    return torch.stack([(h & 0xFFFF).float(), ((h >> 16) & 0xFFFF).float()])
-
-
 def tied_ranges(flat, tied_ids: Sequence[int]):
     """Flat-buffer ranges of the parameters in ``tied_ids``."""
     ids = set(tied_ids)
     return [(o, o + n) for q, o, n in zip(flat.params, flat.offsets, flat.sizes) if id(q) in ids]
+

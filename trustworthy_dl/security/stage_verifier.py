@@ -54,30 +54,29 @@ D_AUDIT_PREV = 24    # recompute audit of the PREVIOUS stage's monitored micro-b
                      # not match f(input; weights) recomputed here (parallel/pipeline.py _audit)
 D_AUDITED_PREV = 25  # 1 when that audit ran this step
 D_AUDIT_ERR = 26     # its relative max error
-# backward audit (parallel/pipeline.py _audit, security/grad_audit.py)
-D_GSK_APP = 27       # [2] sketch of the gradient this stage applies (after every hook, before AdamW)
-D_GSK_BWD = 29       # [2] its committed running sketch after the last micro-batch's backward
-D_AUDIT_KIND_PREV = 31  # bitmask of the failed checks behind D_AUDIT_PREV (AK_* below)
-D_AUDIT_NEXT = 32    # audit of the NEXT stage when it is the loss stage (its predecessor audits it)
-D_AUDITED_NEXT = 33
-D_AUDIT_KIND_NEXT = 34
-D_WHASH = 35         # [2] exact hash of this stage's compute weights committed after its last update
-D_WHASH_PREV = 37    # [2] hash of the weights the audited previous stage shipped here
-D_WHASH_NEXT = 39    # [2] same for the audited next (loss) stage
-D_DXHASH_RECV = 41   # [2] hash of the input gradient received from the next stage for the
-                     #     micro-batch that stage's auditor chose (distributed)
-D_DXHASH_SHIP = 43   # [2] hash of the input gradient the audited previous stage shipped here
-D_GSK_ON = 45        # 1 when D_GSK_* hold commitments this step
-D_TSK_PRE = 46       # [2] sketch of this stage's OWN gradient of its tied weight (before the tied all-reduce)
-D_TSK_APP = 48       # [2] sketch of the tied weight's gradient it applies (after the all-reduce and hooks)
-D_TSK_ON = 50        # 1 when this stage holds a member of the (first) tie group
-D_GCOM_RECV_PREV = 51  # [2] (distributed) 1 + the fold of the last gradient commitment the audited
-                       #     previous stage SENT here (0 = none this step)
-D_GCOM_RECV_NEXT = 53  # [2] same for the audited next (loss) stage: a stage cannot report a different
-                       #     last commitment in its own row than the one its auditor holds
-DIGEST = 55
+# backward audit (parallel/audit.py, parallel/commitments.py, security/grad_audit.py)
+D_AUDIT_KIND_PREV = 27  # bitmask of the failed checks behind D_AUDIT_PREV (AK_* below)
+D_AUDIT_NEXT = 28    # audit of the NEXT stage when it is the loss stage (its predecessor audits it)
+D_AUDITED_NEXT = 29
+D_AUDIT_KIND_NEXT = 30
+D_TSK_ON = 31        # 1 when this stage holds a member of the (first) tie group
+D_TSK_PRE = 32       # [2] sketch of this stage's OWN gradient of its tied weight (before the tied all-reduce)
+D_TSK_APP = 34       # [2] sketch of the tied weight's gradient it applies (after the all-reduce and hooks)
+D_MIRROR = 36        # 1 when this rank checked its audited stages against live optimizer mirrors this step
+# cross-party hashes: the first 128 bits of BLAKE2s Merkle roots as 8 exact 16-bit halves each
+# (grad_audit.hash_row); -1 = none this step
+D_WHASH = 37         # [8] (weight-shipping mode) root of this stage's compute weights after its last update
+D_WHASH_PREV = 45    # [8] root of the weights the audited previous stage shipped here
+D_WHASH_NEXT = 53    # [8] same for the audited next (loss) stage
+D_DXHASH_RECV = 61   # [8] root of the input gradients received from the next stage for the micro-batches
+                     #     that stage's auditor opened (distributed)
+D_DXHASH_SHIP = 69   # [8] root of the input gradients the audited previous stage shipped here
+D_XHASH_SENT = 77    # [8] root of the outputs this stage SENT to the next stage for the micro-batches
+                     #     that stage's auditor opened (= their inputs)
+D_XHASH_SHIP = 85    # [8] root of the inputs the audited previous stage shipped here
+DIGEST = 93          # csrc/stats.hip VD_DIGEST
 # audit check bits
-AK_FWD, AK_DX, AK_DW, AK_WHASH, AK_DXHASH = 1, 2, 4, 8, 16
+AK_FWD, AK_DX, AK_DW, AK_WHASH, AK_DXHASH, AK_GAPP = 1, 2, 4, 8, 16, 32
 
 
 class StageVerifier:
