@@ -40,7 +40,7 @@ def _engine(nodes, attack=None, targets=(), start=6, **cfg):
         att = AdversarialAttacker(AttackConfig(attack_types=[attack], target_nodes=list(targets), intensity=0.5,
                                                start_step=start, probability=1.0, seed=3))
         att.activate_attacks()
-    m = get_model("gpt2-tiny", seq_len=32, seed=1)
+    m = get_model("gpt2-tiny", seq_len=32, seed=1, vocab_size=1024)
     return PipelineEngine(m, EngineConfig(num_nodes=nodes, micro_batches=2, device="cpu", seq_len=32, reassign=False,
                                           monitor_seed=0, **cfg), attacker=att)
 

@@ -44,7 +44,7 @@ def _engine(nodes, attack=None, targets=(), start=6, micro=2, atk_kw=None, **cfg
                                                start_step=start, probability=1.0, seed=3, **(atk_kw or {})))
         att.activate_attacks()
     cfg.setdefault("reassign", False)
-    m = get_model("gpt2-tiny", seq_len=32, seed=1)
+    m = get_model("gpt2-tiny", seq_len=32, seed=1, vocab_size=1024)
     return PipelineEngine(m, EngineConfig(num_nodes=nodes, micro_batches=micro, device="cpu", seq_len=32,
                                           monitor_seed=0, **cfg), attacker=att)
 
@@ -288,6 +288,7 @@ def _worker8(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.slow
 def test_eight_rank_backward_audit_reshard_agree():
     """8 gloo ranks, audit (forward + backward) on, shadows every 2 steps: a Byzantine-backward
     stage is caught at its first tampered step, every rank blames the same node and takes the same

@@ -72,7 +72,8 @@ def _worker(rank, world, port, model_name, steps, micro, out_path, p2p_mode="asy
 @pytest.mark.parametrize("model_name,micro,world,p2p,gran", [
     ("resnet32", 2, 2, "async", "auto"), pytest.param("gpt2-tiny", 4, 2, "async", "auto", marks=pytest.mark.slow),
     ("gpt2-tiny", 4, 2, "grouped", "auto"),
-    pytest.param("gpt2-tiny", 2, 4, "async", "auto", marks=pytest.mark.slow), ("gpt2-tiny", 8, 4, "async", "auto"),
+    pytest.param("gpt2-tiny", 2, 4, "async", "auto", marks=pytest.mark.slow),
+    pytest.param("gpt2-tiny", 8, 4, "async", "auto", marks=pytest.mark.slow),
     ("gpt2-tiny", 4, 4, "async", "half")])  # stage boundaries inside blocks, one process per stage
 def test_pipeline_matches_single_process(model_name, micro, world, p2p, gran, monkeypatch):
     steps = 4
@@ -214,6 +215,7 @@ def _replan_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.slow
 def test_replans_reuse_process_groups():
     """Re-plans do not leak communicators: groups are cached by member set, so re-planning onto a
     member set seen before creates nothing; each rank's communicator and stream counts stay bounded

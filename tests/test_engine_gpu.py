@@ -123,9 +123,9 @@ def test_fused_wgrad_reduce_stats_engine(monkeypatch):
     l0, d0, w0, calls0 = _run_big(monkeypatch, "0")
     assert calls0 == [] and len(calls1) >= 3 * 4 * 4, calls1      # every block weight, every step
     assert l0 == pytest.approx(l1, rel=1e-5)
-    # statistics part of the digest (the weight-commitment hash slots differ with any last bit)
-    from trustworthy_dl.security.stage_verifier import D_GSK_APP
-    d0, d1 = d0[:D_GSK_APP], d1[:D_GSK_APP]
+    # statistics part of the digest (the audit / hash slots after it differ with any last bit)
+    from trustworthy_dl.security.stage_verifier import D_AUDIT_KIND_PREV
+    d0, d1 = d0[:D_AUDIT_KIND_PREV], d1[:D_AUDIT_KIND_PREV]
     assert torch.allclose(d0, d1, rtol=1e-3, atol=1e-3), (d0 - d1).abs().max()
     # (weights are not compared: AdamW's first steps turn the run-order last bits of near-zero
     # gradient elements into +-lr updates)

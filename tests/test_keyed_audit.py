@@ -24,7 +24,7 @@ def _engine(nodes, targets=(1,), start=4, micro=4, atk_kw=None, **cfg):
     att.activate_attacks()
     cfg.setdefault("reassign", False)
     cfg.setdefault("audit_targeted", False)
-    m = get_model("gpt2-tiny", seq_len=32, seed=1)
+    m = get_model("gpt2-tiny", seq_len=32, seed=1, vocab_size=1024)
     return PipelineEngine(m, EngineConfig(num_nodes=nodes, micro_batches=micro, device="cpu", seq_len=32,
                                           monitor_seed=0, **cfg), attacker=att), att
 
@@ -118,7 +118,7 @@ def test_local_clean_run_no_false_keyed_flags():
     """No attack: the keyed recompute and the exact applied hash never flag a clean stage, k = M."""
     from trustworthy_dl.models import get_model
     from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
-    m = get_model("gpt2-tiny", seq_len=32, seed=1)
+    m = get_model("gpt2-tiny", seq_len=32, seed=1, vocab_size=1024)
     eng = PipelineEngine(m, EngineConfig(num_nodes=3, micro_batches=4, device="cpu", seq_len=32, monitor_seed=0,
                                          reassign=False, audit_micro_k=4))
     for b in _batches(6):

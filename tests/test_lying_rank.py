@@ -202,6 +202,7 @@ def test_gloo_lying_rank_caught(kind, target):
         assert set(lied) <= steps, got
 
 
+@pytest.mark.slow
 def test_gloo_lying_rank_one_of_m():
     """k = 1 of M = 4: lie_answer is caught only when its lied micro-batch is opened (~1/4 of the
     steps) — never a clean rank; the mirrors keep every stage's weights bit-identical."""

@@ -106,6 +106,7 @@ def test_resume_4_ranks_into_3():
     assert r0["detector_after_load"]["true_negatives"] == ref["detector_at_save"]["true_negatives"]
 
 
+@pytest.mark.slow
 def test_local_resume_4_into_3_and_missing_shard(tmp_path):
     from trustworthy_dl.utils.checkpoint import consolidate
     batches = _batches(4)
