@@ -43,11 +43,24 @@ def run(variant, args):
     for i in range(args.warmup):
         eng.train_step(batches[i % 2])
     torch.cuda.synchronize()
+    prof = None
+    if args.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for i in range(args.steps):
         eng.train_step(batches[i % 2])
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / args.steps
+    if prof is not None:
+        prof.disable()
+        import io
+        import pstats
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(45)
+        with open(f"{args.cprofile}.{variant}.txt", "w") as f:
+            f.write(buf.getvalue())
     eng.flush()
     rec = {"variant": variant, "ms_per_step": round(ms, 2), "tokens_per_s": round(args.batch * args.seq / ms * 1e3, 1),
            "model": args.model, "stages": args.stages, "micro_batches": args.micro, "batch": args.batch,
@@ -72,15 +85,32 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="off,fwd,mirror")
     ap.add_argument("--out", default="gpurun_out/r6_audit_overhead.jsonl")
+    ap.add_argument("--round-id", type=int, default=0)
+    ap.add_argument("--cprofile", default="", help="write a host cProfile of the timed steps to <path>.<variant>.txt")
+    ap.add_argument("--inproc", action="store_true", help="run in this process (default: one process per run)")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    with open(args.out, "a") as f:
+    variants = args.variants.split(",")
+    if not args.inproc and (len(variants) > 1 or args.rounds > 1):
+        # every (round, variant) in a fresh process: engines of 35 GB of rings + mirrors do not share
+        # one allocator's fragmentation, and no run inherits another's warm caches
+        import subprocess
         for r in range(args.rounds):
-            for v in args.variants.split(","):
-                rec = run(v, args)
-                rec["round"] = r
-                print(json.dumps(rec), flush=True)
-                f.write(json.dumps(rec) + "\n")
+            for v in variants:
+                cmd = [sys.executable, os.path.abspath(__file__), "--inproc", "--variants", v, "--rounds", "1",
+                       "--round-id", str(r), "--model", args.model, "--stages", str(args.stages),
+                       "--micro", str(args.micro), "--batch", str(args.batch), "--seq", str(args.seq),
+                       "--k", str(args.k), "--steps", str(args.steps), "--warmup", str(args.warmup), "--out", args.out]
+                rc = subprocess.run(cmd).returncode
+                if rc != 0:
+                    sys.exit(rc)
+        return
+    with open(args.out, "a") as f:
+        for v in variants:
+            rec = run(v, args)
+            rec["round"] = args.round_id
+            print(json.dumps(rec), flush=True)
+            f.write(json.dumps(rec) + "\n")
 
 
 if __name__ == "__main__":

@@ -116,22 +116,27 @@ def num_cus(device=None) -> int:
 
 def wgrad_split(K: int, M: int, N: int, num_cu: Optional[int] = None) -> int:
     """Split of the reduction depth K of an fp32 product [M, K] @ [K, N] (a weight gradient: K =
-    tokens) for the persistent kernel: the (tiles x slices) work items should fill the CUs in whole
-    rounds (the slices of a round finish together), each slice at least 16 K steps deep; among
-    equally full choices the smallest split (least slab traffic).  At 64k tokens on 256 CUs:
-    qkv 16, out-proj 16, fc / proj 4, tied LM head 8 (profiles/r3_gemm_lab.jsonl)."""
+    tokens) for the persistent kernel, from a cost model fitted to a sweep of every GPT-2-medium
+    product at K = 4k / 16k / 64k tokens (profiles/r6_wgrad_split_sweep.jsonl, it picks the measured
+    best split in all 12 cases):
+
+        T(S) = rounds(S) x (K / S / 64 K steps x 1.5 us + 5 us) + [S > 1] S x M x N x 8 B / 5 TB/s
+
+    (work items = tiles x S over the CUs in whole rounds; a split of S > 1 writes and re-reads S fp32
+    slabs).  The occupancy-first rule it replaces took 16 slices for qkv at 16k tokens (the MP = 8
+    micro-batch), 30 % slower than 4 there."""
     if os.environ.get("TDL_WGRAD_SPLITK", "1") == "0":
         return 1
     cu = num_cu or num_cus()
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
-    best, best_eff = 1, -1.0
+    best, best_t = 1, float("inf")
     for s in (1, 2, 4, 8, 16):
-        if s > 1 and (K // s < 16 * BK or effective_split(K, s) != s):
+        if s > 1 and effective_split(K, s) != s:
             continue
-        items = tiles * s
-        eff = items / (-(-items // cu) * cu)
-        if eff > best_eff + 1e-3:
-            best, best_eff = s, eff
+        rounds = -(-(tiles * s) // cu)
+        t = rounds * ((K // s // BK) * 1.5 + 5.0) + (s * M * N * 8 / 5e6 if s > 1 else 0.0)
+        if t < best_t - 1e-9:
+            best, best_t = s, t
     return best
 
 

@@ -162,6 +162,7 @@ class AuditMixin:
         from ..ops.layers import bump_weight_generation
         bump_weight_generation()
         mir._seed_epoch = self._mirror_epoch
+        mir._master_root = None
         self._audit_cost["seeds"] += 1
 
     def _skip_decision(self, D: torch.Tensor, evidence: torch.Tensor, node: int) -> torch.Tensor:
@@ -187,7 +188,37 @@ class AuditMixin:
                 mir.flat.adamw_step(self.cfg.adamw, ctrl=ctrl, zero_grad=False)
             finally:
                 mir.flat.set_grad_buffer(saved)
+            self._mirror_root_async(mir)
         self._mirror_pending = []
+
+    def _mirror_root_async(self, mir: Stage):
+        """Root of the mirror's master weights for the next step's weight check, taken on a side
+        stream right after its update (overlaps the next step's forward)."""
+        from ..security.grad_audit import merkle_roots
+        f = mir.flat
+        root = torch.empty(1, 8, dtype=torch.int32, device=f.device)
+        if not f.master.is_cuda:
+            mir._master_root = merkle_roots(f.master, [(0, f.numel)], out=root)[0]
+            return
+        key = str(f.device)
+        side = self._audit_side.get(key)
+        if side is None:
+            side = self._audit_side[key] = torch.cuda.Stream(f.device)
+        side.wait_stream(torch.cuda.current_stream(f.device))
+        with torch.cuda.stream(side):
+            merkle_roots(f.master, [(0, f.numel)], out=root)
+        mir._master_root = root[0]
+        mir._master_root_stream = side
+
+    def _mirror_master_root(self, mir: Stage) -> torch.Tensor:
+        from ..security.grad_audit import merkle_root
+        r = getattr(mir, "_master_root", None)
+        if r is None:
+            return merkle_root(mir.flat.master)
+        side = getattr(mir, "_master_root_stream", None)
+        if side is not None:
+            torch.cuda.current_stream(mir.device).wait_stream(side)
+        return r
 
     # ================================================================== checks
     def _audit_verdict(self, y_seen: torch.Tensor, y_ref: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -264,7 +295,7 @@ class AuditMixin:
         scale = torch.maximum(sg.abs().amax(), 0.25 * nrm).clamp_min(1e-30)
         e = torch.nan_to_num((sg - ssum).abs().amax() / scale, nan=1e30, posinf=1e30).reshape(1)
         abad = torch.maximum(gbad, (e > self.audit_sum_tol).float())
-        wbad = roots_differ(merkle_root(mir.flat.master), C[M + 1])
+        wbad = roots_differ(self._mirror_master_root(mir), C[M + 1])
         return abad * SV.AK_GAPP + wbad * SV.AK_WHASH, e
 
     @staticmethod
@@ -386,6 +417,7 @@ class AuditMixin:
         ops = [dist.P2POp(dist.isend, t, r, g) for t, r in sends] + [dist.P2POp(dist.irecv, t, r, g) for t, r in recvs]
         a = self._audit_cost
         a["bytes"] += sum(t.numel() * t.element_size() for t, _ in sends + recvs)
+        a["sent"] += sum(t.numel() * t.element_size() for t, _ in sends)
         self._early_ship = (dist.batch_isend_irecv(ops), mirrors)
 
     # ================================================================== accounting
@@ -400,15 +432,17 @@ class AuditMixin:
 
     def audit_summary(self) -> Dict[str, float]:
         """Per-step cost of the audit protocol on this rank (call after a device sync): P2P bytes
-        it sent + received (applied gradients, opened contributions, inputs, input gradients; the
-        one-off mirror seeds), host wall time of the audit phase, device time between its first and
-        last kernel (HIP events), device memory it holds (contribution rings + mirrors)."""
+        it sent + received and sent alone per step (applied gradient, opened contributions, inputs,
+        input gradients), without the one-off mirror seeds (``seed_bytes`` received in total), host
+        wall time of the audit phase, device time between its first and last kernel (HIP events),
+        device memory it holds (contribution rings + mirrors)."""
         a = self._audit_cost
         tl = self._target_log
         if not a or not a["steps"]:
             return {"steps": 0, "targeted_extra": len(tl)}
         gpu = [e0.elapsed_time(e1) for e0, e1 in a["events"] if e1.query()]
         return {"steps": a["steps"], "bytes_per_step": a["bytes"] / a["steps"],
+                "sent_bytes_per_step": a["sent"] / a["steps"],
                 "seed_bytes": a["seed_bytes"], "mirror_seeds": a["seeds"],
                 "host_ms_per_step": 1e3 * a["host_s"] / a["steps"],
                 "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None,
@@ -424,6 +458,7 @@ class AuditMixin:
         bwd_r = [(t, r) for t, r in recvs if r == nxt]
         a = self._audit_cost
         a["bytes"] += sum(t.numel() * t.element_size() for t, _ in list(sends) + list(recvs))
+        a["sent"] += sum(t.numel() * t.element_size() for t, _ in sends)
         for ss, rr, g in ((fwd_s, fwd_r, act_g), (bwd_s, bwd_r, grad_g)):
             self._note_peers(ss, rr, "dir" if g is not None else "default")
             batched_transfer(ss, rr, group=g)

@@ -96,21 +96,20 @@ class DistAuditMixin:
         a_cost = self._audit_cost
 
         # ---- 1. commit (auditee): roots through the store, the applied gradient over P2P
-        p2p_ops = []
+        p2p_ops, seed_ops = [], []
         if mirror and my_auditor is not None:
             C = self._contrib_commitments(me, st)
             G = self._applied_gradient(me, st)
             run = self._gsk_run.get(me) if self._targeted else None
             mark = (self.plan.version, tuple(st.layer_range), self._mirror_epoch)
-            seed_state = self._seed_mark != mark
             note_host_sync()
             payload = {"C": C.cpu().tolist(), "step_count": st.flat.step_count,
                        "run": run.cpu().tolist() if run is not None else None}
             store.set(f"{tag}/com/{me}", _enc_json(payload))
             p2p_ops.append(("send", G.contiguous(), my_auditor))
-            if seed_state:
+            if self._seed_mark != mark:
                 master, m1, m2, _ = self._optimizer_state(me, st)
-                p2p_ops += [("send", t.contiguous(), my_auditor) for t in (master, m1, m2)]
+                seed_ops += [("send", t.contiguous(), my_auditor) for t in (master, m1, m2)]
                 self._seed_mark = mark
         seeding: Dict[int, bool] = {}
         if mirror:
@@ -122,15 +121,19 @@ class DistAuditMixin:
                 p2p_ops.append(("recv", g_in, p))
                 seeding[p] = not self._mirror_seeded(mir)
                 if seeding[p]:
-                    p2p_ops += [("recv", t, p) for t in (mir.flat.master, mir.flat.exp_avg, mir.flat.exp_avg_sq)]
+                    seed_ops += [("recv", t, p) for t in (mir.flat.master, mir.flat.exp_avg, mir.flat.exp_avg_sq)]
         work = None
-        if p2p_ops:
+        if p2p_ops or seed_ops:
             g = self._audit_pg
-            ops = [dist.P2POp(dist.isend if k == "send" else dist.irecv, t, r, g) for k, t, r in p2p_ops]
-            nb = sum(t.numel() * t.element_size() for _, t, _ in p2p_ops)
-            a_cost["bytes"] += nb
-            self._note_peers([(t, r) for k, t, r in p2p_ops if k == "send"],
-                             [(t, r) for k, t, r in p2p_ops if k == "recv"], "audit")
+            allops = p2p_ops + seed_ops
+            ops = [dist.P2POp(dist.isend if k == "send" else dist.irecv, t, r, g) for k, t, r in allops]
+            nbytes = lambda lst, kind=None: sum(t.numel() * t.element_size() for k, t, _ in lst  # noqa: E731
+                                                if kind is None or k == kind)
+            a_cost["bytes"] += nbytes(p2p_ops)
+            a_cost["sent"] += nbytes(p2p_ops, "send")
+            a_cost["seed_bytes"] += nbytes(seed_ops, "recv")
+            self._note_peers([(t, r) for k, t, r in allops if k == "send"],
+                             [(t, r) for k, t, r in allops if k == "recv"], "audit")
             work = dist.batch_isend_irecv(ops)
 
         # ---- 2. key (auditor): only after the commitments were read
@@ -270,7 +273,6 @@ class DistAuditMixin:
             C = s_p = key = None
             if mirror:
                 if seeding[p]:
-                    a_cost["seed_bytes"] += 3 * mir.flat.numel * 4
                     self._seed_mirror(mir, None, None, None, int(got[p].get("step_count", 0)))
                 C = self._as_tensor(got[p]["C"], torch.int32)
                 s_p, key = sketches[p], keys[p]

@@ -136,6 +136,7 @@ class CommitmentMixin:
         self._gsk_on = bool(self.cfg.audit and self.cfg.audit_backward and self.plan.num_stages > 1 and self.dp == 1)
         self._gring: Dict[int, torch.Tensor] = {}
         self._gprev: Dict[int, torch.Tensor] = {}
+        self._gcom: Dict[int, torch.Tensor] = {}
         self._gsk_run: Dict[int, torch.Tensor] = {}
         self._tsk_pre: Dict[int, torch.Tensor] = {}
         self._mirror_pending = []
@@ -147,6 +148,8 @@ class CommitmentMixin:
             ring, prev = self._ring_buffers(node, st, M)
             prev.copy_(st.flat.grad)
             self._gring[node], self._gprev[node] = ring, prev
+            # [M + 2, 8] roots: filled as the step goes (contributions, master), the applied gradient last
+            self._gcom[node] = torch.empty(M + 2, 8, dtype=torch.int32, device=st.device)
             if self._targeted:
                 sk = self._sketch_for(st)
                 r = torch.zeros(M + 1, 2, dtype=torch.float32, device=st.device)
@@ -164,10 +167,43 @@ class CommitmentMixin:
         ring = self._gring.get(node)
         if ring is not None:
             contrib_snap(st.flat.grad, self._gprev[node], ring[i])
+            # its commitment on the verifier's side stream, overlapping the next micro-batch's compute
+            self._on_side(st, lambda: self._root_into(ring[i], self._commit_segments(st), self._gcom[node][i:i + 1]))
         r = self._gsk_run.get(node)
         if r is not None:
             sk = self._sketch_for(st)
             r[i + 1].copy_(sk(st.flat.grad, sk.offset(self.cfg.seed, self.global_step)))
+
+    def _commit_master(self, node: int, st: Stage):
+        """The root of the master weights this step runs with (taken once its weights are final for
+        the step, ScheduleMixin._attack_params), on the side stream, overlapped with the forward."""
+        com = self._gcom.get(node) if self._gsk_on else None
+        if com is not None:
+            M = com.shape[0] - 2
+            self._on_side(st, lambda: self._root_into(st.flat.master, [(0, st.flat.numel)], com[M + 1:M + 2]))
+
+    @staticmethod
+    def _root_into(x: torch.Tensor, segs, out: torch.Tensor):
+        from ..security.grad_audit import merkle_roots
+        merkle_roots(x, segs, out=out)
+
+    @staticmethod
+    def _on_side(st: Stage, fn):
+        """Run ``fn`` (device work reading tensors the compute stream has written) on the stage's
+        verification side stream after the compute stream's work so far; CPU / serialized: inline."""
+        side = getattr(st.verifier, "side", None)
+        if side is None or not st.flat.grad.is_cuda:
+            fn()
+            return
+        cur = torch.cuda.current_stream(st.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            fn()
+
+    def _join_side(self, st: Stage):
+        side = getattr(st.verifier, "side", None)
+        if side is not None and st.flat.grad.is_cuda:
+            torch.cuda.current_stream(st.device).wait_stream(side)
 
     # ------------------------------------------------------------------ auditee answers (overridable)
     def _applied_gradient(self, node: int, st: Stage) -> torch.Tensor:
@@ -178,14 +214,11 @@ class CommitmentMixin:
     def _contrib_commitments(self, node: int, st: Stage) -> torch.Tensor:
         """[M + 2, 8] int32 roots: the M contributions, the applied gradient, the fp32 master
         weights (before this step's update = after the previous one)."""
-        from ..security.grad_audit import merkle_root, merkle_roots
-        segs = self._commit_segments(st)
-        ring = self._gring[node]
-        M, n = ring.shape
-        C = torch.empty(M + 2, 8, dtype=torch.int32, device=st.device)
-        C[:M].copy_(merkle_roots(ring, segs, batch=M, stride=n))
-        C[M].copy_(merkle_root(self._applied_gradient(node, st), segs))
-        C[M + 1].copy_(merkle_root(st.flat.master))
+        from ..security.grad_audit import merkle_root
+        self._join_side(st)      # the contributions' and the master's roots were taken on the side stream
+        C = self._gcom[node].clone()
+        M = C.shape[0] - 2
+        C[M].copy_(merkle_root(self._applied_gradient(node, st), self._commit_segments(st)))
         return C
 
     @torch.no_grad()

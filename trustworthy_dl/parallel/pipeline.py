@@ -170,7 +170,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._audit_outputs: Dict[int, torch.Tensor] = {}
         self._early_ship = None                  # (P2P works, mirrors) of the early weight shipment
         self._audit_rng = None                   # distributed auditor's private RNG (audit_dist.py)
-        self._audit_cost = {"steps": 0, "host_s": 0.0, "bytes": 0, "events": [], "seeds": 0, "seed_bytes": 0}
+        self._audit_cost = {"steps": 0, "host_s": 0.0, "bytes": 0, "sent": 0, "events": [], "seeds": 0,
+                            "seed_bytes": 0}
         self._target_log: List[Tuple[int, int, int]] = []
         self._mirrors: Dict[Tuple[int, Tuple[int, int]], Stage] = {}
         # gradient commitments (commitments.py) and optimizer mirrors (audit.py)
@@ -178,6 +179,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._gsk_run: Dict[int, torch.Tensor] = {}      # public running sketches (targeting)
         self._gring: Dict[int, torch.Tensor] = {}        # [M, n] per-micro-batch contributions
         self._gprev: Dict[int, torch.Tensor] = {}        # [n] running gradient before the next one
+        self._gcom: Dict[int, torch.Tensor] = {}         # [M + 2, 8] roots: contributions, applied, master
+        self._audit_side: Dict[str, object] = {}         # per device: stream of the mirrors' weight roots
         self._gring_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._mirror_epoch = 0                           # bumped on every rank when mirrors go stale
         self._mirror_pending: List = []                  # (mirror, verified gradient, node) to apply
@@ -460,7 +463,7 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         n_comms = (1 if self.distributed else 0) + len(mine) + n_p2p
         from ..ops.side_stream import WgradSide
         # compute + verification side streams + weight-gradient side streams + RCCL streams
-        streams = 1 + len(self.stages) + WgradSide.count() + n_comms
+        streams = 1 + len(self.stages) + WgradSide.count() + len(self._audit_side) + n_comms
         from ..runtime.hwqueues import effective_hw_queues
         q = effective_hw_queues() if self.device.type == "cuda" else None
         return {"groups_created": len(groups), "groups_member": len(mine), "p2p_peers": p2p,

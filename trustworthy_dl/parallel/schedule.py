@@ -43,6 +43,7 @@ class ScheduleMixin:
         if self.attacker is not None and hasattr(self.attacker, "on_parameters"):
             if self.attacker.on_parameters(node, st.flat, self.global_step):
                 truth[node] = True
+        self._commit_master(node, st)   # the weights this step runs with (side stream)
         # the stage's weights are final for this step from here on: take the integrity checksum now,
         # on the verifier's side stream, overlapped with the forward / backward instead of serially
         # on the step's tail (_integrity_flag picks it up after finish_step joined the side stream)

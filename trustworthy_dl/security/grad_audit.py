@@ -117,22 +117,30 @@ def _merkle_host(flat: torch.Tensor, segs, batch: int, stride: int) -> torch.Ten
 
 @torch.no_grad()
 def merkle_roots(x: torch.Tensor, segments: Sequence[Tuple[int, int]], batch: int = 1,
-                 stride: Optional[int] = None) -> torch.Tensor:
+                 stride: Optional[int] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[batch, 8] int32 (raw uint32 bits) BLAKE2s Merkle roots of the 32-bit words of
-    ``x.reshape(-1)[y * stride + lo : y * stride + hi]`` over ``segments``, y < batch.  Device
-    tensors stay on the device (no host sync); identical bits on CPU and GPU."""
+    ``x.reshape(-1)[y * stride + lo : y * stride + hi]`` over ``segments``, y < batch (written into
+    ``out`` when given: contiguous [batch, 8] int32).  Device tensors stay on the device (no host
+    sync; runs on the current stream); identical bits on CPU and GPU."""
     flat = x.reshape(-1)
     if flat.element_size() != 4:
         raise ValueError("merkle_roots hashes 32-bit words")
     stride = int(stride if stride is not None else 0)
     segs = [(int(lo), int(hi)) for lo, hi in segments if hi > lo]
     if not flat.is_cuda:
-        return _merkle_host(flat, segs, batch, stride)
+        r = _merkle_host(flat, segs, batch, stride)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
     from ..ops import _lib
     from ..ops._lib import ptr, stream_ptr
     dev = flat.device
     sp = stream_ptr(dev)
-    final = torch.empty(batch, DIGEST_WORDS, dtype=torch.int32, device=dev)
+    if out is not None and (not out.is_contiguous() or tuple(out.shape) != (batch, DIGEST_WORDS)
+                            or out.dtype != torch.int32 or out.device != dev):
+        raise ValueError("out must be a contiguous [batch, 8] int32 tensor on the input's device")
+    final = out if out is not None else torch.empty(batch, DIGEST_WORDS, dtype=torch.int32, device=dev)
     if not segs:
         final.copy_(_root_bytes_to_tensor(_combine_cpu([])).expand(batch, -1))
         return final
