@@ -136,6 +136,22 @@ def test_local_lying_rank_caught(kind):
         assert all(k == "gradient_poisoning" for _, _, k in got), got
 
 
+def test_local_lying_sumsq_does_not_move_the_clip():
+    """A stage that reports a huge gradient sum of squares would shrink every stage's update through
+    the global clip scale; in mirror mode the clip uses the sums its auditor computed from the
+    shipped gradient, so training is bit-identical to the clean run."""
+    clean = _make(3, None, micro=2, k=2)
+    liar = _make(3, "lie_sumsq", target=1, start=1, micro=2, k=2)
+    for b in _batches(3):
+        clean.train_step(b)
+        liar.train_step(b)
+    clean.flush()
+    liar.flush()
+    assert liar.lied_steps == [1, 2, 3]
+    for n in clean.stages:
+        assert torch.equal(clean.stages[n].flat.master, liar.stages[n].flat.master), n
+
+
 def test_local_clean_run_no_blame_with_mirrors():
     """Clean: commitments, sums, openings, mirror weights all match for 6 steps (k = M)."""
     eng = _make(3, None, micro=4, k=4)

@@ -17,6 +17,8 @@ scripts/lying_rank.py) or, in local mode, for its own node only.
 * ``hash_forge``   applies and ships a sign-flipped gradient with r5's mix32 second-preimage
   fix-up, and commits the honest gradient's root in its place: a collision of the BLAKE2s Merkle
   root would be needed.  Caught every step (root of the shipped gradient != commitment).
+* ``lie_sumsq``     reports a huge gradient sum of squares in its digest row (every stage's updates
+  would be clipped to nothing).  Harmless: the global clip uses the sums its auditor computed.
 
 Ground truth: ``lied_steps`` lists the steps where the rank applied something else than the honest
 gradient.  Reference: the optimizer step trusts every node (distributed_trainer.py:441-446).
@@ -28,7 +30,7 @@ from typing import List, Optional
 
 import torch
 
-ATTACKS = ("lie_applied", "lie_answer", "hash_forge")
+ATTACKS = ("lie_applied", "lie_answer", "hash_forge", "lie_sumsq")
 
 
 def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 0):
@@ -64,7 +66,7 @@ def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 
             self._lie_init()
             self._honest_g = None
             self._lie_j = -1
-            if not self._lying_now(node):
+            if not self._lying_now(node) or kind == "lie_sumsq":
                 return super()._contrib_commitments(node, st)
             if kind == "lie_applied":
                 self._honest_g = st.flat.grad.clone()            # shipped + committed
@@ -86,6 +88,13 @@ def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 
             C = super()._contrib_commitments(node, st)
             C[C.shape[0] - 2].copy_(honest_root.to(C.device))
             return C
+
+        def _write_commitments(self, node, st, d):
+            super()._write_commitments(node, st, d)
+            if kind == "lie_sumsq" and self._lying_now(node):
+                from ..security import stage_verifier as SV
+                d[SV.D_GRAD_SUMSQ:SV.D_GRAD_SUMSQ + 1].fill_(1e12)
+                self.lied_steps.append(self.global_step)
 
         def _applied_gradient(self, node, st):
             if self._lying_now(node) and kind == "lie_applied" and self._honest_g is not None:

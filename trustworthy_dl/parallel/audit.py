@@ -134,9 +134,41 @@ class AuditMixin:
             for k in [k for k in cache if k[0] != self.plan.version]:
                 del cache[k]
             # (its gradient-folding hooks stay: the backward audit recomputes weight gradients on it)
-            cache[key] = Stage(self.model, rng, sid, self.plan.num_stages, device or self.device, self.dtype,
-                               {"output_detection": False, "gradient_verification": False, "serialize_streams": True})
+            mir = cache[key] = Stage(self.model, rng, sid, self.plan.num_stages, device or self.device, self.dtype,
+                                     {"output_detection": False, "gradient_verification": False,
+                                      "serialize_streams": True})
+            mir.set_clip_exclusions(self._clip_excluded_ids(mir))   # the auditor computes its clip sum
         return cache[key]
+
+    def _clip_excluded_ids(self, st: Stage):
+        """Parameters of ``st`` another stage counts in the global clipping norm: members of a tie
+        group whose first member lives outside ``st``'s layer range."""
+        a, b = st.layer_range
+        ex = set()
+        for grp in self.ties:
+            if a <= grp[0][0] < b:
+                continue
+            for li, attr in grp:
+                prm = st.local_param(li, attr)
+                if prm is not None:
+                    ex.add(id(prm))
+        return ex
+
+    def _clip_sumsq_audited(self, D: torch.Tensor) -> torch.Tensor:
+        """Mirror mode: per node, the clipping sum of squares its AUDITOR computed from the gradient
+        it shipped (``D_SUMSQ_*`` of the auditor's row), zero where the node's own update is
+        quarantined — the global clip scale takes no stage's word for its own gradient norm."""
+        sq = torch.zeros(D.shape[0], dtype=torch.float32, device=D.device)
+        for idx in self._replica_orders():
+            n = idx.numel()
+            if n < 2:
+                continue
+            sq[idx[:-1]] = D[idx[1:], SV.D_SUMSQ_PREV]
+            sq[idx[-1:]] = D[idx[-2:-1], SV.D_SUMSQ_NEXT]
+        q = torch.maximum((D[:, SV.D_GRAD_FLAG] > 0).float(), (D[:, SV.D_NONFINITE] > 0).float()) \
+            if self.cfg.quarantine else torch.zeros_like(sq)
+        sq = torch.where((q > 0) | ~torch.isfinite(sq), torch.zeros_like(sq), sq.clamp_min(0.0))
+        return sq
 
     def _invalidate_mirrors(self):
         """Every rank, at the same step: the mirrors' state no longer follows their stages (a step
@@ -367,6 +399,8 @@ class AuditMixin:
                 res = ((kd > 0).float(), kd, e)
                 self._mirror_pending.append((mir, G, p))
                 rows[aud][SV.D_MIRROR:SV.D_MIRROR + 1].fill_(1.0)
+                slot = SV.D_SUMSQ_NEXT if last else SV.D_SUMSQ_PREV
+                rows[aud][slot:slot + 1].copy_(mir.clip_sumsq(G).reshape(1).to(rows[aud].device))
             else:
                 if not chosen:
                     continue
@@ -499,7 +533,8 @@ class AuditMixin:
                         differ(D[up, SV.D_XHASH_SENT:SV.D_XHASH_SENT + R], D[au, SV.D_XHASH_SHIP:SV.D_XHASH_SHIP + R]))
                     kind[q] += bad * SV.AK_DXHASH
             if bwd:
-                L, A = idx[-1], idx[-2]
+                # 1-element index tensors: a 0-d device tensor as an index is read back to the host
+                L, A = idx[-1:], idx[-2:-1]
                 kind[L] = D[A, SV.D_AUDIT_KIND_NEXT]
                 done[L] = D[A, SV.D_AUDITED_NEXT]
                 if self.distributed:

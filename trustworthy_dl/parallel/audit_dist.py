@@ -285,6 +285,8 @@ class DistAuditMixin:
                     res = ((kd > 0).float(), kd, e)
                 self._mirror_pending.append((mir, mir._g_in, p))
                 d[SV.D_MIRROR:SV.D_MIRROR + 1].fill_(1.0)
+                slot = SV.D_SUMSQ_NEXT if nxt_peer else SV.D_SUMSQ_PREV
+                d[slot:slot + 1].copy_(mir.clip_sumsq(mir._g_in).reshape(1))
             for j, m in enumerate(ms):
                 if nxt_peer:
                     labels = self._audit_targets[m].to(self.device, non_blocking=True)

@@ -167,8 +167,13 @@ class CommitmentMixin:
         ring = self._gring.get(node)
         if ring is not None:
             contrib_snap(st.flat.grad, self._gprev[node], ring[i])
-            # its commitment on the verifier's side stream, overlapping the next micro-batch's compute
-            self._on_side(st, lambda: self._root_into(ring[i], self._commit_segments(st), self._gcom[node][i:i + 1]))
+            if i == ring.shape[0] - 1:
+                # every contribution is in: their roots in ONE batched tree (a launch per level for
+                # all M) on the verifier's side stream, overlapping the rest of the step (per
+                # micro-batch trees cost ~5 latency-bound node launches each)
+                M, n = ring.shape
+                self._on_side(st, lambda: self._roots_into(ring, self._commit_segments(st), M, n,
+                                                           self._gcom[node][:M]))
         r = self._gsk_run.get(node)
         if r is not None:
             sk = self._sketch_for(st)
@@ -186,6 +191,11 @@ class CommitmentMixin:
     def _root_into(x: torch.Tensor, segs, out: torch.Tensor):
         from ..security.grad_audit import merkle_roots
         merkle_roots(x, segs, out=out)
+
+    @staticmethod
+    def _roots_into(x: torch.Tensor, segs, batch: int, stride: int, out: torch.Tensor):
+        from ..security.grad_audit import merkle_roots
+        merkle_roots(x, segs, batch=batch, stride=stride, out=out)
 
     @staticmethod
     def _on_side(st: Stage, fn):

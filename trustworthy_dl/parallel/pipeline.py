@@ -783,7 +783,7 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
             # global gradient norm for clipping: sum of the per-stage sumsq of the updates that will
             # be applied (each tied weight counted once, quarantined stages left out); every rank
             # computes it from the same all-gathered digest
-            sq = D[:, SV.D_GRAD_SUMSQ]
+            sq = self._clip_sumsq_audited(D) if self._gsk_on else D[:, SV.D_GRAD_SUMSQ]
             if self.quarantine_on_evidence:
                 sq = sq * (1.0 - evidence)
             total_sumsq = sq.sum()

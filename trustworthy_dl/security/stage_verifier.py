@@ -74,7 +74,10 @@ D_DXHASH_SHIP = 69   # [8] root of the input gradients the audited previous stag
 D_XHASH_SENT = 77    # [8] root of the outputs this stage SENT to the next stage for the micro-batches
                      #     that stage's auditor opened (= their inputs)
 D_XHASH_SHIP = 85    # [8] root of the inputs the audited previous stage shipped here
-DIGEST = 93          # csrc/stats.hip VD_DIGEST
+D_SUMSQ_PREV = 93    # (mirror mode) clipping sum of squares of the gradient the audited previous stage
+                     #     shipped here, computed by this auditor (-1: none); the global clip uses these
+D_SUMSQ_NEXT = 94    # same for the audited next (loss) stage
+DIGEST = 95          # csrc/stats.hip VD_DIGEST
 # audit check bits
 AK_FWD, AK_DX, AK_DW, AK_WHASH, AK_DXHASH, AK_GAPP = 1, 2, 4, 8, 16, 32
 
