@@ -256,7 +256,42 @@ __global__ __launch_bounds__(256) void contrib_snap_kernel(const float* __restri
     }
 }
 
+// out[0] = max |a - b|, out[1] = max |b| over [lo, hi) (fp32 bits of non-negative values compare as
+// unsigned integers; a NaN's bits exceed +inf's, so a NaN anywhere reads as the largest error).
+// out must be zeroed by the caller.  No temporaries (the torch form allocated two n-sized ones).
+__global__ __launch_bounds__(256) void absdiff_max_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         long long lo, long long hi, unsigned int* __restrict__ out) {
+    float d = 0.f, r = 0.f;
+    const long long step = (long long)gridDim.x * 256;
+    for (long long j = lo + (long long)blockIdx.x * 256 + threadIdx.x; j < hi; j += step) {
+        const float x = a[j], y = b[j];
+        const float e = fabsf(x - y), m = fabsf(y);
+        d = (e > d || e != e) ? e : d;
+        r = (m > r || m != m) ? m : r;
+    }
+    unsigned int ud = __float_as_uint(d), ur = __float_as_uint(r);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ud = max(ud, (unsigned int)__shfl_xor((int)ud, o, 64));
+        ur = max(ur, (unsigned int)__shfl_xor((int)ur, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(out, ud);
+        atomicMax(out + 1, ur);
+    }
+}
+
 }  // namespace
+
+// out (uint32[2], zeroed) = bits of (max |a - b|, max |b|) over [lo, hi)
+TDL_API int tdl_absdiff_max(const float* a, const float* b, long long lo, long long hi, unsigned int* out,
+                            hipStream_t s) {
+    if (hi <= lo) return 0;
+    long long nb = (hi - lo + 256 * 8 - 1) / (256 * 8);
+    if (nb > 2048) nb = 2048;
+    absdiff_max_kernel<<<(int)nb, 256, 0, s>>>(a, b, lo, hi, out);
+    TDL_LAUNCH_CHECK();
+}
 
 // ---- BLAKE2s Merkle levels (the Python side walks the tree: grad_audit.merkle_roots)
 TDL_API long long tdl_b2s_leaf_words() { return LEAF_WORDS; }

@@ -110,3 +110,19 @@ def test_gpu_local_protocol(kind):
             assert len(mir) == 1 and torch.equal(mir[0].flat.master, st.flat.master)
     else:
         assert blamed and {n for _, n in blamed} == {1}, blamed
+
+
+def test_seg_rel_err_matches_torch():
+    torch.manual_seed(3)
+    n = 2_000_003
+    a, b = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    segs = [(0, 1000), (5000, n)]
+    got = float(ga.seg_rel_err(a, b, segs))
+    keep = torch.zeros(n, dtype=torch.bool, device=DEV)
+    for lo, hi in segs:
+        keep[lo:hi] = True
+    want = float((a - b).abs()[keep].max() / b.abs()[keep].max())
+    assert got == pytest.approx(want, rel=1e-6)
+    a[7000] = float("nan")
+    assert float(ga.seg_rel_err(a, b, segs)) >= 1e29          # NaN reads as the largest error
+    assert float(ga.seg_sumsq(b, segs)) == pytest.approx(float(b[keep].double().square().sum()), rel=1e-4)

@@ -151,6 +151,7 @@ _SIGNATURES = {
     "tdl_keyed_sketch_ws_floats": [_L],
     "tdl_keyed_sketch": [_P, _L, _I, _P, _L, _L, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I, _P],
     "tdl_contrib_snap": [_P, _P, _P, _L, _P],
+    "tdl_absdiff_max": [_P, _P, _L, _L, _P, _P],
     # conv.hip / bn.hip
     "tdl_conv_nt": [_P] * 5 + [_I] * 12 + [_P],
     "tdl_conv_stats_ws_floats": [_I, _I],

@@ -264,11 +264,8 @@ class AuditMixin:
     @staticmethod
     def _seg_rel_err(a: torch.Tensor, ref: torch.Tensor, segs) -> torch.Tensor:
         """max |a - ref| / max |ref| over the segments (device scalar; non-finite -> 1e30)."""
-        if not segs:
-            return torch.zeros((), device=ref.device)
-        num = torch.stack([(a[lo:hi] - ref[lo:hi]).abs().amax() for lo, hi in segs]).amax()
-        den = torch.stack([ref[lo:hi].abs().amax() for lo, hi in segs]).amax().clamp_min(1e-30)
-        return torch.nan_to_num(num / den, nan=1e30, posinf=1e30)
+        from ..security.grad_audit import seg_rel_err
+        return seg_rel_err(a, ref, segs)
 
     def _audit_one(self, mir: Stage, x: torch.Tensor, m: int, M: int, y_seen=None, dy=None, labels=None,
                    dx_seen=None, c_m: Optional[torch.Tensor] = None, C: Optional[torch.Tensor] = None,
@@ -322,8 +319,8 @@ class AuditMixin:
         gbad = roots_differ(merkle_root(G, segs), C[M])
         sg = keyed_sketch(G, segs, key)
         ssum = s.to(dev).float().sum(0)
-        nrm = torch.stack([G[lo:hi].float().square().sum() for lo, hi in segs]).sum().sqrt() if segs \
-            else torch.zeros((), device=dev)
+        from ..security.grad_audit import seg_sumsq
+        nrm = seg_sumsq(G, segs).sqrt()
         scale = torch.maximum(sg.abs().amax(), 0.25 * nrm).clamp_min(1e-30)
         e = torch.nan_to_num((sg - ssum).abs().amax() / scale, nan=1e30, posinf=1e30).reshape(1)
         abad = torch.maximum(gbad, (e > self.audit_sum_tol).float())

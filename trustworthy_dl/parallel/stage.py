@@ -78,11 +78,8 @@ class Stage:
     def clip_sumsq(self, grad: torch.Tensor) -> torch.Tensor:
         """Sum of squares of ``grad`` (this stage's flat gradient) over the parameters this stage
         counts for clipping (device scalar)."""
-        sq = (grad * grad).sum()
-        for o, n in self.clip_excluded:
-            g = grad[o:o + n]
-            sq = sq - (g * g).sum()
-        return sq
+        from ..security.grad_audit import _segments, seg_sumsq
+        return seg_sumsq(grad, _segments(grad.numel(), [(o, o + n) for o, n in self.clip_excluded]))
 
     @staticmethod
     def _fold_grad(p: torch.Tensor):

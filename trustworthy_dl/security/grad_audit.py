@@ -232,6 +232,36 @@ def keyed_sketch(a: torch.Tensor, segments: Sequence[Tuple[int, int]], key: int,
 
 
 @torch.no_grad()
+def seg_rel_err(a: torch.Tensor, ref: torch.Tensor, segments) -> torch.Tensor:
+    """max |a - ref| / max |ref| over the segments (device scalar, no host sync, no n-sized
+    temporaries on the GPU; NaN / inf -> 1e30)."""
+    a, ref = a.reshape(-1), ref.reshape(-1)
+    if not segments:
+        return torch.zeros((), device=ref.device)
+    if a.is_cuda:
+        from ..ops import _lib
+        from ..ops._lib import ptr, stream_ptr
+        bits = torch.zeros(2, dtype=torch.int32, device=a.device)
+        for lo, hi in segments:
+            _lib.call("tdl_absdiff_max", ptr(a), ptr(ref), int(lo), int(hi), ptr(bits), stream_ptr(a.device))
+        v = bits.view(torch.float32)
+        num, den = v[0], v[1].clamp_min(1e-30)
+    else:
+        num = torch.stack([(a[lo:hi] - ref[lo:hi]).abs().amax() for lo, hi in segments]).amax()
+        den = torch.stack([ref[lo:hi].abs().amax() for lo, hi in segments]).amax().clamp_min(1e-30)
+    return torch.nan_to_num(num / den, nan=1e30, posinf=1e30)
+
+
+@torch.no_grad()
+def seg_sumsq(x: torch.Tensor, segments) -> torch.Tensor:
+    """sum of squares over the segments (device scalar, no n-sized temporary)."""
+    x = x.reshape(-1)
+    if not segments:
+        return torch.zeros((), device=x.device)
+    return torch.stack([torch.linalg.vector_norm(x[lo:hi], 2).square() for lo, hi in segments]).sum()
+
+
+@torch.no_grad()
 def contrib_snap(g: torch.Tensor, prev: torch.Tensor, c: torch.Tensor) -> None:
     """c = g - prev; prev = g (one micro-batch's weight-gradient contribution, fp32)."""
     if g.is_cuda:
