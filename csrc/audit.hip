@@ -10,8 +10,10 @@
 //    up to one root per segment (at least one node level), then one combine over the segments'
 //    roots (node_depth = 255, last_node).  Bit-identical to Python's hashlib.blake2s with the same
 //    node parameters (the CPU path and the GPU tests use it as the oracle).  One thread per leaf /
-//    node: 16 compressions of 10 rounds each, integer VALU only; a batch dimension (grid.y) hashes
-//    the M per-micro-batch contributions of a step in one launch per tree level.
+//    node: 16 compressions of 10 rounds each, integer VALU only.  Two launches per segment: leaves
+//    + level 1 (each workgroup's 8 level-1 nodes from its 256 leaf digests in LDS), then the rest of
+//    the tree in one workgroup per batch entry (levels >= 3 in LDS); a batch dimension (grid.y)
+//    hashes the M per-micro-batch contributions of a step in the same two launches.
 //  * keyed sketch — K = 4 full-coverage random-sign projections sum_j s_k(key, j) a_j with the
 //    signs derived from a PRIVATE per-step key revealed only after the commitments were received;
 //    two-pass, fixed-order reduction (deterministic: the auditor recomputes the auditee's value
@@ -115,38 +117,123 @@ __device__ __forceinline__ void b2s_words(uint32_t* h, int nw, bool last_node, L
     }
 }
 
-// leaves: out[y][j] = leaf digest j of x[y * stride + lo : y * stride + hi)
+// leaves AND their level-1 parents in one launch: out[y][q] = level-1 node q (over leaves
+// [32 q, 32 q + 32)) of x[y * stride + lo : ... + hi); each 256-thread workgroup hashes 256 leaves
+// into LDS, then 8 of its threads hash the 8 level-1 nodes they form
 template <bool ALIGNED>
-__global__ __launch_bounds__(256) void b2s_leaf_kernel(const uint32_t* __restrict__ x, long long stride, long long lo,
-                                                      long long hi, long long nleaf, uint32_t* __restrict__ out,
-                                                      long long out_stride) {
+__global__ __launch_bounds__(256) void b2s_leaf_l1_kernel(const uint32_t* __restrict__ x, long long stride,
+                                                         long long lo, long long hi, long long nleaf,
+                                                         uint32_t* __restrict__ out, long long out_stride) {
+    __shared__ uint32_t dig[256 * 8];
     const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j >= nleaf) return;
-    const uint32_t* src = x + (long long)blockIdx.y * stride + lo + j * LEAF_WORDS;
-    const long long rem = hi - lo - j * LEAF_WORDS;
-    const int nw = rem < LEAF_WORDS ? (int)rem : LEAF_WORDS;
-    uint32_t h[8];
-    b2s_init(h, (uint32_t)j, 0u);
-    b2s_words(h, nw, false, [&](int b, uint32_t* m) {
-        const int w0 = b * 16;
-        if (ALIGNED && w0 + 16 <= nw) {
-            const uint4* s4 = reinterpret_cast<const uint4*>(src + w0);
+    if (j < nleaf) {
+        const uint32_t* src = x + (long long)blockIdx.y * stride + lo + j * LEAF_WORDS;
+        const long long rem = hi - lo - j * LEAF_WORDS;
+        const int nw = rem < LEAF_WORDS ? (int)rem : LEAF_WORDS;
+        uint32_t h[8];
+        b2s_init(h, (uint32_t)j, 0u);
+        b2s_words(h, nw, false, [&](int b, uint32_t* m) {
+            const int w0 = b * 16;
+            if (ALIGNED && w0 + 16 <= nw) {
+                const uint4* s4 = reinterpret_cast<const uint4*>(src + w0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 u = s4[q];
-                m[4 * q] = u.x;
-                m[4 * q + 1] = u.y;
-                m[4 * q + 2] = u.z;
-                m[4 * q + 3] = u.w;
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 u = s4[q];
+                    m[4 * q] = u.x;
+                    m[4 * q + 1] = u.y;
+                    m[4 * q + 2] = u.z;
+                    m[4 * q + 3] = u.w;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) m[q] = w0 + q < nw ? src[w0 + q] : 0u;
             }
-        } else {
+        });
 #pragma unroll
-            for (int q = 0; q < 16; ++q) m[q] = w0 + q < nw ? src[w0 + q] : 0u;
+        for (int i = 0; i < 8; ++i) dig[threadIdx.x * 8 + i] = h[i];
+    }
+    __syncthreads();
+    if (threadIdx.x < 256 / FANOUT) {
+        const long long q = (long long)blockIdx.x * (256 / FANOUT) + threadIdx.x;
+        const long long rem = nleaf - q * FANOUT;
+        if (rem > 0) {
+            const int nch = rem < FANOUT ? (int)rem : FANOUT;
+            const uint32_t* src = dig + threadIdx.x * FANOUT * 8;
+            uint32_t h[8];
+            b2s_init(h, (uint32_t)q, 1u);
+            b2s_words(h, nch * 8, false, [&](int b, uint32_t* m) {
+                const int w0 = b * 16;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) m[i] = w0 + i < nch * 8 ? src[w0 + i] : 0u;
+            });
+            uint32_t* o = out + (long long)blockIdx.y * out_stride + q * 8;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = h[i];
         }
-    });
-    uint32_t* o = out + (long long)blockIdx.y * out_stride + j * 8;
+    }
+}
+
+constexpr int TOP_MAX = 1024;   // level-(d0+1) digests the top kernel keeps in LDS (32 KiB)
+
+// the rest of a segment's tree in ONE workgroup per batch entry: in[y] holds n_in >= 1 digests of
+// level d0 - 1; levels d0, d0 + 1, ... until one digest remains (levels >= d0 + 1 live in LDS).
+// root[y * root_stride] = the segment root; with `combine`, the tree's final node over this single
+// segment's root (node_depth 255, last_node) instead.  n_in <= FANOUT * TOP_MAX.
+__global__ __launch_bounds__(256) void b2s_top_kernel(const uint32_t* __restrict__ in, long long in_stride,
+                                                     int n_in, int d0, int combine, uint32_t* __restrict__ root,
+                                                     long long root_stride) {
+    __shared__ uint32_t buf[2][TOP_MAX * 8];
+    const uint32_t* src_g = in + (long long)blockIdx.y * in_stride;
+    uint32_t* dst = root + (long long)blockIdx.y * root_stride;
+    auto node = [&](const uint32_t* src, int n, long long q, uint32_t depth, uint32_t* o) {
+        const long long rem = n - q * FANOUT;
+        const int nch = rem < FANOUT ? (int)rem : FANOUT;
+        const uint32_t* c = src + q * FANOUT * 8;
+        uint32_t h[8];
+        b2s_init(h, (uint32_t)q, depth);
+        b2s_words(h, nch * 8, false, [&](int b, uint32_t* m) {
+            const int w0 = b * 16;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = h[i];
+            for (int i = 0; i < 16; ++i) m[i] = w0 + i < nch * 8 ? c[w0 + i] : 0u;
+        });
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = h[i];
+    };
+    int n = n_in;
+    const uint32_t* cur = src_g;
+    int which = 0;
+    uint32_t depth = (uint32_t)d0;
+    if (n > 1) {
+        while (true) {
+            const int n_out = (n + FANOUT - 1) / FANOUT;
+            for (int q = threadIdx.x; q < n_out; q += 256) node(cur, n, q, depth, buf[which] + q * 8);
+            __syncthreads();
+            cur = buf[which];
+            which ^= 1;
+            n = n_out;
+            ++depth;
+            if (n == 1) break;
+        }
+    }
+    if (threadIdx.x == 0) {
+        uint32_t r[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = cur[i];
+        if (combine) {
+            uint32_t h[8];
+            b2s_init(h, 0u, 255u);
+            b2s_words(h, 8, true, [&](int, uint32_t* m) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) m[i] = r[i];
+#pragma unroll
+                for (int i = 8; i < 16; ++i) m[i] = 0u;
+            });
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = h[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[i] = r[i];
+    }
 }
 
 // internal nodes: out[y][j] = node j over children [F j, F j + F) of in[y] (n_in digests)
@@ -297,17 +384,30 @@ TDL_API int tdl_absdiff_max(const float* a, const float* b, long long lo, long l
 TDL_API long long tdl_b2s_leaf_words() { return LEAF_WORDS; }
 TDL_API long long tdl_b2s_fanout() { return FANOUT; }
 
-// out[y][0..nleaf) digests of x[y * stride + lo : ... + hi), y < batch
-TDL_API int tdl_b2s_leaves(const void* x, long long stride, int batch, long long lo, long long hi, void* out,
-                           long long out_stride, hipStream_t s) {
+// out[y][0..ceil(nleaf / 32)) = level-1 nodes of x[y * stride + lo : ... + hi), y < batch
+TDL_API int tdl_b2s_leaves_l1(const void* x, long long stride, int batch, long long lo, long long hi, void* out,
+                              long long out_stride, hipStream_t s) {
     if (hi <= lo || batch <= 0) return 0;
     const long long nleaf = (hi - lo + LEAF_WORDS - 1) / LEAF_WORDS;
     const dim3 grid((unsigned)((nleaf + 255) / 256), (unsigned)batch);
     const bool aligned = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) && ((lo & 3) == 0) && ((stride & 3) == 0);
     if (aligned)
-        b2s_leaf_kernel<true><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out, out_stride);
+        b2s_leaf_l1_kernel<true><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out,
+                                                      out_stride);
     else
-        b2s_leaf_kernel<false><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out, out_stride);
+        b2s_leaf_l1_kernel<false><<<grid, 256, 0, s>>>((const uint32_t*)x, stride, lo, hi, nleaf, (uint32_t*)out,
+                                                       out_stride);
+    TDL_LAUNCH_CHECK();
+}
+
+TDL_API long long tdl_b2s_top_max_in() { return (long long)FANOUT * TOP_MAX; }
+
+// root[y] = the rest of the tree over in[y][0..n_in) (level d0 - 1 digests); combine: the final node too
+TDL_API int tdl_b2s_top(const void* in, long long in_stride, int n_in, int batch, int d0, int combine, void* root,
+                        long long root_stride, hipStream_t s) {
+    if (n_in <= 0 || batch <= 0 || n_in > FANOUT * TOP_MAX) return (int)hipErrorInvalidValue;
+    b2s_top_kernel<<<dim3(1, (unsigned)batch), 256, 0, s>>>((const uint32_t*)in, in_stride, n_in, d0, combine,
+                                                           (uint32_t*)root, root_stride);
     TDL_LAUNCH_CHECK();
 }
 

@@ -146,8 +146,10 @@ _SIGNATURES = {
     "tdl_gemm": [_P] * 6 + [_I] * 10 + [_L, _P],
     "tdl_gemm_set_timestamps": [_P],
     # audit.hip
-    "tdl_b2s_leaves": [_P, _L, _I, _L, _L, _P, _L, _P],
     "tdl_b2s_nodes": [_P, _L, _L, _I, _I, _I, _I, _P, _L, _P],
+    "tdl_b2s_leaves_l1": [_P, _L, _I, _L, _L, _P, _L, _P],
+    "tdl_b2s_top_max_in": [],
+    "tdl_b2s_top": [_P, _L, _I, _I, _I, _I, _P, _L, _P],
     "tdl_keyed_sketch_ws_floats": [_L],
     "tdl_keyed_sketch": [_P, _L, _I, _P, _L, _L, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _I, _P],
     "tdl_contrib_snap": [_P, _P, _P, _L, _P],

@@ -167,13 +167,9 @@ class CommitmentMixin:
         ring = self._gring.get(node)
         if ring is not None:
             contrib_snap(st.flat.grad, self._gprev[node], ring[i])
-            if i == ring.shape[0] - 1:
-                # every contribution is in: their roots in ONE batched tree (a launch per level for
-                # all M) on the verifier's side stream, overlapping the rest of the step (per
-                # micro-batch trees cost ~5 latency-bound node launches each)
-                M, n = ring.shape
-                self._on_side(st, lambda: self._roots_into(ring, self._commit_segments(st), M, n,
-                                                           self._gcom[node][:M]))
+            # its commitment on the verifier's side stream (two launches: leaves + level 1, the rest
+            # of the tree), overlapping the next micro-batches' compute instead of the step's tail
+            self._on_side(st, lambda: self._root_into(ring[i], self._commit_segments(st), self._gcom[node][i:i + 1]))
         r = self._gsk_run.get(node)
         if r is not None:
             sk = self._sketch_for(st)

@@ -145,25 +145,30 @@ def merkle_roots(x: torch.Tensor, segments: Sequence[Tuple[int, int]], batch: in
         final.copy_(_root_bytes_to_tensor(_combine_cpu([])).expand(batch, -1))
         return final
     nseg = len(segs)
-    roots = torch.empty(batch, nseg, DIGEST_WORDS, dtype=torch.int32, device=dev)
+    roots = final if nseg == 1 else torch.empty(batch, nseg, DIGEST_WORDS, dtype=torch.int32, device=dev)
+    top_max = int(_lib.lib().tdl_b2s_top_max_in())
     for k, (lo, hi) in enumerate(segs):
-        n = (hi - lo + LEAF_WORDS - 1) // LEAF_WORDS
+        # leaves + level 1 in one launch, then (beyond ~8 M words) plain node levels, then the rest of
+        # the tree in one workgroup per batch entry (with the final combine when there is one segment)
+        nleaf = (hi - lo + LEAF_WORDS - 1) // LEAF_WORDS
+        n = (nleaf + FANOUT - 1) // FANOUT
         cur = torch.empty(batch, n * DIGEST_WORDS, dtype=torch.int32, device=dev)
-        _lib.call("tdl_b2s_leaves", ptr(flat), stride, batch, lo, hi, ptr(cur), n * DIGEST_WORDS, sp)
-        depth = 1
-        while True:
+        _lib.call("tdl_b2s_leaves_l1", ptr(flat), stride, batch, lo, hi, ptr(cur), n * DIGEST_WORDS, sp)
+        depth = 2
+        while n > top_max:
             n_out = (n + FANOUT - 1) // FANOUT
-            if n_out == 1:
-                dst, dstride = roots[:, k], nseg * DIGEST_WORDS
-            else:
-                dst = torch.empty(batch, n_out * DIGEST_WORDS, dtype=torch.int32, device=dev)
-                dstride = n_out * DIGEST_WORDS
-            _lib.call("tdl_b2s_nodes", ptr(cur), n * DIGEST_WORDS, n, batch, FANOUT, depth, 0, ptr(dst), dstride, sp)
-            if n_out == 1:
-                break
+            dst = torch.empty(batch, n_out * DIGEST_WORDS, dtype=torch.int32, device=dev)
+            _lib.call("tdl_b2s_nodes", ptr(cur), n * DIGEST_WORDS, n, batch, FANOUT, depth, 0, ptr(dst),
+                      n_out * DIGEST_WORDS, sp)
             cur, n, depth = dst, n_out, depth + 1
-    _lib.call("tdl_b2s_nodes", ptr(roots), nseg * DIGEST_WORDS, nseg, batch, nseg, 255, 1, ptr(final),
-              DIGEST_WORDS, sp)
+        if nseg == 1:
+            _lib.call("tdl_b2s_top", ptr(cur), n * DIGEST_WORDS, n, batch, depth, 1, ptr(final), DIGEST_WORDS, sp)
+        else:
+            _lib.call("tdl_b2s_top", ptr(cur), n * DIGEST_WORDS, n, batch, depth, 0, ptr(roots[:, k]),
+                      nseg * DIGEST_WORDS, sp)
+    if nseg > 1:
+        _lib.call("tdl_b2s_nodes", ptr(roots), nseg * DIGEST_WORDS, nseg, batch, nseg, 255, 1, ptr(final),
+                  DIGEST_WORDS, sp)
     return final
 
 
