@@ -943,7 +943,7 @@ enum {
     VD_LOSS = 0, VD_OUT_FLAG = 1, VD_OUT_Z = 2, VD_GRAD_FLAG = 3, VD_GRAD_Z = 4, VD_METRICS = 5, VD_GRAD_SUMSQ = 11,
     VD_OUT_MEAN = 12, VD_OUT_STD = 13, VD_GRAD_L2 = 14, VD_NONFINITE = 15, VD_GRAD_COS = 16, VD_ATTACK_TRUTH = 17,
     VD_PRESENT = 18, VD_STAGE = 19, VD_OUT_CONF = 20, VD_GRAD_CONF = 21,
-    VD_DIGEST = 95   // security/stage_verifier.py DIGEST
+    VD_DIGEST = 115  // security/stage_verifier.py DIGEST
 };
 
 __global__ __launch_bounds__(256) void verify_finish_kernel(VerifyFinishArgs a) {

@@ -166,6 +166,40 @@ def test_local_clean_run_no_blame_with_mirrors():
         assert len(mir) == 1 and torch.equal(mir[0].flat.master, st.flat.master), node
 
 
+@pytest.mark.parametrize("target", [0, 2])
+def test_local_lying_tied_member_caught(target):
+    """The tied embedding / LM-head gradient: a member applying (and committing, and shipping) a
+    sign-flipped tied gradient passes its own sum check (the tied rows are the all-reduce's) and is
+    caught by the cross-member tie check, computed by the two members' auditors only."""
+    eng = _make(3, "lie_tied", target=target, start=3, micro=4, k=1)
+    for b in _batches(6):
+        eng.train_step(b)
+    eng.flush()
+    got = _blamed(eng)
+    assert eng.lied_steps == [3, 4, 5, 6]
+    assert {n for _, n, _ in got} == {target}, got
+    assert set(eng.lied_steps) <= {s for s, _, _ in got}, got
+
+
+def test_local_lying_tied_feed_is_skipped_not_blamed():
+    """A member feeding the tied all-reduce something else than its committed contributions makes
+    both members apply the same wrong sum: not attributable, so nobody is blamed and every such
+    step's update is skipped — the weights never move off the last clean step's."""
+    eng = _make(3, "lie_tied_feed", target=2, start=3, micro=2, k=1)
+    bs = _batches(5)
+    for b in bs[:2]:
+        eng.train_step(b)
+    eng.flush()
+    before = {n: st.flat.master.clone() for n, st in eng.stages.items()}
+    for b in bs[2:]:
+        eng.train_step(b)
+    eng.flush()
+    assert eng.lied_steps == [3, 4, 5]
+    assert _blamed(eng) == []
+    for n, st in eng.stages.items():
+        assert torch.equal(st.flat.master, before[n]), n
+
+
 # ---------------------------------------------------------------------------------------------- gloo ranks
 def _free_port():
     s = socket.socket()
@@ -199,7 +233,7 @@ def _run_gloo(world, kind, target, micro, k, steps, seed=0):
 
 
 @pytest.mark.parametrize("kind,target", [("lie_applied", 1), ("lie_answer", 1), ("hash_forge", 2),
-                                         ("lie_answer", 0)])
+                                         ("lie_answer", 0), ("lie_tied", 2)])
 @pytest.mark.slow
 def test_gloo_lying_rank_caught(kind, target):
     """3 gloo processes, the liar is a subclass in its own process (the loss stage for hash_forge,

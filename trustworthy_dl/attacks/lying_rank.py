@@ -19,6 +19,16 @@ scripts/lying_rank.py) or, in local mode, for its own node only.
   root would be needed.  Caught every step (root of the shipped gradient != commitment).
 * ``lie_sumsq``     reports a huge gradient sum of squares in its digest row (every stage's updates
   would be clipped to nothing).  Harmless: the global clip uses the sums its auditor computed.
+* ``lie_tied``      a tie-group member (GPT-2: the embedding or the LM-head stage) applies, ships and
+  commits the tied weight's gradient sign-flipped after the tied all-reduce; everything else honest.
+  The stage's own sum check excludes the tied rows (the all-reduce adds the other member's
+  contributions there): caught by the cross-member tie check (its auditor's sketch of the tied
+  gradient it applies != the sum of both members' committed tied contributions, while the other
+  member's matches).
+* ``lie_tied_feed`` a tie-group member feeds the tied all-reduce its gradient sign-flipped (after its
+  contributions were committed): both members then apply the same wrong sum.  Which member fed it
+  is not identifiable from the sums, so nobody is blamed — the replica's update is skipped every
+  such step (tampering evidence), and the weights never take the poisoned gradient.
 
 Ground truth: ``lied_steps`` lists the steps where the rank applied something else than the honest
 gradient.  Reference: the optimizer step trusts every node (distributed_trainer.py:441-446).
@@ -30,7 +40,7 @@ from typing import List, Optional
 
 import torch
 
-ATTACKS = ("lie_applied", "lie_answer", "hash_forge", "lie_sumsq")
+ATTACKS = ("lie_applied", "lie_answer", "hash_forge", "lie_sumsq", "lie_tied", "lie_tied_feed")
 
 
 def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 0):
@@ -66,7 +76,13 @@ def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 
             self._lie_init()
             self._honest_g = None
             self._lie_j = -1
-            if not self._lying_now(node) or kind == "lie_sumsq":
+            if not self._lying_now(node) or kind in ("lie_sumsq", "lie_tied_feed"):
+                return super()._contrib_commitments(node, st)
+            if kind == "lie_tied":
+                tr = self._tie_range(st)
+                if tr is not None:
+                    st.flat.grad[tr[0]:tr[0] + tr[1]].neg_()     # applied, shipped and committed
+                    self.lied_steps.append(self.global_step)
                 return super()._contrib_commitments(node, st)
             if kind == "lie_applied":
                 self._honest_g = st.flat.grad.clone()            # shipped + committed
@@ -95,6 +111,16 @@ def make_lying_engine(base_cls, kind: str, target: int, start: int, seed: int = 
                 from ..security import stage_verifier as SV
                 d[SV.D_GRAD_SUMSQ:SV.D_GRAD_SUMSQ + 1].fill_(1e12)
                 self.lied_steps.append(self.global_step)
+
+        @torch.no_grad()
+        def _note_tied_pre(self, st):
+            super()._note_tied_pre(st)
+            node = self._node_of(st)
+            if kind == "lie_tied_feed" and self._lying_now(node):
+                tr = self._tie_range(st)
+                if tr is not None:
+                    st.flat.grad[tr[0]:tr[0] + tr[1]].neg_()     # what goes into the all-reduce
+                    self.lied_steps.append(self.global_step)
 
         def _applied_gradient(self, node, st):
             if self._lying_now(node) and kind == "lie_applied" and self._honest_g is not None:

@@ -70,7 +70,12 @@ class AttributionMixin:
             akind, _ = self._audit_vectors(D)
         abad = (akind > 0).float()
         # a tied-weight member applying something else than the sum of the members' contributions
-        gbad = self._tied_mismatch(D) if self._gsk_on else torch.zeros_like(of)
+        # (blame), or the tie group's all-reduce fed something else than the committed contributions
+        # (evidence: the replica's update is skipped; which member fed it is not identifiable)
+        if self._gsk_on:
+            gbad, gev = self._tied_mismatch(D)
+        else:
+            gbad, gev = torch.zeros_like(of), torch.zeros_like(of)
         # proof of tampering (not a statistic): compromises at once (compromise_on_proof)
         self._proof = torch.maximum(torch.maximum((pf > 0).float(), abad), gbad)
         self._proof_kind = akind + gbad * 32.0
@@ -129,7 +134,7 @@ class AttributionMixin:
             gb = gbad[idx]
             blame[idx] = torch.maximum(b, gb)
             # a gradient rewritten after the backward skips that stage's update (it does not echo)
-            evidence[idx] = torch.maximum(ev.expand(n), gb)
+            evidence[idx] = torch.maximum(torch.maximum(ev.expand(n), gb), gev[idx])
         return blame, evidence
 
     # ================================================================== heartbeat -> OFFLINE

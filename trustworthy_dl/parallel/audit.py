@@ -269,7 +269,8 @@ class AuditMixin:
 
     def _audit_one(self, mir: Stage, x: torch.Tensor, m: int, M: int, y_seen=None, dy=None, labels=None,
                    dx_seen=None, c_m: Optional[torch.Tensor] = None, C: Optional[torch.Tensor] = None,
-                   s: Optional[torch.Tensor] = None, key: Optional[int] = None):
+                   s: Optional[torch.Tensor] = None, key: Optional[int] = None,
+                   sT: Optional[torch.Tensor] = None, tkey: Optional[int] = None):
         """Checks of one opened micro-batch ``m``, recomputed on ``mir`` (the live mirror, or the
         stage's own modules / shipped weights outside mirror mode).  Returns device tensors
         (mismatch flag [1], failed-check bitmask [1], worst relative error [1]).
@@ -278,7 +279,8 @@ class AuditMixin:
         * input gradient (AK_DX): the gradient sent upstream == the recomputed one for the output
           gradient the audited stage received;
         * contribution (AK_DW): the opened c_m hashes to its commitment, its keyed sketch equals
-          the committed s_m bit for bit, and it equals the recomputed contribution."""
+          the committed s_m bit for bit, and it equals the recomputed contribution; for a tie-group
+          member, its tied part's sketch under the shared tie key equals the committed one too."""
         from ..security.grad_audit import keyed_sketch, merkle_root, roots_differ
         bwd = self.cfg.audit_backward and (mir.computes_loss or dy is not None)
         y_ref, dx_ref, g_ref = self._recompute(mir, x, dy, labels, M, backward=bwd)
@@ -296,7 +298,12 @@ class AuditMixin:
             segs = self._commit_segments(mir)
             c = c_m.to(mir.device)
             hbad = roots_differ(merkle_root(c, segs), C[m])
-            sbad = (keyed_sketch(c, segs, key) != s[m].to(mir.device)).any().float().reshape(1)
+            sbad = (keyed_sketch(c, self._sum_segments(mir), key) != s[m].to(mir.device)).any().float().reshape(1)
+            tr = self._tie_range(mir) if sT is not None else None
+            if tr is not None:
+                o, nt = tr
+                tb = (keyed_sketch(c[o:o + nt], [(0, nt)], tkey) != sT[m].to(mir.device)).any().float().reshape(1)
+                sbad = torch.maximum(sbad, tb)
             e = self._seg_rel_err(c, g_ref, segs).reshape(1)
             f = torch.maximum(torch.maximum(hbad, sbad), (e > self.cfg.audit_grad_tol).float())
             kind += f * SV.AK_DW
@@ -314,9 +321,9 @@ class AuditMixin:
         if C.shape[0] != M + 2:
             one = torch.ones(1, device=dev)
             return one * (SV.AK_GAPP + SV.AK_WHASH), one * 1e30
-        segs = self._commit_segments(mir)
+        segs = self._sum_segments(mir)
         G = G.to(dev)
-        gbad = roots_differ(merkle_root(G, segs), C[M])
+        gbad = roots_differ(merkle_root(G, self._commit_segments(mir)), C[M])
         sg = keyed_sketch(G, segs, key)
         ssum = s.to(dev).float().sum(0)
         from ..security.grad_audit import seg_sumsq
@@ -326,6 +333,30 @@ class AuditMixin:
         abad = torch.maximum(gbad, (e > self.audit_sum_tol).float())
         wbad = roots_differ(self._mirror_master_root(mir), C[M + 1])
         return abad * SV.AK_GAPP + wbad * SV.AK_WHASH, e
+
+    @torch.no_grad()
+    def _write_tie(self, d: torch.Tensor, mir: Stage, G: torch.Tensor, sT: Optional[torch.Tensor],
+                   tkey: int, next_slot: bool):
+        """Tie-group member audited here: U = sum of its M committed tied contribution sketches,
+        G = the sketch of the tied part of the gradient it shipped (= the one its mirror applies),
+        N = that part's norm, all under the step's shared tie key, into this auditor's digest row
+        (``_tied_mismatch`` compares them across the members).  A malformed ``sT`` leaves ON = 1
+        with non-finite U: the member deviates."""
+        from ..security.grad_audit import K_KEYED, keyed_sketch
+        tr = self._tie_range(mir)
+        if tr is None:
+            return
+        o, nt = tr
+        g = G.to(d.device)[o:o + nt]
+        bu, bg, bn, bo = (SV.D_TIE_U_NEXT, SV.D_TIE_G_NEXT, SV.D_TIE_N_NEXT, SV.D_TIE_ON_NEXT) if next_slot else \
+            (SV.D_TIE_U_PREV, SV.D_TIE_G_PREV, SV.D_TIE_N_PREV, SV.D_TIE_ON_PREV)
+        if sT is None or sT.dim() != 2 or sT.shape[1] != K_KEYED:
+            d[bu:bu + K_KEYED].fill_(float("nan"))
+        else:
+            d[bu:bu + K_KEYED].copy_(sT.to(d.device).float().sum(0))
+        d[bg:bg + K_KEYED].copy_(keyed_sketch(g, [(0, nt)], tkey))
+        d[bn:bn + 1].copy_(torch.linalg.vector_norm(g).reshape(1))
+        d[bo:bo + 1].fill_(1.0)
 
     @staticmethod
     def _combine(acc, res):
@@ -365,6 +396,22 @@ class AuditMixin:
         M = len(self._audit_batch)
         mirror = self._gsk_on
         picks = self._target_picks(order) if self._targeted else {}
+        coms: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        tkey = None
+        if mirror:
+            # every audited stage commits before any key exists (the tie key is shared by the tie
+            # group's members: drawn after all of them committed)
+            for k in range(S):
+                if k == S - 1 and not self.cfg.audit_backward:
+                    continue
+                aud = order[k + 1] if k < S - 1 else order[k - 1]
+                if aud in rows:
+                    p = order[k]
+                    dev = self.stages[aud].device
+                    coms[p] = (self._contrib_commitments(p, self.stages[p]).to(dev),
+                               self._applied_gradient(p, self.stages[p]).to(dev))
+            if self._tie_members():
+                tkey = self._mon_rng.getrandbits(63)
         for k in range(S):
             p = order[k]
             last = k == S - 1
@@ -378,7 +425,7 @@ class AuditMixin:
             chosen = [m for m in dict.fromkeys(list(self._audit_ms) + [picks.get(p, -1)])
                       if m >= 0 and "x" in recs.get(m, {})] if self._audit_now else []
             res = None
-            C = s = key = None
+            C = s = key = sT = None
             opened: List[torch.Tensor] = []
             if mirror:
                 dev = self.stages[aud].device
@@ -387,10 +434,13 @@ class AuditMixin:
                     self._seed_mirror(mir, *self._optimizer_state(p, st))
                 # the key is drawn only after the commitments exist, the opened set only after the
                 # sketches (private RNG; a lying auditee-side method sees them in that order)
-                C = self._contrib_commitments(p, st).to(dev)
-                G = self._applied_gradient(p, st).to(dev)
+                C, G = coms[p]
                 key = self._mon_rng.getrandbits(63)
                 s = self._contrib_sketches(p, st, key).to(dev)
+                if tkey is not None and self._tie_range(st) is not None:
+                    sT = self._tie_sketches(p, st, tkey)
+                    sT = sT.to(dev) if sT is not None else None
+                    self._write_tie(rows[aud], mir, G, sT, tkey, next_slot=last)
                 opened = self._open_contributions(p, st, chosen)
                 kd, e = self._verify_applied(mir, C, G, s, key)
                 res = ((kd > 0).float(), kd, e)
@@ -411,7 +461,7 @@ class AuditMixin:
                 res = self._combine(res, self._audit_one(
                     mir, rec["x"].to(mir.device), m, M, y_seen=rec.get("y"), dy=None if last else rec.get("dy"),
                     labels=rec.get("labels"), dx_seen=rec.get("dx"), c_m=opened[j] if opened else None,
-                    C=C, s=s, key=key))
+                    C=C, s=s, key=key, sT=sT, tkey=tkey))
             if res is not None:
                 self._write_verdict(rows[aud], res, next_slot=last)
 

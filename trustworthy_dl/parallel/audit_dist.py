@@ -136,33 +136,54 @@ class DistAuditMixin:
                              [(t, r) for k, t, r in allops if k == "recv"], "audit")
             work = dist.batch_isend_irecv(ops)
 
-        # ---- 2. key (auditor): only after the commitments were read
+        # ---- 2. key (auditor): only after the commitments were read; for a tie-group member also
+        # this auditor's part of the step's shared tie key
         got: Dict[int, dict] = {}
         keys: Dict[int, int] = {}
+        tie_pos = self._tie_members() if mirror else []
+        for k in self._tkey_trash:      # last step's tie-key parts: every rank read them before it
+            store.delete_key(k)         # joined that step's digest all-gather
+        self._tkey_trash = []
         if mirror:
-            for p, _, _ in peers:
+            for p, sid, _ in peers:
                 k = f"{tag}/com/{p}"
                 got[p] = json.loads(store.get(k).decode())
                 store.delete_key(k)
                 keys[p] = self._audit_rng.getrandbits(63)
                 store.set(f"{tag}/key/{p}", str(keys[p]))
+                if sid in tie_pos:
+                    k = f"{tag}/tkey/{p}"
+                    store.set(k, str(self._audit_rng.getrandbits(63)))
+                    self._tkey_trash.append(k)
+
+        def tie_key():
+            parts = [int(store.get(f"{tag}/tkey/{self.plan.ranks[j]}").decode()) for j in tie_pos]
+            return self._tie_key_of(parts)
 
         # ---- 3. sketches (auditee)
         if mirror and my_auditor is not None:
             k = f"{tag}/key/{me}"
             key_req = int(store.get(k).decode())
             store.delete_key(k)
+            sT = self._tie_sketches(me, st, tie_key()) if s in tie_pos else None
             note_host_sync()
             sk = self._contrib_sketches(me, st, key_req).cpu().tolist()
-            store.set(f"{tag}/sk/{me}", _enc_json(sk))
+            store.set(f"{tag}/sk/{me}", _enc_json({"s": sk, "t": sT.cpu().tolist() if sT is not None else None}))
 
         # ---- 4. open (auditor): only after the sketches were read
         sketches: Dict[int, Optional[torch.Tensor]] = {}
+        tsk: Dict[int, Optional[torch.Tensor]] = {}
+        tkey = tie_key() if any(sid in tie_pos for _, sid, _ in peers) else None
         if mirror:
             for p, _, _ in peers:
                 k = f"{tag}/sk/{p}"
-                sketches[p] = self._as_tensor(json.loads(store.get(k).decode()), torch.float32)
+                pl = json.loads(store.get(k).decode())
                 store.delete_key(k)
+                pl = pl if isinstance(pl, dict) else {}
+                sketches[p] = self._as_tensor(pl.get("s"), torch.float32)
+                t = self._as_tensor(pl.get("t"), torch.float32) if pl.get("t") is not None else None
+                from ..security.grad_audit import K_KEYED
+                tsk[p] = t if t is not None and t.dim() == 2 and tuple(t.shape) == (M, K_KEYED) else None
         tgt: Dict[int, int] = {}
         if self._targeted and peers:
             zs = []
@@ -283,6 +304,8 @@ class DistAuditMixin:
                 else:
                     kd, e = self._verify_applied(mir, C, mir._g_in, s_p, key)
                     res = ((kd > 0).float(), kd, e)
+                if sid in tie_pos:
+                    self._write_tie(d, mir, mir._g_in, tsk.get(p), tkey, next_slot=nxt_peer)
                 self._mirror_pending.append((mir, mir._g_in, p))
                 d[SV.D_MIRROR:SV.D_MIRROR + 1].fill_(1.0)
                 slot = SV.D_SUMSQ_NEXT if nxt_peer else SV.D_SUMSQ_PREV
@@ -292,13 +315,14 @@ class DistAuditMixin:
                     labels = self._audit_targets[m].to(self.device, non_blocking=True)
                     r1 = self._audit_one(mir, self._audit_outputs.get(m), m, M, labels=labels,
                                          dx_seen=self._audit_recv_dy.get(m), c_m=ib["c"][j] if ib["c"] else None,
-                                         C=C, s=s_p, key=key)
+                                         C=C, s=s_p, key=key, sT=tsk.get(p), tkey=tkey)
                 else:
                     xp = ib["x"][j] if ib["x"] else self._stage_input(self._audit_batch[m], mir)
                     dy = self._audit_sent_dx.get(m) if bwd else None
                     r1 = self._audit_one(mir, xp, m, M, y_seen=self._audit_inputs[m], dy=dy,
                                          dx_seen=ib["dx"][j] if ib["dx"] else None,
-                                         c_m=ib["c"][j] if ib["c"] else None, C=C, s=s_p, key=key)
+                                         c_m=ib["c"][j] if ib["c"] else None, C=C, s=s_p, key=key,
+                                         sT=tsk.get(p), tkey=tkey)
                 res = self._combine(res, r1)
             if res is not None:
                 self._write_verdict(d, res, next_slot=nxt_peer)

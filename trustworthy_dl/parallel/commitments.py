@@ -5,8 +5,10 @@ Per step, every audited stage A (its auditor V: the next stage, or the previous 
 stage):
 
 1. during the backward, after micro-batch i's weight gradients: c_i = g - prev, prev = g into a
-   ring of M contributions (the tied weight's elements excluded from everything below: the tied
-   all-reduce adds to them; they have their own cross-stage check, ``_tied_mismatch``);
+   ring of M contributions (the tied weight's part of the last one is taken right before the tied
+   all-reduce when that starts early; the all-reduce adds the other member's contributions to the
+   tied rows of G, so the sum check of step 5 leaves them out and the members' auditors check them
+   against each other instead, step 6);
 2. **commit**: A sends V the BLAKE2s Merkle roots of c_0..c_{M-1}, of the gradient G it applies and
    of its fp32 master weights (``_contrib_commitments``), and ships G itself;
 3. **key**: only after V RECEIVED the commitments does it reveal a private sketch key; A answers
@@ -21,6 +23,11 @@ stage):
    opened with probability >= k/M per step), cannot apply something else than the G it shipped
    (the mirror diverges: caught at the next step's weight check), and cannot rewrite its weights
    outside the optimizer.
+6. **tie**: for the tied embedding / LM-head weight, each member's auditor adds a private part to a
+   shared tie key after reading its auditee's commitments; each member answers with the keyed
+   sketches of its M contributions' tied rows under that key (opened ones verified like s_m), and
+   its auditor publishes U = their sum and sketch(tied rows of G).  Every rank checks that each
+   member applies U_embedding + U_head (``_tied_mismatch``).
 
 Every auditee-side answer is a method a lying rank can override (tests/test_lying_rank.py runs
 such subclasses as gloo ranks); no check trusts a value the audited rank reports about itself.
@@ -66,8 +73,14 @@ class CommitmentMixin:
         return sk
 
     def _commit_segments(self, st: Stage) -> List[Tuple[int, int]]:
-        """Flat-gradient ranges the commitments cover: everything but the tied weight's elements
-        (the tied all-reduce writes those, possibly while a micro-batch commit is being taken)."""
+        """Flat ranges the Merkle commitments and the recompute comparison cover: all of it (the
+        tied weight's own per-micro-batch contributions included)."""
+        return [(0, st.flat.numel)]
+
+    def _sum_segments(self, st: Stage) -> List[Tuple[int, int]]:
+        """Flat ranges of the keyed sum check sketch(G) = sum_i s_i: everything but the tied
+        weight's elements (its applied gradient is the tie group's all-reduce of the members'
+        contributions, checked across the members' auditors: ``_tied_mismatch``)."""
         from ..security.grad_audit import _segments, tied_ranges
         key = ("seg", tuple(st.layer_range), st.flat.numel)
         segs = self._gsk_cache.get(key)
@@ -98,36 +111,54 @@ class CommitmentMixin:
                 n += g_in.numel() * 4
         return n
 
-    # ------------------------------------------------------------------ tied weight (public sketch)
-    def _tied_param(self, st: Stage) -> Optional[torch.Tensor]:
-        """This stage's member of the first tie group (GPT-2: wte / LM head), if any."""
+    # ------------------------------------------------------------------ tied weight
+    def _tie_members(self) -> List[int]:
+        """Stage positions (in the replica's order) holding a member of the first tie group, when
+        the group spans more than one stage (GPT-2: the embedding stage and the LM-head stage)."""
         if not self.ties:
+            return []
+        pos = sorted({i for li, _ in self.ties[0] for i, (a, b) in enumerate(self.plan.ranges) if a <= li < b})
+        return pos if len(pos) > 1 else []
+
+    @staticmethod
+    def _tie_key_of(parts) -> int:
+        """The step's shared tie key from every member auditor's private contribution (each posted
+        only after its auditee's commitments were read): no member knows it before committing."""
+        import hashlib
+        h = hashlib.blake2b(",".join(str(int(v)) for v in sorted(parts)).encode(), digest_size=8).digest()
+        return int.from_bytes(h, "little") & ((1 << 63) - 1)
+
+    def _tie_range(self, st: Stage) -> Optional[Tuple[int, int]]:
+        """(offset, numel) of this stage's member of a cross-stage tie group in its flat buffer."""
+        if st.stage_id not in self._tie_members():
             return None
         for li, attr in self.ties[0]:
             prm = st.local_param(li, attr)
             if prm is not None:
-                return prm
+                for q, o, n in zip(st.flat.params, st.flat.offsets, st.flat.sizes):
+                    if q is prm:
+                        return o, n
         return None
 
-    def _tied_sketch(self, st: Stage, g: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-        """Sketch of the tied weight's gradient with a pattern shared by every member of the tie
-        group (parameter-local indexing), so the members' sketches add up across stages."""
-        from ..security.grad_audit import GradSketch
-        prm = self._tied_param(st)
-        if prm is None or getattr(prm, "main_grad", None) is None:
-            return None
-        key = (prm.numel(), str(st.device))
-        sk = self._tsk_cache.get(key)
-        if sk is None:
-            sk = self._tsk_cache[key] = GradSketch(prm.numel(), st.device, seed=self.cfg.seed * 7 + 424242)
-        return sk((prm.main_grad if g is None else g).reshape(-1), sk.offset(self.cfg.seed, self.global_step))
+    def _node_of(self, st: Stage) -> int:
+        for n, s_ in self.stages.items():
+            if s_ is st:
+                return n
+        return -1
 
     def _note_tied_pre(self, st: Stage):
-        """Right before the tied all-reduce: the stage's own tied-weight gradient contribution."""
-        if self._gsk_on:
-            t = self._tied_sketch(st)
-            if t is not None:
-                self._tsk_pre[st.stage_id] = t
+        """Right before a tied all-reduce: when it is launched before the last micro-batch's
+        contribution was taken (the early path, from an autograd hook), take the tied weight's part
+        of that contribution now — the all-reduce rewrites those elements in place."""
+        node = self._node_of(st)
+        ring = self._gring.get(node) if self._gsk_on else None
+        tr = self._tie_range(st)
+        if ring is None or tr is None or self._gcount.get(node, 0) != ring.shape[0] - 1:
+            return
+        from ..security.grad_audit import contrib_snap
+        o, n = tr
+        contrib_snap(st.flat.grad[o:o + n], self._gprev[node][o:o + n], ring[-1][o:o + n])
+        self._tied_snapped[node] = True
 
     # ------------------------------------------------------------------ per-micro-batch contributions
     def _begin_commitments(self, M: int):
@@ -137,8 +168,9 @@ class CommitmentMixin:
         self._gring: Dict[int, torch.Tensor] = {}
         self._gprev: Dict[int, torch.Tensor] = {}
         self._gcom: Dict[int, torch.Tensor] = {}
+        self._gcount: Dict[int, int] = {}
+        self._tied_snapped: Dict[int, bool] = {}
         self._gsk_run: Dict[int, torch.Tensor] = {}
-        self._tsk_pre: Dict[int, torch.Tensor] = {}
         self._mirror_pending = []
         if not self._gsk_on:
             # a step whose gradients no mirror sees: every mirror must be re-seeded before it is used
@@ -166,7 +198,13 @@ class CommitmentMixin:
                 self._truth_now[node] = True
         ring = self._gring.get(node)
         if ring is not None:
-            contrib_snap(st.flat.grad, self._gprev[node], ring[i])
+            self._gcount[node] = i + 1
+            if self._tied_snapped.get(node) and i == ring.shape[0] - 1:
+                g, prev = st.flat.grad, self._gprev[node]
+                for lo, hi in self._sum_segments(st):   # the tied part was taken before its all-reduce
+                    contrib_snap(g[lo:hi], prev[lo:hi], ring[i][lo:hi])
+            else:
+                contrib_snap(st.flat.grad, self._gprev[node], ring[i])
             # its commitment on the verifier's side stream (two launches: leaves + level 1, the rest
             # of the tree), overlapping the next micro-batches' compute instead of the step's tail
             self._on_side(st, lambda: self._root_into(ring[i], self._commit_segments(st), self._gcom[node][i:i + 1]))
@@ -229,11 +267,25 @@ class CommitmentMixin:
 
     @torch.no_grad()
     def _contrib_sketches(self, node: int, st: Stage, key: int) -> torch.Tensor:
-        """[M, K_KEYED] keyed sketches of the M committed contributions under the revealed key."""
+        """[M, K_KEYED] keyed sketches of the M committed contributions under the revealed key
+        (the tied weight's elements excluded: ``_tie_sketches``)."""
         from ..security.grad_audit import keyed_sketch
         ring = self._gring[node]
         M, n = ring.shape
-        return keyed_sketch(ring, self._commit_segments(st), key, batch=M, stride=n)
+        return keyed_sketch(ring, self._sum_segments(st), key, batch=M, stride=n)
+
+    @torch.no_grad()
+    def _tie_sketches(self, node: int, st: Stage, tie_key: int) -> Optional[torch.Tensor]:
+        """[M, K_KEYED] keyed sketches of the tied weight's part of the M contributions under the
+        step's shared tie key, indexed parameter-locally (so every member's sketches add up)."""
+        from ..security.grad_audit import keyed_sketch
+        tr = self._tie_range(st)
+        if tr is None:
+            return None
+        o, nt = tr
+        ring = self._gring[node]
+        M, n = ring.shape
+        return keyed_sketch(ring.reshape(-1)[o:], [(0, nt)], tie_key, batch=M, stride=n)
 
     def _open_contributions(self, node: int, st: Stage, ms: List[int]) -> List[torch.Tensor]:
         """The contributions of the opened micro-batches (views into the ring)."""
@@ -247,27 +299,54 @@ class CommitmentMixin:
 
     # ------------------------------------------------------------------ digest slots + tied check
     def _write_commitments(self, node: int, st: Stage, d: torch.Tensor):
-        """Digest slots of the tied-weight cross check: this stage's own contribution to the tied
-        gradient (before the all-reduce) and the tied gradient it applies."""
-        pre = self._tsk_pre.get(st.stage_id) if self._gsk_on else None
-        if pre is not None:
-            d[SV.D_TSK_PRE:SV.D_TSK_PRE + 2].copy_(pre)
-            d[SV.D_TSK_APP:SV.D_TSK_APP + 2].copy_(self._tied_sketch(st))
-            d[SV.D_TSK_ON:SV.D_TSK_ON + 1].fill_(1.0)
-        else:
-            d[SV.D_TSK_ON:SV.D_TSK_ON + 1].fill_(0.0)
+        """Hook point for the stage's own digest row before the audit (the checks themselves are
+        all computed by auditors; a lying subclass overrides this to misreport its statistics)."""
+        return
 
-    def _tied_mismatch(self, D: torch.Tensor) -> torch.Tensor:
-        """Per-node 1.0 where a member of the tied weight's group applies a tied gradient that is not
-        the sum of the members' own contributions (public sketches, as reported by the members)."""
-        from ..security.grad_audit import K_SKETCH
-        bad = torch.zeros(D.shape[0], dtype=torch.float32, device=D.device)
-        ton = (D[:, SV.D_TSK_ON] > 0).float()
-        pre, tapp = D[:, SV.D_TSK_PRE:SV.D_TSK_PRE + K_SKETCH], D[:, SV.D_TSK_APP:SV.D_TSK_APP + K_SKETCH]
+    def _tied_mismatch(self, D: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Per node (blame, evidence) of the tied-weight check, identical on every rank, from values
+        the tie members' AUDITORS computed: U_X = sum of member X's committed tied contribution
+        sketches (each opened one verified against X's commitment and recompute), G_X = sketch of the
+        tied gradient X shipped (and its mirror applies), under the step's shared tie key.  Every
+        member must apply sum_X U_X.  A member whose G deviates while another's matches applied
+        something else: blamed.  When every member deviates alike, the all-reduce was fed something
+        other than the committed contributions — which member did it is not identifiable from the
+        sum — so the replica's update is skipped (evidence) and nobody is blamed."""
+        from ..security.grad_audit import K_KEYED
+        N = D.shape[0]
+        bad = torch.zeros(N, dtype=torch.float32, device=D.device)
+        ev = torch.zeros_like(bad)
+        mem = self._tie_members()
+        if not mem:
+            return bad, ev
+        K = K_KEYED
         for idx in self._replica_orders():
-            t = ton[idx]
-            exp = (pre[idx] * t[:, None]).sum(0, keepdim=True)
-            sc = torch.maximum(exp.abs().amax(), tapp[idx].abs().amax(1)).clamp_min(1e-20)
-            e = torch.nan_to_num((tapp[idx] - exp).abs().amax(1) / sc, nan=1e30, posinf=1e30)
-            bad[idx] = torch.maximum(bad[idx], t * (t.sum() >= 2).float() * (e > 1e-3).float())
-        return bad
+            S = idx.numel()
+            if S < 2 or max(mem) >= S:
+                continue
+            us, gs, ns, ons, nodes = [], [], [], [], []
+            for j in mem:
+                if j + 1 < S:
+                    a, base = idx[j + 1:j + 2], (SV.D_TIE_U_PREV, SV.D_TIE_G_PREV, SV.D_TIE_N_PREV, SV.D_TIE_ON_PREV)
+                else:
+                    a, base = idx[j - 1:j], (SV.D_TIE_U_NEXT, SV.D_TIE_G_NEXT, SV.D_TIE_N_NEXT, SV.D_TIE_ON_NEXT)
+                us.append(D[a, base[0]:base[0] + K].reshape(K))
+                gs.append(D[a, base[1]:base[1] + K].reshape(K))
+                ns.append(D[a, base[2]].reshape(()))
+                ons.append((D[a, base[3]] > 0).float().reshape(()))
+                nodes.append(idx[j:j + 1])
+            on = torch.stack(ons).amin()
+            tot = torch.stack(us).sum(0)
+            dev = []
+            for g, n_ in zip(gs, ns):
+                sc = torch.maximum(torch.maximum(tot.abs().amax(), g.abs().amax()), 0.25 * n_).clamp_min(1e-30)
+                e = torch.nan_to_num((g - tot).abs().amax() / sc, nan=1e30, posinf=1e30)
+                dev.append((e > self.audit_sum_tol).float() * on)
+            dev = torch.stack(dev)
+            every = dev.amin()
+            for d_, nd in zip(dev, nodes):
+                bad[nd] = torch.maximum(bad[nd], (d_ * (1.0 - every)).reshape(1))
+                ev[nd] = torch.maximum(ev[nd], (d_ * every).reshape(1))
+            if every.numel():
+                ev[idx] = torch.maximum(ev[idx], every.expand(S))
+        return bad, ev

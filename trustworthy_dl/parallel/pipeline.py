@@ -185,9 +185,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._mirror_epoch = 0                           # bumped on every rank when mirrors go stale
         self._mirror_pending: List = []                  # (mirror, verified gradient, node) to apply
         self._seed_mark = None                           # (plan, range, epoch) my auditor's mirror was seeded for
-        self._tsk_pre: Dict[int, torch.Tensor] = {}
+        self._tkey_trash: List[str] = []                 # store keys of last step's tie-key parts (audit_dist.py)
         self._gsk_cache: Dict[tuple, object] = {}
-        self._tsk_cache: Dict[tuple, object] = {}
         # attribution (attribution.py)
         self._proof: Optional[torch.Tensor] = None
         self._proof_kind: Optional[torch.Tensor] = None

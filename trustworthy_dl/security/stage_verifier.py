@@ -59,9 +59,7 @@ D_AUDIT_KIND_PREV = 27  # bitmask of the failed checks behind D_AUDIT_PREV (AK_*
 D_AUDIT_NEXT = 28    # audit of the NEXT stage when it is the loss stage (its predecessor audits it)
 D_AUDITED_NEXT = 29
 D_AUDIT_KIND_NEXT = 30
-D_TSK_ON = 31        # 1 when this stage holds a member of the (first) tie group
-D_TSK_PRE = 32       # [2] sketch of this stage's OWN gradient of its tied weight (before the tied all-reduce)
-D_TSK_APP = 34       # [2] sketch of the tied weight's gradient it applies (after the all-reduce and hooks)
+# 31-35 unused (r5's self-reported tied-weight sketches)
 D_MIRROR = 36        # 1 when this rank checked its audited stages against live optimizer mirrors this step
 # cross-party hashes: the first 128 bits of BLAKE2s Merkle roots as 8 exact 16-bit halves each
 # (grad_audit.hash_row); -1 = none this step
@@ -77,7 +75,13 @@ D_XHASH_SHIP = 85    # [8] root of the inputs the audited previous stage shipped
 D_SUMSQ_PREV = 93    # (mirror mode) clipping sum of squares of the gradient the audited previous stage
                      #     shipped here, computed by this auditor (-1: none); the global clip uses these
 D_SUMSQ_NEXT = 94    # same for the audited next (loss) stage
-DIGEST = 95          # csrc/stats.hip VD_DIGEST
+# tied weight (mirror mode): for an audited previous / next stage holding a member of the tie group,
+# computed by this auditor under the step's shared tie key: U = sum of its M committed tied
+# contribution sketches (each opened one verified), G = sketch of the tied gradient it shipped and
+# applies, N = that gradient's norm, ON = 1 when set (parallel/commitments.py ``_tied_mismatch``)
+D_TIE_U_PREV, D_TIE_G_PREV, D_TIE_N_PREV, D_TIE_ON_PREV = 95, 99, 103, 104
+D_TIE_U_NEXT, D_TIE_G_NEXT, D_TIE_N_NEXT, D_TIE_ON_NEXT = 105, 109, 113, 114
+DIGEST = 115         # csrc/stats.hip VD_DIGEST
 # audit check bits
 AK_FWD, AK_DX, AK_DW, AK_WHASH, AK_DXHASH, AK_GAPP = 1, 2, 4, 8, 16, 32
 
