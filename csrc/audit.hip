@@ -119,14 +119,67 @@ __device__ __forceinline__ void b2s_words(uint32_t* h, int nw, bool last_node, L
 
 // leaves AND their level-1 parents in one launch: out[y][q] = level-1 node q (over leaves
 // [32 q, 32 q + 32)) of x[y * stride + lo : ... + hi); each 256-thread workgroup hashes 256 leaves
-// into LDS, then 8 of its threads hash the 8 level-1 nodes they form
+// into LDS, then 8 of its threads hash the 8 level-1 nodes they form.
+// Loads: a thread hashes one 1 KiB leaf, so direct loads put its 64 lanes on 64 different cache
+// lines per instruction (the address path, not HBM, bounded the r6 kernel at ~0.6 TB/s).  A full,
+// aligned workgroup instead stages its 256 leaves through LDS two blocks (128 B per leaf) at a
+// time: 8 consecutive lanes load one leaf's 128 B line, so a wave's uint4 load covers 8 whole lines;
+// the next stage's loads are in flight (registers) while the current two compressions run.  Rows
+// are padded to 36 words: each lane's 16-byte LDS reads of its own row hit distinct banks.
+constexpr int STG_ROW4 = 9;                 // uint4 per padded LDS row (32 words + 4 pad)
+constexpr int STAGES = LEAF_WORDS / 32;     // 8 stages of 2 blocks per leaf
+
 template <bool ALIGNED>
 __global__ __launch_bounds__(256) void b2s_leaf_l1_kernel(const uint32_t* __restrict__ x, long long stride,
                                                          long long lo, long long hi, long long nleaf,
                                                          uint32_t* __restrict__ out, long long out_stride) {
-    __shared__ uint32_t dig[256 * 8];
-    const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (j < nleaf) {
+    __shared__ uint4 stg[256 * STG_ROW4];   // 36 KiB staging; reused for the 256 leaf digests
+    uint32_t* dig = reinterpret_cast<uint32_t*>(stg);
+    const int tid = threadIdx.x;
+    const long long j = (long long)blockIdx.x * 256 + tid;
+    const bool full = ALIGNED && (long long)(blockIdx.x + 1) * 256 * LEAF_WORDS <= hi - lo;
+    if (full) {
+        const uint4* base = reinterpret_cast<const uint4*>(x + (long long)blockIdx.y * stride + lo +
+                                                           (long long)blockIdx.x * 256 * LEAF_WORDS);
+        // piece p = i * 256 + tid of a stage: leaf p >> 3, 16-byte part p & 7; named registers (an
+        // array carried around the stage loop was put in scratch)
+        const uint4* src = base + (tid >> 3) * (LEAF_WORDS / 4) + (tid & 7);
+        constexpr int LS = 32 * (LEAF_WORDS / 4);     // 32 leaves further: the next 256 pieces
+        uint4 r0 = src[0], r1 = src[LS], r2 = src[2 * LS], r3 = src[3 * LS];
+        uint4 r4 = src[4 * LS], r5 = src[5 * LS], r6 = src[6 * LS], r7 = src[7 * LS];
+        uint4* dst = stg + (tid >> 3) * STG_ROW4 + (tid & 7);
+        constexpr int DS = 32 * STG_ROW4;
+        uint32_t h[8];
+        b2s_init(h, (uint32_t)j, 0u);
+        for (int st = 0; st < STAGES; ++st) {
+            __syncthreads();                 // every lane is done reading the previous stage
+            dst[0] = r0; dst[DS] = r1; dst[2 * DS] = r2; dst[3 * DS] = r3;
+            dst[4 * DS] = r4; dst[5 * DS] = r5; dst[6 * DS] = r6; dst[7 * DS] = r7;
+            __syncthreads();
+            // the next stage's loads in flight during this stage's compressions (the last stage
+            // reloads its own data: a uniform, in-bounds no-op)
+            const uint4* nx = src + (st + 1 < STAGES ? st + 1 : st) * 8;
+            r0 = nx[0]; r1 = nx[LS]; r2 = nx[2 * LS]; r3 = nx[3 * LS];
+            r4 = nx[4 * LS]; r5 = nx[5 * LS]; r6 = nx[6 * LS]; r7 = nx[7 * LS];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                uint32_t m[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 u = stg[tid * STG_ROW4 + b * 4 + q];
+                    m[4 * q] = u.x;
+                    m[4 * q + 1] = u.y;
+                    m[4 * q + 2] = u.z;
+                    m[4 * q + 3] = u.w;
+                }
+                const int blk = st * 2 + b;
+                b2s_compress(h, m, (uint32_t)(blk + 1) * 64u, blk == 2 * STAGES - 1, false);
+            }
+        }
+        __syncthreads();                     // staging reads done before it holds digests
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dig[tid * 8 + i] = h[i];
+    } else if (j < nleaf) {
         const uint32_t* src = x + (long long)blockIdx.y * stride + lo + j * LEAF_WORDS;
         const long long rem = hi - lo - j * LEAF_WORDS;
         const int nw = rem < LEAF_WORDS ? (int)rem : LEAF_WORDS;
@@ -150,15 +203,15 @@ __global__ __launch_bounds__(256) void b2s_leaf_l1_kernel(const uint32_t* __rest
             }
         });
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dig[threadIdx.x * 8 + i] = h[i];
+        for (int i = 0; i < 8; ++i) dig[tid * 8 + i] = h[i];
     }
     __syncthreads();
-    if (threadIdx.x < 256 / FANOUT) {
-        const long long q = (long long)blockIdx.x * (256 / FANOUT) + threadIdx.x;
+    if (tid < 256 / FANOUT) {
+        const long long q = (long long)blockIdx.x * (256 / FANOUT) + tid;
         const long long rem = nleaf - q * FANOUT;
         if (rem > 0) {
             const int nch = rem < FANOUT ? (int)rem : FANOUT;
-            const uint32_t* src = dig + threadIdx.x * FANOUT * 8;
+            const uint32_t* src = dig + tid * FANOUT * 8;
             uint32_t h[8];
             b2s_init(h, (uint32_t)q, 1u);
             b2s_words(h, nch * 8, false, [&](int b, uint32_t* m) {
