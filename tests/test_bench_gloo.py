@@ -70,7 +70,11 @@ def test_bench_multirank_json_line(n, mode):
         ring = {(i + dd) % S for dd in range(1, k + 1)} | {(i - dd) % S for dd in range(1, k + 1)}
         default_peers = (ring | nb) if mode == "grouped" else ring
         dir_peers = nb if mode == "async" else set()
-        expect = 1 + groups + (tie if i in (0, S - 1) else 0) + 2 * len(dir_peers) + len(default_peers)
+        # mirror-mode audit on its own group: applied gradient / openings to the auditor (next stage,
+        # or the previous one for the loss stage), the same from the auditee
+        audit_peers = nb
+        expect = 1 + groups + (tie if i in (0, S - 1) else 0) + 2 * len(dir_peers) + len(default_peers) \
+            + len(audit_peers)
         assert c == expect, (r, comms, expect)
         assert streams[r] == c + 2                    # + compute stream + verification side stream
     assert max(streams) <= 32

@@ -161,12 +161,14 @@ def test_parameter_tampering_caught_by_integrity_and_mirror():
     eng.flush()
     hits = [r for r in eng.attack_history if r["attack_type"] == "model_poisoning"]
     assert {r["node_id"] for r in eng.attack_history} == {1}
-    # caught at every tampered step; with no re-shard (reassign=False) the perturbed weights stay
-    # in place and keep failing the check against the auditor's optimizer mirror (the verified
-    # trajectory) on every later step too — they are never accepted as the stage's weights
-    assert sorted({r["step"] for r in hits}) == list(range(12, 19))
+    # caught at every tampered step and only then: right after its update the stage takes the
+    # auditor's verified optimizer state (the mirror), so the perturbation does not outlive its step
+    assert sorted({r["step"] for r in hits}) == [12, 13, 14]
     m = atk.detection_metrics()
-    assert m["recall"] == 1.0
+    assert m["recall"] == 1.0 and m["fp"] == 0
+    st = eng.stages[1]
+    mir = [m_ for (v, rng), m_ in eng._mirrors.items() if rng == tuple(st.layer_range)]
+    assert len(mir) == 1 and torch.equal(mir[0].flat.master, st.flat.master)
 
 
 def test_byzantine_blame_goes_to_the_earliest_stage_only():

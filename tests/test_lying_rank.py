@@ -263,3 +263,52 @@ def test_gloo_lying_rank_one_of_m():
     assert got, "never caught in 12 lying steps at k/M = 1/4"
     a = res[2]["audit"]
     assert a["mirror_seeds"] == 1 and a["steps"] == 14
+
+
+# ---------------------------------------------------------------------------------------------- healing
+def _heal_worker(rank, world, port, out_path, steps):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from trustworthy_dl.attacks import AdversarialAttacker, AttackConfig
+    from trustworthy_dl.models import get_model
+    from trustworthy_dl.parallel.pipeline import EngineConfig, PipelineEngine
+    atk = AdversarialAttacker(AttackConfig(["model_poisoning"], target_nodes=[1], intensity=0.05, start_step=3,
+                                           end_step=3))
+    atk.activate_attacks()
+    m = get_model("gpt2-tiny", seq_len=32, seed=1, vocab_size=1024)
+    eng = PipelineEngine(m, EngineConfig(num_nodes=world, micro_batches=2, device="cpu", seq_len=32, monitor_seed=0,
+                                         reassign=False, audit_micro_k=1, audit_targeted=False),
+                         attacker=atk)
+    for b in _batches(steps, bs=4):
+        eng.train_step(b)
+    eng.flush()
+    st = eng.my_stage()
+    rec = {"blamed": _blamed(eng), "master": ga.root_hex(ga.merkle_root(st.flat.master)),
+           "heals": eng.audit_summary().get("heals", 0) if hasattr(eng, "audit_summary") else 0}
+    if rank == 2:   # the auditor of stage 1: its mirror's master
+        mir = [m_ for (v, rng), m_ in eng._mirrors.items() if rng == tuple(eng.plan.ranges[1])]
+        rec["mirror_of_1"] = ga.root_hex(ga.merkle_root(mir[0].flat.master))
+    with open(f"{out_path}.{rank}", "w") as f:
+        json.dump(rec, f)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_gloo_tampered_weights_healed_from_the_auditors_mirror():
+    """3 gloo ranks, stage 1's weights perturbed once (step 3, outside the optimizer), no re-shard:
+    blamed from step 3 until the step-3 report is processed (REPORT_LAG steps later), when its
+    auditor ships the mirror's verified optimizer state and the stage adopts it — no blame after
+    that, and its master weights equal the mirror's bit for bit."""
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "h")
+        mp.spawn(_heal_worker, args=(3, _free_port(), out, 9), nprocs=3, join=True)
+        res = [json.load(open(f"{out}.{r}")) for r in range(3)]
+    got = res[0]["blamed"]
+    assert all(r["blamed"] == got for r in res)
+    steps = sorted({s for s, n, _ in got})
+    assert {n for _, n, _ in got} == {1} and steps and steps[0] == 3 and steps[-1] <= 5, got
+    assert res[1]["master"] == res[2]["mirror_of_1"]

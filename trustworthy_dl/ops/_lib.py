@@ -118,6 +118,7 @@ _SIGNATURES = {
     # optim.hip
     "tdl_adamw_flat": [_P, _P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _F, _P, _I, _P],
     "tdl_fill_f32": [_P, _L, _F, _P],
+    "tdl_copy_if": [_P, _P, _P, _L, _P],
     "tdl_splitk_reduce_add": [_P, _P, _I, _L, _P],
     # stats.hip
     "tdl_tensor_stats": [_P, _I, _L, _P, _P, _I, _P],

@@ -160,14 +160,14 @@ class AttributionMixin:
 
     def _consume_reports(self, upto: Optional[int]):
         while self._pending and (upto is None or self._pending[0][0] <= upto):
-            step, epoch, host, ev, truth, lasts = self._pending.popleft()
+            step, epoch, host, ev, truth, lasts, mode = self._pending.popleft()
             note_host_sync()
             if ev is not None:
                 ev.synchronize()
-            self._process_report(step, epoch, host, truth, lasts)
+            self._process_report(step, epoch, host, truth, lasts, mode)
 
     def _process_report(self, step: int, epoch: int, host: torch.Tensor, truth: Dict[int, bool],
-                        loss_ranks: Optional[List[int]] = None):
+                        loss_ranks: Optional[List[int]] = None, mode=None):
         N = self.num_nodes
         D = host[: N * SV.DIGEST].view(N, SV.DIGEST).tolist()
         values = host[N * SV.DIGEST: N * SV.DIGEST + N].tolist()
@@ -239,6 +239,12 @@ class AttributionMixin:
                   and n not in newly and n in detections]
         if newly and self.cfg.reassign:
             self.reassign(sorted(set(newly)), step)
+        elif self.distributed and mode is not None and mode[1] and mode[0] == self.plan.version:
+            # weights proven to differ from the auditor's mirror (written outside the verified
+            # optimizer) and no re-shard: the stage takes the mirror's verified state back
+            heal = [n for n in range(N) if n in present and audit_kind[n] & SV.AK_WHASH]
+            if heal:
+                self._heal_dist(heal)
         # runtime metrics for the next digest (latency s, utilization, error, uptime)
         util = 1.0 - (self._comm_wait / self._step_time) if self._step_time > 0 else 0.0
         for n in range(N):

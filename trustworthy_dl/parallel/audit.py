@@ -211,6 +211,7 @@ class AuditMixin:
     def _mirror_update(self, D: torch.Tensor, evidence: torch.Tensor, total_sumsq: torch.Tensor):
         """Advance every mirror this rank holds with the gradient its stage shipped (verified this
         step) under the clip scale and skip decision every rank derives from the digest."""
+        self._mirror_applied = {node: mir for mir, _, node in self._mirror_pending}
         for mir, G, node in self._mirror_pending:
             ctrl = mir.verifier.ctrl
             mir.verifier.set_clip_scale(total_sumsq.to(mir.device), self.cfg.adamw.max_grad_norm)
@@ -222,6 +223,36 @@ class AuditMixin:
                 mir.flat.set_grad_buffer(saved)
             self._mirror_root_async(mir)
         self._mirror_pending = []
+
+    @torch.no_grad()
+    def _heal_from_mirror(self, node: int, st: Stage):
+        """Local mirror mode, right after ``node``'s own update: when its auditor proved this step
+        that the master weights it committed are not the mirror's (AK_WHASH: a write outside the
+        verified optimizer), the stage takes the mirror's verified optimizer state (master, moments,
+        compute weights) — device-side, no host read of the verdict: a conditional copy that does
+        nothing on a clean step.  The tampering is blamed once and does not outlive the step
+        (distributed mode: ``_heal_dist``, from the lagged host report)."""
+        mir = self._mirror_applied.get(node)
+        if mir is None or self._proof_kind is None:
+            return
+        flag = ((self._proof_kind[node:node + 1].to(torch.int64) & SV.AK_WHASH) > 0).float()
+        f, g = mir.flat, st.flat
+        pairs = [(f.master, g.master), (f.exp_avg, g.exp_avg), (f.exp_avg_sq, g.exp_avg_sq)]
+        if g.data is not g.master:
+            pairs.append((f.data, g.data))
+        if st.device.type == "cuda" and all(a.device == b.device for a, b in pairs):
+            from ..ops import _lib
+            from ..ops._lib import ptr, stream_ptr
+            fl = flag.to(st.device)
+            for src, dst in pairs:
+                _lib.call("tdl_copy_if", ptr(fl), ptr(src), ptr(dst), dst.numel() * dst.element_size(),
+                          stream_ptr(st.device))
+            return
+        if float(flag) > 0:     # CPU tensors (or mirror on another device): a host read
+            for src, dst in pairs:
+                dst.copy_(src.to(dst.device))
+            from ..ops.layers import bump_weight_generation
+            bump_weight_generation()
 
     def _mirror_root_async(self, mir: Stage):
         """Root of the mirror's master weights for the next step's weight check, taken on a side
@@ -527,7 +558,7 @@ class AuditMixin:
                 "seed_bytes": a["seed_bytes"], "mirror_seeds": a["seeds"],
                 "host_ms_per_step": 1e3 * a["host_s"] / a["steps"],
                 "device_ms_per_step": (sum(gpu) / len(gpu)) if gpu else None,
-                "memory_bytes": self.audit_memory_bytes(), "targeted_extra": len(tl)}
+                "memory_bytes": self.audit_memory_bytes(), "targeted_extra": len(tl), "heals": a.get("heals", 0)}
 
     def _audit_transfer(self, sends, recvs, prev, nxt, act_g, grad_g):
         """Audit traffic: toward the next stage on the activation communicator, toward the

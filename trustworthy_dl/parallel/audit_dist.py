@@ -340,6 +340,51 @@ class DistAuditMixin:
         self._audit_recv_dy = {}
         self._audit_outputs = {}
 
+    @torch.no_grad()
+    def _heal_dist(self, nodes: List[int]):
+        """Distributed counterpart of ``_heal_from_mirror``, run by every rank from the same lagged
+        host report (so the same steps and list on every rank): for each node whose committed master
+        weights failed its auditor's mirror check, the auditor ships its mirror's verified optimizer
+        state (master, AdamW moments) and the stage adopts it (compute weights rebuilt, integrity
+        checksum re-baselined).  Both sides are post-update at the same step, so the next commitment
+        matches.  A rank that refuses keeps failing the check (and is compromised)."""
+        S = self.plan.num_stages
+        me = self.rank
+        sends, recvs, adopt = [], [], None
+        for x in nodes:
+            sid = self.plan.stage_of_rank(x)
+            if sid is None or S < 2:
+                continue
+            aud = self.plan.ranks[sid + 1] if sid + 1 < S else self.plan.ranks[sid - 1]
+            if me == aud:
+                mir = self._audit_mirror(tuple(self.plan.ranges[sid]), sid)
+                if self._mirror_seeded(mir):
+                    sends += [(t, x) for t in (mir.flat.master, mir.flat.exp_avg, mir.flat.exp_avg_sq)]
+            elif me == x:
+                st = self.my_stage()
+                # the auditor ships only from a mirror seeded in the current epoch, which is when this
+                # stage shipped it a seed in this epoch: both sides decide alike
+                if st is not None and self._seed_mark == (self.plan.version, tuple(st.layer_range), self._mirror_epoch):
+                    recvs += [(t, aud) for t in (st.flat.master, st.flat.exp_avg, st.flat.exp_avg_sq)]
+                    adopt = st
+        if not sends and not recvs:
+            return
+        g = self._audit_pg
+        self._note_peers(sends, recvs, "audit")
+        ops = [dist.P2POp(dist.isend, t.contiguous(), r, g) for t, r in sends] + \
+              [dist.P2POp(dist.irecv, t, r, g) for t, r in recvs]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        self._audit_cost["seed_bytes"] += sum(t.numel() * t.element_size() for t, _ in recvs)
+        self._audit_cost["heals"] = self._audit_cost.get("heals", 0) + (1 if adopt is not None else 0)
+        if adopt is not None:
+            f = adopt.flat
+            if f.data is not f.master:
+                f.data.copy_(f.master)
+            from ..ops.layers import bump_weight_generation
+            bump_weight_generation()
+            adopt.param_checksum = None      # re-baselined at the next step's integrity check
+
     def _as_tensor(self, v, dtype) -> Optional[torch.Tensor]:
         """A JSON payload from a peer as a device tensor (None if it is not a rectangular number list)."""
         try:

@@ -172,6 +172,7 @@ class CommitmentMixin:
         self._tied_snapped: Dict[int, bool] = {}
         self._gsk_run: Dict[int, torch.Tensor] = {}
         self._mirror_pending = []
+        self._mirror_applied = {}
         if not self._gsk_on:
             # a step whose gradients no mirror sees: every mirror must be re-seeded before it is used
             self._invalidate_mirrors()

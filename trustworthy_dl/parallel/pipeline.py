@@ -184,6 +184,7 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
         self._gring_cache: Dict[tuple, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._mirror_epoch = 0                           # bumped on every rank when mirrors go stale
         self._mirror_pending: List = []                  # (mirror, verified gradient, node) to apply
+        self._mirror_applied: Dict[int, object] = {}     # node -> its mirror advanced this step (local heal)
         self._seed_mark = None                           # (plan, range, epoch) my auditor's mirror was seeded for
         self._tkey_trash: List[str] = []                 # store keys of last step's tie-key parts (audit_dist.py)
         self._gsk_cache: Dict[tuple, object] = {}
@@ -826,6 +827,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
                 # the weights must still be those checksummed at the start of the step
                 st._tail_flag = (dstats.checksum(st.flat.data) != cur).any().float().reshape(1)
             st.flat.adamw_step(self.cfg.adamw, ctrl=st.verifier.ctrl)
+            if self._gsk_on and not self.distributed:
+                self._heal_from_mirror(node, st)
             if self.cfg.param_integrity:
                 st.param_checksum = dstats.checksum(st.flat.data, st.param_checksum)
         self.tracer.end(to)
@@ -847,7 +850,8 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
             ev.record()
         else:
             host, ev = rep.clone(), None
-        self._pending.append((self.global_step, self.epoch, host, ev, dict(truth), list(self.last_ranks())))
+        self._pending.append((self.global_step, self.epoch, host, ev, dict(truth), list(self.last_ranks()),
+                              (self.plan.version, bool(self._gsk_on))))
 
     def close(self):
         if self.heartbeat is not None:
