@@ -28,8 +28,14 @@ __device__ __forceinline__ void unpack8(const uint4 u, float* f) {
         f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
 }
+// Two floats -> two bf16 in ONE v_cvt_pk_bf16_f32 (a vector conversion; two scalar __bf16 casts
+// compiled to two single-source conversions plus a shift and an SDWA or: 4 VALU instead of 1 — a
+// third of gemm_pd's epilogue instructions).  Bit-identical to f2bf on each element.
+typedef float tdl_f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 tdl_bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    const tdl_bf16x2_t r = __builtin_convertvector((tdl_f32x2_t){a, b}, tdl_bf16x2_t);
+    return __builtin_bit_cast(uint32_t, r);
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {
     return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));

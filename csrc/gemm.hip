@@ -1153,7 +1153,11 @@ __device__ __forceinline__ void pd_bias_load(const GemmParams& p, int nw, int la
         braw[j] = __builtin_amdgcn_raw_buffer_load_b64(rbias, n < p.N ? (uint32_t)n * 2u : 0x80000000u, 0, 0);
     }
 }
-template <int EPI, class Get>
+// BIAS = false (no bias): no adds of zeros.  At K = 1024 this epilogue is 27-37 % of the kernel
+// (the K loop alone runs 1.50-1.55 PF/s, profiles/r6_pd_epilogue_ab.jsonl); neither deferring half
+// of its stores into the next tile's first K step, nor staggering the workgroups' start, nor a
+// third fewer VALU moved it: the stores delay the next tile's copies queued behind them.
+template <int EPI, bool BIAS = true, class Get>
 __device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int mw, int nw, int lane,
                                             const u32x2_t (&braw)[8]) {
     static_assert(EPI == EPI_BF16 || EPI == EPI_GELU, "16-byte store epilogue: bf16 (+ bias), bias + GELU");
@@ -1173,8 +1177,12 @@ __device__ __forceinline__ void pd_store_x4(const GemmParams& p, Get& get, int m
             constexpr int i = decltype(ic)::value;
             const f32x4 a = get(std::integral_constant<int, i>{}, std::integral_constant<int, j>{});
             const f32x4 b = get(std::integral_constant<int, i>{}, std::integral_constant<int, j + 1>{});
-            float va[4] = {a[0] + ba[0], a[1] + ba[1], a[2] + ba[2], a[3] + ba[3]};
-            float vb[4] = {b[0] + bb[0], b[1] + bb[1], b[2] + bb[2], b[3] + bb[3]};
+            float va[4] = {a[0], a[1], a[2], a[3]};
+            float vb[4] = {b[0], b[1], b[2], b[3]};
+            if constexpr (BIAS) {   // (BIAS = false: no bias, no adds of zeros)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) va[r] += ba[r], vb[r] += bb[r];
+            }
             const uint32_t off = col == 0x80000000u ? col : lrow + (uint32_t)(16 * i) * (uint32_t)p.ldc * 2u + col;
             auto store8 = [&](const float (&xa)[4], const float (&xb)[4], const __amdgpu_buffer_rsrc_t& r) {
                 const uint2 qa = pack4(xa), qb = pack4(xb);
@@ -1285,7 +1293,7 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
 template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2,
-          bool TA = false, bool TB = false>
+          bool TA = false, bool TB = false, bool NOEPI = false>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(B1 >= 16 * RP + 2 && DS > B1 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
@@ -1294,7 +1302,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     // the first wait after an epilogue: the copies it waits for precede the epilogue's VMEM ops
     // (>= 64 per wave for the per-tile-row epilogue, exactly PD_X4_VMEM for pd_store_x4) and the NB
     // copies issued since; vmcnt counts in issue order, so vmcnt(that sum) retires exactly the copies
-    constexpr int EV = X4 ? pd_x4_vmem(EPI) : 64;
+    constexpr int EV = NOEPI ? 0 : X4 ? pd_x4_vmem(EPI) : 64;
     constexpr int NB_EPI = EV + NB < 63 ? EV + NB : 63;
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1460,8 +1468,12 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         acc_fence<48>(acc);
         __builtin_amdgcn_sched_barrier(0);
         auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
-        if constexpr (X4 && EPI == EPI_DGELU) pd_store_x4_dgelu(p, get, cm0 + wm * 128, cn0 + wn * 128, lane);
-        else if constexpr (X4) pd_store_x4<EPI>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+        if constexpr (NOEPI) {   // diagnostics only (TDL_PD_SCHED=10): the K loop without the epilogue
+        } else if constexpr (X4 && EPI == EPI_DGELU) pd_store_x4_dgelu(p, get, cm0 + wm * 128, cn0 + wn * 128, lane);
+        else if constexpr (X4) {
+            if (p.bias != nullptr) pd_store_x4<EPI, true>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+            else pd_store_x4<EPI, false>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
+        }
         else epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         __builtin_amdgcn_sched_barrier(0);
         read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
@@ -1514,12 +1526,13 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
     GemmParams p{(const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (bf16_t*)aux, colsum, M, N, K,
                  lda, ldb, ldc, kps, split_stride, (N + BN - 1) / BN, 0, split, 0, g_gemm_ts};
     {
-        // tile order: groups of 8 tile rows for the wide (N >= 4096) products, where the 32 CUs of
-        // an XCD then share an 8 x 4 block of A / B panels (fc forward +7-8 %, interleaved A/B,
-        // profiles/r5_gemm_order_ring_ab.jsonl); row-major elsewhere (within noise).
-        // TDL_GEMM_GROUPM overrides (read per launch: in-process A/B)
+        // tile order: groups of 8 tile rows, so the 32 CUs of an XCD share a block of at most 8 A
+        // panels x 4 B panels (fc forward +7-8 %, profiles/r5_gemm_order_ring_ab.jsonl; the
+        // weight gradients: qkv / out / fc +2-4 %, profiles/r6_wgrad_ab.jsonl — with 4 tile rows
+        // the row-major walk spans every B panel).  TDL_GEMM_GROUPM overrides (read per launch:
+        // in-process A/B)
         const char* g = std::getenv("TDL_GEMM_GROUPM");
-        p.group_m = g ? std::atoi(g) : (p.tiles_n >= 16 ? 8 : 0);
+        p.group_m = g ? std::atoi(g) : 8;
     }
     p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
 #ifdef TDL_GEMM_ISA_ONLY  // inspection builds: one instantiation (scripts/isa_p4.sh)
@@ -1559,6 +1572,7 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
                 case 7: gemm_pd<0, 1, 26, 6, 100, true, 0, 24><<<grid, PNTHR, 0, s>>>(p); break;
                 case 8: gemm_pd<0, 1, 24, 6, 100, true, 0, 22><<<grid, PNTHR, 0, s>>>(p); break;
                 case 9: gemm_pd<0, 1, 30, 6, 104, true, 0, 28><<<grid, PNTHR, 0, s>>>(p); break;
+                case 10: gemm_pd<0, 1, 20, 7, 100, true, 0, 18, false, false, true><<<grid, PNTHR, 0, s>>>(p); break;
                 default: gemm_pd<0, 1, 20, 7, 108><<<grid, PNTHR, 0, s>>>(p); break;
             }
             TDL_LAUNCH_CHECK();

@@ -66,11 +66,18 @@ def test_engine_never_uses_stale_forward_weights(monkeypatch):
     # every cached copy equals its parameter after the last (native AdamW) update
     monkeypatch.setenv("TDL_FWD_WEIGHT_T", "1")
     eng.eval_step(batches[3])
+    from trustworthy_dl.ops import layers as L
     n = 0
     for st in eng.stages.values():
         for p in st.module.parameters():
             c = getattr(p, "_tdl_fwd_t", None)
-            if c is not None:
+            if c is None:
+                continue
+            if c[0][0] == L._WEIGHT_GEN[0]:      # built for the current weights (this forward)
                 assert torch.equal(c[1].t(), p.detach()), "stale forward-layout copy"
                 n += 1
+            else:   # the tied LM-head copy (built by the last backward's dX): refreshed on its next use
+                with torch.no_grad():
+                    assert torch.equal(B.fwd_weight(p), p.detach())
+                assert p._tdl_fwd_t[0][0] == L._WEIGHT_GEN[0]
     assert n == 4 * 4, n   # 4 blocks x 4 GEMM weights

@@ -639,6 +639,40 @@ def test_fused_lm_head_cross_entropy_matches_fp32(chunk):
     assert _rel(w2.main_grad, wr.grad) < 2e-2
 
 
+def test_lm_head_gpt2_vocab_native_dx_matches_fp32():
+    """GPT-2 vocab (V = 50257 padded to 50304, ignored labels): dX runs on gemm_pd over the cached
+    [n, Vp] copy of the tied weight (layers._lmhead_dx); loss / dX / dW vs fp32, and the copy is
+    rebuilt after the weight changes (new weight generation)."""
+    from trustworthy_dl.ops import gemm
+    from trustworthy_dl.ops.layers import _lmhead_dx, bump_weight_generation, fwd_weight, lm_head_cross_entropy
+    torch.manual_seed(3)
+    N, n, V, Vp = 512, 1024, 50257, 50304
+    x = (torch.randn(N, n, device=DEV) * 0.5).bfloat16().requires_grad_(True)
+    w = (torch.randn(Vp, n, device=DEV) * 0.05).bfloat16()
+    w[V:] = 0
+    w.requires_grad_(True)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::5] = -100
+    assert gemm.supported(torch.empty(N, Vp, dtype=torch.bfloat16, device=DEV), fwd_weight(w.detach()))
+    loss = lm_head_cross_entropy(x, w, labels, V)
+    loss.backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy((xr @ wr.t())[:, :V], labels, ignore_index=-100)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 2e-3 * float(ref)
+    assert _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    # the direct product and a changed weight (the cached transposed copy must follow it)
+    dl = (torch.randn(N, Vp, device=DEV) * 1e-3).bfloat16()
+    with torch.no_grad():
+        assert _rel(_lmhead_dx(dl, w.detach()), dl.float() @ w.detach().float()) < 1e-2
+        w2 = w.detach()
+        w2.mul_(-1.0)
+        bump_weight_generation()
+        assert _rel(_lmhead_dx(dl, w2), dl.float() @ w2.float()) < 1e-2
+
+
 @pytest.mark.parametrize("V,ld", [(50257, 50304), (32000, 32000), (1000, 1024)])
 def test_xent_fused_rows_vs_fp32(V, ld):
     """tdl_xent_fused on full GPT-2-vocab rows, a 32k vocab and a small padded row: loss, lse and

@@ -86,10 +86,12 @@ def _launch(a, b, c, ldc, epi, bias=None, aux=None, colsum=None, split=1, split_
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           epi: str = "none", aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+           epi: str = "none", aux: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None,
+           kernel: Optional[str] = None) -> torch.Tensor:
     """bf16 ``epi(a @ b)``.  ``epi='gelu'`` needs ``aux`` (receives the pre-activation, shape of the
     output); ``'resadd'`` adds into ``out``; ``'dgelu'`` reads the pre-activation from ``aux`` and
-    accumulates the column sums of the result into ``colsum`` (fp32) when given."""
+    accumulates the column sums of the result into ``colsum`` (fp32) when given.  ``kernel``
+    overrides the per-epilogue choice (``KERNELS``)."""
     M, K = a.shape
     N = b.shape[1]
     if out is None:
@@ -102,8 +104,9 @@ def matmul(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None
         raise ValueError(f"{epi} needs aux with the output's layout")
     if epi == "dgelu" and _operand_a(a)[0]:
         raise ValueError("dgelu needs a row-major A (rows past M must read as zero for the column sums)")
-    _launch(a, b, out, out.stride(0), epi, bias=bias, aux=aux, colsum=colsum,
-            kernel=(GELU_KERNEL or None) if epi == "gelu" else (DGELU_KERNEL or None) if epi == "dgelu" else None)
+    if kernel is None:
+        kernel = (GELU_KERNEL or None) if epi == "gelu" else (DGELU_KERNEL or None) if epi == "dgelu" else None
+    _launch(a, b, out, out.stride(0), epi, bias=bias, aux=aux, colsum=colsum, kernel=kernel)
     return out
 
 

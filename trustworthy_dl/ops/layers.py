@@ -524,6 +524,19 @@ def _scale_bf16(x: torch.Tensor, y: torch.Tensor, g: torch.Tensor):
         torch.mul(x, g.reshape(()), out=y)
 
 
+def _lmhead_dx(dl: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dX = dL @ W (W = wte [Vp, n]) on the persistent LDS-DMA kernel (gemm_pd) over a [n, Vp] copy
+    of W (``fwd_weight``: one native transpose per weight generation, ~30 us): the NT form of the
+    product runs 4565 vs 5004 us for the library's at the bench shape (profiles/r6_lmhead_ab.jsonl).
+    ``TDL_LMHEAD_DX=lib`` keeps the library GEMM (A/B switch)."""
+    from . import gemm
+    if os.environ.get("TDL_LMHEAD_DX", "pd") == "pd" and dl.is_cuda:
+        wt = fwd_weight(weight)       # logical [Vp, n], stored [n][Vp]: k-contiguous
+        if gemm.supported(dl, wt):
+            return gemm.matmul(dl, wt, kernel="pd")
+    return torch.mm(dl, weight)
+
+
 class _LMHeadXent(torch.autograd.Function):
     """loss = mean CE(x @ W^T, labels) with W = wte [Vp, n] tied; padded vocab columns masked.
 
@@ -592,7 +605,7 @@ class _LMHeadXent(torch.autograd.Function):
             gf = g.float().reshape(1).contiguous()
             dx = None
             if ctx.needs_input_grad[0]:
-                dx = torch.mm(dl, weight)
+                dx = _lmhead_dx(dl, weight)
                 _scale_bf16(dx, dx, gf)
             xg = torch.empty_like(x2)
             _scale_bf16(x2, xg, gf)
