@@ -298,6 +298,7 @@ def run(args):
     tokens = global_batch * args.seq_len * args.steps
     tps = tokens / elapsed
     if rank == 0:
+        from trustworthy_dl.ops import gemm as gemm_mod
         line = {
             "metric": _metric(args),
             "value": round(tps, 1), "unit": "tokens/s", "n_gpus": N, "steps": args.steps,
@@ -314,8 +315,9 @@ def run(args):
                        "detections": len(engine.attack_history),
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
-                       "native_gemm": "fc fwd+gelu (pd), proj dgrad+dgelu (pp), all weight gradients (p4)",
-                       "native_wgrad": os.environ.get("TDL_WGRAD_KERNEL", "p4"),
+                       "native_gemm": "fc fwd+gelu (pd), proj dgrad+dgelu (pp), LM-head dX (pd), all weight gradients "
+                                      f"({gemm_mod.WGRAD_KERNEL})",
+                       "native_wgrad": gemm_mod.WGRAD_KERNEL,
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        # per-rank RCCL communicators / HIP streams (compute + verification + one per
                        # communicator) vs the hardware-queue budget (PipelineEngine.comm_inventory)

@@ -1362,8 +1362,20 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         const uint32_t vo = i < 8 ? sa.base[TR ? (j & 1) : 0] : sb.base[TR ? (j & 1) : 0];
         const uint32_t dl = i < 8 ? sa.delta : sb.delta;
         char* dst = stage + (i < 8 ? 0 : TILE_BYTES) + (w + 4 * j) * 1024;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 8 ? qa : qb, (lds_void_t*)dst, 16, vo,
-                                                 __builtin_amdgcn_readfirstlane((uint32_t)j * dl), 0, 0);
+        if constexpr (TR) {
+            // Row-contiguous images are read with ds_read_b64_tr_b16, whose builtin hipcc cannot tell
+            // apart from the DMA's destination: it drained every copy in flight (s_waitcnt vmcnt(0))
+            // in front of the transposed reads, 10 times per K step — 62 % of the wave cycles parked,
+            // 0.62x gemm_p4 (profiles/r6_pmc_wgrad_pd.txt).  Issued from asm, the copy is invisible
+            // to that alias check; its completion is still counted by the explicit vmcnt waits.
+            const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void_t*)dst);
+            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)j * dl);
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                         :: "s"(la), "v"(vo), "s"(i < 8 ? qa : qb), "s"(so) : "memory", "m0");
+        } else {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 8 ? qa : qb, (lds_void_t*)dst, 16, vo,
+                                                     __builtin_amdgcn_readfirstlane((uint32_t)j * dl), 0, 0);
+        }
     };
     auto frag_base = [&](bool isB, int buf, int ks) -> uint32_t {
         const int wb = isB ? wn : wm;

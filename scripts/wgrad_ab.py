@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--nt", type=int, default=1)
+    ap.add_argument("--pd", type=int, default=0, help="also the LDS-DMA kernel (gemm_pd TT) at the default split")
     ap.add_argument("--out", default="gpurun_out/r6_wgrad_ab.jsonl")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
@@ -59,6 +60,11 @@ def main():
                 os.environ["TDL_GEMM_GROUPM"] = g
                 gemm.matmul_f32_acc(acc, x.t(), dy)
             variants[f"tt_g{g}"] = run
+        if a.pd:
+            def run_pd():
+                os.environ.pop("TDL_GEMM_GROUPM", None)
+                gemm.matmul_f32_acc(acc, x.t(), dy, kernel="pd")
+            variants["tt_pd"] = run_pd
         if a.nt:
             xt = x.t().contiguous()     # [M][K]
             dyt = dy.t().contiguous()   # [N][K]
@@ -67,6 +73,11 @@ def main():
                 os.environ.pop("TDL_GEMM_GROUPM", None)
                 gemm.matmul_f32_acc(acc, xt, dyt.t())
             variants["nt"] = run_nt
+            if a.pd:
+                def run_nt_pd():
+                    os.environ.pop("TDL_GEMM_GROUPM", None)
+                    gemm.matmul_f32_acc(acc, xt, dyt.t(), kernel="pd")
+                variants["nt_pd"] = run_nt_pd
         # correctness of every variant once
         bad = {}
         for k, fn in variants.items():

@@ -120,17 +120,37 @@ def test_dgelu_rejects_transposed_a():
                     colsum=torch.zeros(256, device=DEV))
 
 
+@pytest.mark.parametrize("kernel", ["p4", "pd"])
 @pytest.mark.parametrize("mode,split", [("slab", None), ("atomic", 4), ("slab", 1), ("slab", 3)])
-def test_wgrad_f32(mode, split):
+def test_wgrad_f32(mode, split, kernel):
     from trustworthy_dl.ops import gemm
     Mt, K, N = 4096, 256, 512          # tokens, in, out
     x = _rand(Mt, K)
     dy = _rand(Mt, N)
     acc = torch.randn(K, N, device=DEV)
     base = acc.clone()
-    gemm.matmul_f32_acc(acc, x.t(), dy, split=split, mode=mode)
+    gemm.matmul_f32_acc(acc, x.t(), dy, split=split, mode=mode, kernel=kernel)
     ref = base + x.float().t() @ dy.float()
     assert _rel(acc - base, ref - base) < 2e-3
+
+
+@pytest.mark.parametrize("Mt,K,N,split", [(65536, 1024, 3072, 16), (65536, 4096, 1024, 4), (4096, 1000, 264, 2),
+                                          (16384, 50304, 1024, 4)])
+def test_wgrad_pd_transposed_operands(Mt, K, N, split):
+    """The LDS-DMA kernel on the weight-gradient layout (both operands row-contiguous, read with
+    ds_read_b64_tr_b16; copies issued from asm): production shapes, ragged tiles, the LM head."""
+    from trustworthy_dl.ops import gemm
+    x = _rand(Mt, K)
+    dy = _rand(Mt, N, scale=0.1)
+    acc = torch.randn(K, N, device=DEV)
+    ref = acc + x.float().t() @ dy.float()
+    gemm.matmul_f32_acc(acc, x.t(), dy, split=split, kernel="pd")
+    assert float((acc - ref).norm() / ref.norm()) < 1e-4
+    acc2 = torch.zeros(K, N, device=DEV)   # bit-identical to a second run (deterministic split reduce)
+    acc3 = torch.zeros(K, N, device=DEV)
+    gemm.matmul_f32_acc(acc2, x.t(), dy, split=split, kernel="pd")
+    gemm.matmul_f32_acc(acc3, x.t(), dy, split=split, kernel="pd")
+    assert torch.equal(acc2, acc3)
 
 
 # every product the engine routes to a native kernel, at the production shape (64k tokens)

@@ -35,7 +35,11 @@ KERNEL = os.environ.get("TDL_GEMM_KERNEL", "pp")        # bf16-output products (
 # per step over the ping-pong kernel, 3 of 3 interleaved rounds (profiles/r5_gemm_pd_gelu_ab.txt)
 GELU_KERNEL = os.environ.get("TDL_GEMM_GELU_KERNEL", "pd")
 DGELU_KERNEL = os.environ.get("TDL_GEMM_DGELU_KERNEL", "")   # the dGELU product (proj dgrad); "" = KERNEL
-WGRAD_KERNEL = os.environ.get("TDL_WGRAD_KERNEL", "p4")  # fp32 weight-gradient products
+# fp32 weight-gradient products (both operands row-contiguous: transposed LDS reads) on the LDS-DMA
+# kernel: 7-10 % faster than the register-staged gemm_p4 on every GPT-2-medium weight gradient at
+# 64k tokens once its copies stopped being drained in front of the transposed reads
+# (profiles/r6_wgrad_pd_ab.jsonl)
+WGRAD_KERNEL = os.environ.get("TDL_WGRAD_KERNEL", "pd")
 
 
 def _operand_a(a: torch.Tensor):
