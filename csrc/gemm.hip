@@ -1293,7 +1293,7 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
 template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2,
-          bool TA = false, bool TB = false, bool NOEPI = false>
+          bool TA = false, bool TB = false, bool NOEPI = false, bool NOBIAS = false>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(B1 >= 16 * RP + 2 && DS > B1 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
@@ -1425,7 +1425,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         constexpr bool ZERO = decltype(zc)::value, LAST = decltype(lc)::value;
         const int cur = s & 1, nxt = cur ^ 1;
         char* cstage = smem + cur * STAGE_BYTES;
-        if constexpr (X4 && LAST && EPI != EPI_DGELU) pd_bias_load(p, bias_n0, lane, braw);   // ahead of this step's copies
+        if constexpr (X4 && LAST && EPI != EPI_DGELU && !NOBIAS) pd_bias_load(p, bias_n0, lane, braw);   // ahead of this step's copies
         produce_rsrc();
         auto slot = [&](auto gc, const uint32_t* fb) {
             constexpr int g = decltype(gc)::value;
@@ -1482,10 +1482,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         auto get = [&](auto ic, auto jc) { return acc[8 * decltype(ic)::value + decltype(jc)::value]; };
         if constexpr (NOEPI) {   // diagnostics only (TDL_PD_SCHED=10): the K loop without the epilogue
         } else if constexpr (X4 && EPI == EPI_DGELU) pd_store_x4_dgelu(p, get, cm0 + wm * 128, cn0 + wn * 128, lane);
-        else if constexpr (X4) {
-            if (p.bias != nullptr) pd_store_x4<EPI, true>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
-            else pd_store_x4<EPI, false>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
-        }
+        else if constexpr (X4) pd_store_x4<EPI, !NOBIAS>(p, get, cm0 + wm * 128, cn0 + wn * 128, lane, braw);
         else epilogue_store<EPI, 8>(p, get, cm0 + wm * 128, cn0 + wn * 128, csp, lane);
         __builtin_amdgcn_sched_barrier(0);
         read_f0(s & 1);  // the next tile's first k-half (its copies were waited for in the last step)
@@ -1556,7 +1553,15 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
 #ifndef P4_LEPI
 #define P4_LEPI false
 #endif
+#ifdef PD_ISA   // the 16-byte-store gemm_pd epilogues instead (register / spill inspection)
+    gemm_pd<EPI_BF16, 1, 20, 7, 100, true><<<256, PNTHR, 0, s>>>(p);
+    gemm_pd<EPI_BF16, 1, 20, 7, 100, true, 0, 18, false, false, false, true><<<256, PNTHR, 0, s>>>(p);
+    gemm_pd<EPI_GELU, 1, 20, 7, 100, true><<<256, PNTHR, 0, s>>>(p);
+    gemm_pd<EPI_DGELU, 1, 20, 7, 100, true><<<256, PNTHR, 0, s>>>(p);
+    gemm_pd<EPI_F32, 1, 20, 7, 100, false, 0, 18, true, true><<<256, PNTHR, 0, s>>>(p);
+#else
     gemm_p4<P4_TA, P4_TB, P4_EPI, P4_LEPI><<<256, PNTHR, 0, s>>>(p);
+#endif
     TDL_LAUNCH_CHECK();
 #else
     if (kernel == 3) {  // gemm_pd: NT operands, or TT (the weight gradients) with fp32 outputs
@@ -1592,7 +1597,11 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
         const char* xe = std::getenv("TDL_PD_X4");   // "0": per-tile-row stores (A/B)
         const bool x4 = (N % 8 == 0) && (ldc % 8 == 0) && ((uintptr_t)C % 16 == 0) && !(xe && xe[0] == '0');
         if ((epi == EPI_BF16 || epi == EPI_GELU || epi == EPI_DGELU) && x4 && (epi == EPI_BF16 || (uintptr_t)aux % 16 == 0)) {
-            if (epi == EPI_BF16) gemm_pd<EPI_BF16, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
+            // (a bias / no-bias branch inside one kernel pushed it past 256 VGPRs: 13 spills whose
+            // reloads drained every copy in flight, so the two are separate instantiations)
+            if (epi == EPI_BF16 && bias == nullptr)
+                gemm_pd<EPI_BF16, 1, 20, 7, 100, true, 0, 18, false, false, false, true><<<grid, PNTHR, 0, s>>>(p);
+            else if (epi == EPI_BF16) gemm_pd<EPI_BF16, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             else if (epi == EPI_GELU) gemm_pd<EPI_GELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             else gemm_pd<EPI_DGELU, 1, 20, 7, 100, true><<<grid, PNTHR, 0, s>>>(p);
             TDL_LAUNCH_CHECK();
