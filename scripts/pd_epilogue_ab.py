@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--staggers", default="", help="extra gemm_pd variants: TDL_PD_STAGGER values, ';'-separated")
     ap.add_argument("--noepi", type=int, default=1)
+    ap.add_argument("--kernels", default="", help="extra native kernels to time (p4, p4l, pp), comma-separated")
     ap.add_argument("--envs", default="", help="extra gemm_pd variants 'name:VAR=V,VAR2=V;...' (env per launch)")
     ap.add_argument("--out", default="gpurun_out/r6_pd_epilogue_ab.jsonl")
     a = ap.parse_args()
@@ -67,6 +68,10 @@ def main():
         variants = {"lib": lambda: torch.mm(x, w.t(), out=y), "pd": pd("")}
         if a.noepi:
             variants["pd_noepi"] = pd("10")
+        for kn in [t for t in a.kernels.split(",") if t]:
+            def run_kn(kn=kn):
+                gemm.matmul(x, w.t(), out=y, kernel=kn)
+            variants[kn] = run_kn
         for st in [t for t in a.staggers.split(";") if t]:
             variants[f"pd_st{st}"] = pd("", st)
         for spec in [t for t in a.envs.split(";") if t]:

@@ -364,8 +364,14 @@ class PipelineEngine(ScheduleMixin, CommitmentMixin, AuditMixin, DistAuditMixin,
                     prm = st.local_param(li, attr)
                     if prm is not None:
                         tied.add(id(prm))
+        # the split-K reduce of the last micro-batch's weight gradients may complete main_grad on
+        # the verifier's side stream (stage.py _arm_sinks) only where nothing else reads the
+        # gradient before the step tail joins that stream: no commitments / audit, no replicas, no
+        # gradient attacker
+        side_ok = (not (self.cfg.audit and self.plan.num_stages > 1) and self.dp == 1 and self.attacker is None)
         for st in self.stages.values():
             st.set_early_stats(tied)
+            st.side_reduce_ok = side_ok
             # early tied all-reduce only with hardware queues to spare (the p2p "async" mode): its
             # RCCL kernel waits on a stream of its own for the embedding stage, and on a queue
             # shared with the compute stream it would block the rest of this stage's backward

@@ -139,27 +139,51 @@ class Stage:
                     lo = b
             self._layer_seg_runs[li] = runs
 
+    def _fused_mode(self) -> str:
+        """Where the last micro-batch's split-K weight-gradient reduce runs (TDL_FUSED_GRAD_STATS):
+        "side" — fused with the verifier's statistics (ops/stats.py reduce_partial) on the
+        verifier's side stream, so the compute stream carries neither (only where nothing reads
+        the gradient before the step tail: ``side_reduce_ok``, set by the engine; measured 0.4 %
+        slower than "0": the reduce traffic then competes with the backward's GEMMs,
+        profiles/r6_side_reduce_ab.txt); "1" — fused, on the compute stream (1.4 % slower:
+        profiles/r3_fused_grad_stats_ab.txt); "0" (default) — a reduce pass on the compute stream
+        and the statistics on the side stream."""
+        m = os.environ.get("TDL_FUSED_GRAD_STATS", "0")
+        if m == "auto":
+            m = "side" if getattr(self, "side_reduce_ok", False) and self.verifier.side is not None else "0"
+        return m
+
     def _arm_sinks(self, runner_idx: int):
         """Autograd hook body: runner ``runner_idx`` is about to run its backward for the step's
         last micro-batch -> arm the verifier's fused split-K reduce on its (untied) weight
-        gradients: that backward's weight-gradient GEMM then completes each gradient and takes its
-        statistics in one kernel (ops/stats.py reduce_partial), instead of a reduce pass plus a
-        side-stream pass re-reading the final gradient.  Opt-in (TDL_FUSED_GRAD_STATS=1): it saves
-        the re-read but puts the statistics on the compute stream, and measured 1.4 % slower per
-        step than the overlapped side-stream pass (GPT-2-medium N=1, 3 interleaved rounds:
-        profiles/r3_fused_grad_stats_ab.txt)."""
+        gradients: that backward's weight-gradient GEMM then hands its fp32 slabs to one kernel
+        that completes each gradient and takes its statistics (ops/stats.py reduce_partial),
+        instead of a reduce pass plus a side-stream pass re-reading the final gradient."""
         gs = self.verifier.grad_stats
-        if gs is None or not self.verifier.verify_on or os.environ.get("TDL_FUSED_GRAD_STATS", "0") != "1":
+        mode = self._fused_mode()
+        if gs is None or not self.verifier.verify_on or mode == "0":
             return
+        sink = self._fused_sink_side if mode == "side" else self._fused_sink
         for li in self._runner_layer_idx[runner_idx]:
             for lo, hi in self._layer_seg_runs.get(li, []):
                 for j in range(lo, hi):
                     mg = getattr(self.flat.params[j], "main_grad", None)
                     if mg is not None and mg.dim() == 2:
-                        mg._tdl_stats_sink = functools.partial(self._fused_sink, j)
+                        mg._tdl_stats_sink = functools.partial(sink, j)
 
     def _fused_sink(self, seg: int, slabs, nsplit: int) -> bool:
         return self.verifier.grad_stats.reduce_partial(self.flat.grad, seg, slabs, nsplit)
+
+    def _fused_sink_side(self, seg: int, slabs, nsplit: int) -> bool:
+        """The fused reduce on the verifier's side stream, ordered after the GEMM that wrote the
+        slabs; the slabs stay allocated until it ran; ``finish_step`` joins the stream before
+        anything reads the gradient."""
+        side = self.verifier.side
+        side.wait_stream(torch.cuda.current_stream(slabs.device))
+        with torch.cuda.stream(side):
+            ok = self.verifier.grad_stats.reduce_partial(self.flat.grad, seg, slabs, nsplit)
+        slabs.record_stream(side)
+        return ok
 
     def _grad_ready(self, runner_idx: int):
         """Autograd hook body: runner ``runner_idx``'s backward (incl. weight gradients) of the
