@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--splits", default="1,2,4,8,16")
     ap.add_argument("--products", default="qkv,o,fc,proj")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--kernel", default=None, help="p4 | pd (default: ops.gemm.WGRAD_KERNEL)")
     ap.add_argument("--out", default="gpurun_out/r6_wgrad_split_sweep.jsonl")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
@@ -42,16 +43,17 @@ def main():
                 if gemm.effective_split(K, S) != S:
                     continue
                 for _ in range(3):
-                    gemm.matmul_f32_acc(acc, x.t(), dy, split=S)
+                    gemm.matmul_f32_acc(acc, x.t(), dy, split=S, kernel=a.kernel)
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(a.iters):
-                    gemm.matmul_f32_acc(acc, x.t(), dy, split=S)
+                    gemm.matmul_f32_acc(acc, x.t(), dy, split=S, kernel=a.kernel)
                 e.record()
                 e.synchronize()
                 us = s.elapsed_time(e) * 1e3 / a.iters
-                rec = {"product": name, "M": M, "N": N, "K": K, "split": S, "us": round(us, 1),
+                rec = {"product": name, "kernel": a.kernel or gemm.WGRAD_KERNEL, "M": M, "N": N, "K": K, "split": S,
+                       "us": round(us, 1),
                        "tflops": round(2.0 * M * N * K / us / 1e6, 1), "default_split": default}
                 best = rec if best is None or us < best["us"] else best
                 print(json.dumps(rec), flush=True)

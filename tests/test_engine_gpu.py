@@ -46,7 +46,8 @@ def test_serialized_streams_match_overlapped():
     _, l0, d0, w0 = _run(serialize_streams=False, output_check="first")
     _, l1, d1, w1 = _run(serialize_streams=True, output_check="first")
     assert l0 == pytest.approx(l1, rel=1e-6)
-    assert torch.allclose(d0, d1, rtol=1e-5, atol=1e-6), (d0 - d1).abs().max()
+    bad = ((d0 - d1).abs() > 1e-6 + 1e-5 * d1.abs()).nonzero().tolist()
+    assert not bad, [(i, j, float(d0[i, j]), float(d1[i, j])) for i, j in bad[:8]]
     # weights: fp32 atomics in the embedding / column-sum backward make the last bits run-order dependent
     assert torch.allclose(w0, w1, rtol=1e-4, atol=1e-6), (w0 - w1).abs().max()
 
@@ -75,7 +76,8 @@ def test_early_grad_stats_match_final_pass():
     _, l0, d0, w0 = _run(early_grad_stats=True, output_check="first")
     _, l1, d1, w1 = _run(early_grad_stats=False, output_check="first")
     assert l0 == pytest.approx(l1, rel=1e-6)
-    assert torch.allclose(d0, d1, rtol=1e-5, atol=1e-6), (d0 - d1).abs().max()
+    bad = ((d0 - d1).abs() > 1e-6 + 1e-5 * d1.abs()).nonzero().tolist()
+    assert not bad, [(i, j, float(d0[i, j]), float(d1[i, j])) for i, j in bad[:8]]
 
 
 def test_early_grad_stats_actually_split():

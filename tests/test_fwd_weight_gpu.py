@@ -80,4 +80,26 @@ def test_engine_never_uses_stale_forward_weights(monkeypatch):
                 with torch.no_grad():
                     assert torch.equal(B.fwd_weight(p), p.detach())
                 assert p._tdl_fwd_t[0][0] == L._WEIGHT_GEN[0]
-    assert n == 4 * 4, n   # 4 blocks x 4 GEMM weights
+    assert n >= 4 * 4, n   # 4 blocks x 4 GEMM weights (+ the tied LM-head copy, prebuilt at the forward)
+
+
+def test_prebuild_fwd_weights_batched_matches_lazy():
+    """The batched rebuild (one tdl_transpose_bf16_batch launch per 64 weights, ops/layers.py
+    prebuild_fwd_weights) refreshes exactly the stale copies fwd_weight built before, to the same
+    values; weights without a copy, or with shapes the kernel does not take, are left to fwd_weight."""
+    from trustworthy_dl.ops import layers as L
+    shapes = [(1024, 3072), (1024, 1024), (4096, 1024), (64, 128)] * 20 + [(192, 64), (100, 64)]
+    ws = [(torch.randn(*s, device="cuda") * 0.02).to(torch.bfloat16) for s in shapes]
+    for w in ws[:-1]:
+        B.fwd_weight(w)                  # lazily built copies (the 100 x 64 one never gets one)
+    L.bump_weight_generation()
+    for w in ws:
+        w.mul_(-1.5)
+    L.bump_weight_generation()
+    L.prebuild_fwd_weights(ws)
+    torch.cuda.synchronize()
+    for w in ws[:-1]:
+        key, wt = w._tdl_fwd_t
+        assert key[0] == L._WEIGHT_GEN[0] and torch.equal(wt.t(), w)
+        assert B.fwd_weight(w).data_ptr() == wt.data_ptr()   # cache hit: no rebuild
+    assert getattr(ws[-1], "_tdl_fwd_t", None) is None

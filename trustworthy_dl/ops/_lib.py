@@ -79,6 +79,14 @@ class LayoutBatch(ctypes.Structure):
                 ("RS", ctypes.c_int * 32), ("n", ctypes.c_int)]
 
 
+class TransposeBatch(ctypes.Structure):
+    """csrc/norm_act.hip TransposeBatch (passed by value): up to 64 bf16 [R, C] -> [C, R] jobs;
+    ``first[j]`` = first 64 x 64 tile of job j, ``first[n]`` = total tiles."""
+    MAX = 64
+    _fields_ = [("inp", ctypes.c_void_p * 64), ("out", ctypes.c_void_p * 64), ("R", ctypes.c_int * 64),
+                ("C", ctypes.c_int * 64), ("first", ctypes.c_int * 65), ("n", ctypes.c_int)]
+
+
 class BnFin(ctypes.Structure):
     """csrc/conv.hip BnFin: a folded BatchNorm finalized by the producing convolution's kernels."""
     _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("save_mean", ctypes.c_void_p),
@@ -110,6 +118,7 @@ _SIGNATURES = {
     "tdl_colsum_f32": [_P, _I, _I, _I, _P, _P],
     "tdl_colsum_bf16": [_P, _P, _I, _I, _P, _P],
     "tdl_transpose_bf16": [_P, _P, _I, _I, _P],
+    "tdl_transpose_bf16_batch": [TransposeBatch, _P],
     # xent.hip
     "tdl_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
     "tdl_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _F, _P],

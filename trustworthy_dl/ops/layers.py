@@ -184,6 +184,38 @@ def fwd_weight(w: torch.Tensor) -> torch.Tensor:
     return wt.t()
 
 
+def prebuild_fwd_weights(weights) -> None:
+    """Rebuild every stale forward-layout copy among ``weights`` (those ``fwd_weight`` has built
+    before: the block projections and the tied LM-head weight) in batched native launches
+    (tdl_transpose_bf16_batch, 64 weights per launch) instead of one launch per weight at its first
+    use; the pipeline stage calls this at the head of each forward (parallel/stage.py).  Same copies
+    and cache as ``fwd_weight``."""
+    if not _fwd_layout_enabled():
+        return
+    todo = []
+    for w in weights:
+        cached = getattr(w, "_tdl_fwd_t", None)
+        if cached is None or not w.is_cuda:
+            continue
+        key = (_WEIGHT_GEN[0], w._version, w.data_ptr())
+        R, C = w.shape
+        if (cached[0] != key and w.dtype == torch.bfloat16 and w.is_contiguous() and R % 64 == 0 and C % 64 == 0
+                and cached[1].shape == (C, R)):
+            todo.append((w, cached[1], key))
+    for i in range(0, len(todo), _lib.TransposeBatch.MAX):
+        chunk = todo[i:i + _lib.TransposeBatch.MAX]
+        b = _lib.TransposeBatch()
+        b.n = len(chunk)
+        t = 0
+        for j, (w, wt, key) in enumerate(chunk):
+            R, C = w.shape
+            b.inp[j], b.out[j], b.R[j], b.C[j], b.first[j] = w.data_ptr(), wt.data_ptr(), R, C, t
+            t += (R // 64) * (C // 64)
+            w._tdl_fwd_t = (key, wt)
+        b.first[len(chunk)] = t
+        _lib.call("tdl_transpose_bf16_batch", b, stream_ptr(chunk[0][0].device))
+
+
 def _gemm_backend(t: torch.Tensor) -> str:
     return "gpu" if t.is_cuda else "cpu"
 

@@ -26,7 +26,12 @@ _ws_cache = {}
 
 
 def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    """Persistent scratch of the statistics kernels, one per (device, current stream): two stages
+    sharing a GPU (local mode) run their output statistics on their own side streams concurrently,
+    and a per-device buffer let them overwrite each other's partials (flaky output mean / std in the
+    digests: tests/test_engine_gpu.py serialized-vs-overlapped, 2 of 6 suite runs)."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(torch.device("cuda", idx)).cuda_stream)
     w = _ws_cache.get(key)
     if w is None or w.numel() < nbytes:
         w = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)

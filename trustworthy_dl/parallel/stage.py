@@ -228,6 +228,12 @@ class Stage:
             if cw:   # their kernel layouts for this weight generation, batched (ops/conv.py)
                 from ..ops.conv import prebuild_layouts
                 prebuild_layouts(cw)
+            mw = getattr(self, "_matrix_weights", None)
+            if mw is None:   # 2-D weights: their forward-layout copies, batched (ops/layers.py)
+                mw = self._matrix_weights = [p for p in self.module.parameters() if p.dim() == 2]
+            if mw and os.environ.get("TDL_FWD_PREBUILD", "1") != "0":   # (A/B switch)
+                from ..ops.layers import prebuild_fwd_weights
+                prebuild_fwd_weights(mw)
         arm = arm_grad_stats and getattr(self, "_layer_seg_runs", None) is not None
         for k, layer in enumerate(layers[:-1]):
             if arm and x.requires_grad:
