@@ -116,7 +116,27 @@ __global__ __launch_bounds__(256) void xent_fused_kernel(bf16_t* __restrict__ lo
     bf16_t* lr = logits + (size_t)row * ld;
     float m = -INFINITY, s = 0.f;
     const int nvec = V / 8;
-    for (int i = threadIdx.x; i < nvec; i += 256) {
+    // four 16-B loads per lane in flight per trip (one at a time left each block latency-bound:
+    // ~4.2 TB/s over the row's read / re-read / write)
+    int i0 = threadIdx.x;
+    for (; i0 + 3 * 256 < nvec; i0 += 4 * 256) {
+        uint4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = ((const uint4*)lr)[i0 + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float v[8];
+            unpack8(q[u], v);
+            float vm = v[0];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) vm = fmaxf(vm, v[k]);
+            float vs = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) vs += __expf(v[k] - vm);
+            online_merge(m, s, vm, vs);
+        }
+    }
+    for (int i = i0; i < nvec; i += 256) {
         float v[8];
         unpack8(((const uint4*)lr)[i], v);
         float vm = v[0];
@@ -153,7 +173,27 @@ __global__ __launch_bounds__(256) void xent_fused_kernel(bf16_t* __restrict__ lo
     const float lse = bcast[0];
     const float sc = ign ? 0.f : scale_ptr[0];
     const int nv = ld / 8;
-    for (int i = threadIdx.x; i < nv; i += 256) {
+    auto dl8 = [&](const uint4& q, int i) -> uint4 {
+        float v[8];
+        unpack8(q, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = i * 8 + k;
+            float p = j < V ? __expf(v[k] - lse) : 0.f;
+            if (j == lab) p -= 1.f;
+            v[k] = p * sc;
+        }
+        return pack8(v);
+    };
+    int i1 = threadIdx.x;
+    for (; i1 + 3 * 256 < nv; i1 += 4 * 256) {
+        uint4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = ((const uint4*)lr)[i1 + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ((uint4*)lr)[i1 + u * 256] = dl8(q[u], i1 + u * 256);
+    }
+    for (int i = i1; i < nv; i += 256) {
         float v[8];
         unpack8(((const uint4*)lr)[i], v);
 #pragma unroll
