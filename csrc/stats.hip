@@ -1130,14 +1130,7 @@ __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __r
     // position weight (i % 1021) + 1, carried incrementally: one 64-bit modulo per thread, then
     // +2048 elements per iteration = +6 (mod 1021) — a per-element int64 modulo was the cost
     int r = (int)((beg + threadIdx.x * 8) % 1021);
-    for (int64_t i = beg + threadIdx.x * 8; i < end; i += 256 * 8) {
-        float f[8];
-        if (i + 8 <= end) {
-            unpack8(*(const uint4*)(x + i), f);
-        } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = i + e < end ? bf2f(x[i + e]) : 0.f;
-        }
+    auto acc8 = [&](const float (&f)[8]) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             const double v = (double)f[e];
@@ -1148,6 +1141,30 @@ __global__ __launch_bounds__(256) void checksum_partial_kernel(const bf16_t* __r
         }
         r += 2048 - 2 * 1021;
         if (r >= 1021) r -= 1021;
+    };
+    int64_t i = beg + threadIdx.x * 8;
+    // four 16-B loads in flight per lane per trip (one at a time left the pass latency-bound); the
+    // vectors are then summed in the same per-lane order as before: bit-identical results
+    for (; i + 3 * 2048 + 8 <= end; i += 4 * 2048) {
+        uint4 qv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) qv[u] = *(const uint4*)(x + i + u * 2048);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float f[8];
+            unpack8(qv[u], f);
+            acc8(f);
+        }
+    }
+    for (; i < end; i += 256 * 8) {
+        float f[8];
+        if (i + 8 <= end) {
+            unpack8(*(const uint4*)(x + i), f);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = i + e < end ? bf2f(x[i + e]) : 0.f;
+        }
+        acc8(f);
     }
     s = wave_sum_d(s);
     q = wave_sum_d(q);
