@@ -73,6 +73,16 @@ struct GemmParams {
     int splits;
     int group_m;          // tile order: 0 = row-major over (tm, tn); G > 0 = groups of G tile rows, tn-major
     unsigned long long* ts;  // diagnostics (tdl_gemm_set_timestamps): per-workgroup s_memrealtime stamps
+    // gemm_pd GROUPED (weight gradients): a second product sharing M, K and the split, its items
+    // numbered after the first product's items1 = tiles x splits
+    struct Second {
+        const bf16_t* A;
+        const bf16_t* B;
+        void* C;
+        int N, lda, ldb, ldc, tiles_n, tiles;
+        long long split_stride;
+    } g2;
+    int items1;
 };
 
 // timestamp slot `k` of this workgroup (wave 0, lane 0; 64 slots per workgroup)
@@ -1293,7 +1303,7 @@ constexpr int copies_before(int ds, int dp, int wg) {
 // head of half 0, then lgkmcnt(0) + barrier; copy i at slot DS + DP i; the vmcnt wait + barrier at
 // slot WG; F0 reads after it.
 template <int EPI, int RP = 1, int DS = 20, int DP = 7, int WG = 100, bool X4 = false, int ORD = 0, int B1 = 16 * RP + 2,
-          bool TA = false, bool TB = false, bool NOEPI = false, bool NOBIAS = false>
+          bool TA = false, bool TB = false, bool NOEPI = false, bool NOBIAS = false, bool GROUPED = false>
 __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     static_assert(B1 >= 16 * RP + 2 && DS > B1 && DS + 15 * DP <= 127 && WG + 16 <= 127, "schedule must fit one K step");
     constexpr int NB = copies_before(DS, DP, WG);          // this step's copies in flight at the wait
@@ -1311,12 +1321,31 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
     const int G = gridDim.x;
     const int lb = xcd_remap(blockIdx.x, G);
     const int nk = p.k_per_split / BK;
-    const int n_items = p.tiles * p.splits;
-    const int n_mine = lb < n_items ? (n_items - 1 - lb) / G + 1 : 0;
+    // GROUPED: one item per workgroup (host: items <= CUs), so a workgroup's product is fixed: the
+    // ones past the first product's items switch every operand / output field to the second product
+    // once, here, and the rest of the kernel is the plain one
+    int ioff = 0;
+    const int n_items = GROUPED ? p.items1 + p.g2.tiles * p.splits : p.tiles * p.splits;
+    if constexpr (GROUPED) {
+        if (lb >= p.items1) {
+            p.A = p.g2.A;
+            p.B = p.g2.B;
+            p.C = p.g2.C;
+            p.N = p.g2.N;
+            p.lda = p.g2.lda;
+            p.ldb = p.g2.ldb;
+            p.ldc = p.g2.ldc;
+            p.tiles_n = p.g2.tiles_n;
+            p.tiles = p.g2.tiles;
+            p.split_stride = p.g2.split_stride;
+            ioff = p.items1;
+        }
+    }
+    const int n_mine = lb < n_items ? (GROUPED ? 1 : (n_items - 1 - lb) / G + 1) : 0;
     const int total = n_mine * nk;
     if (total == 0) return;
     auto coords = [&](int i, int& m0, int& n0, int& sp) {
-        const int item = lb + i * G;
+        const int item = lb + i * G - ioff;
         sp = item / p.tiles;
         const int tile = item - sp * p.tiles;
         int tm, tn;
@@ -1678,4 +1707,37 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
 #undef PP_LAUNCH
     TDL_LAUNCH_CHECK();
 #endif
+}
+
+// Two weight gradients in ONE launch (gemm_pd, both operands row-contiguous, fp32 split-K slabs):
+// C1[s] = A1^T B1 over slice s, C2[s] = A2^T B2, sharing M (the weights' input width) and K (the
+// tokens).  The qkv (48 tiles) and out-projection (16 tiles) weight gradients of a GPT-2-medium
+// block fill the 256 CUs in one round at split 4 together, where apart they need split 16 (three
+// rounds of 16 fp32 slabs for qkv) to do so.  A stored [K][lda], B [K][ldb]; slabs [split][M][N].
+TDL_API int tdl_gemm_wgrad_grouped(const void* A1, const void* B1, float* C1, int N1, int lda1, int ldb1, const void* A2,
+                                   const void* B2, float* C2, int N2, int lda2, int ldb2, int M, int K, int split,
+                                   hipStream_t s) {
+    if (M <= 0 || N1 <= 0 || N2 <= 0 || K <= 0 || split < 1 || K % (BK * split) || K / BK / split < 2) return (int)hipErrorInvalidValue;
+    if (M % 8 || N1 % 8 || N2 % 8 || lda1 % 8 || ldb1 % 8 || lda2 % 8 || ldb2 % 8) return (int)hipErrorInvalidValue;
+    GemmParams p{(const bf16_t*)A1, (const bf16_t*)B1, C1, nullptr, nullptr, nullptr, M, N1, K, lda1, ldb1, N1,
+                 K / split, (long long)M * N1, (N1 + BN - 1) / BN, 0, split, 0, g_gemm_ts};
+    const char* g = std::getenv("TDL_GEMM_GROUPM");
+    p.group_m = g ? std::atoi(g) : 8;
+    p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
+    p.g2.A = (const bf16_t*)A2;
+    p.g2.B = (const bf16_t*)B2;
+    p.g2.C = C2;
+    p.g2.N = N2;
+    p.g2.lda = lda2;
+    p.g2.ldb = ldb2;
+    p.g2.ldc = N2;
+    p.g2.tiles_n = (N2 + BN - 1) / BN;
+    p.g2.tiles = ((M + BM - 1) / BM) * p.g2.tiles_n;
+    p.g2.split_stride = (long long)M * N2;
+    p.items1 = p.tiles * split;
+    const int items = p.items1 + p.g2.tiles * split;
+    if (items > num_cus()) return (int)hipErrorInvalidValue;   // one item per workgroup (the caller splits less)
+    const int grid = items;
+    gemm_pd<EPI_F32, 1, 20, 7, 100, false, 0, 18, true, true, false, false, true><<<grid, PNTHR, 0, s>>>(p);
+    TDL_LAUNCH_CHECK();
 }

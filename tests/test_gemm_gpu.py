@@ -206,3 +206,39 @@ def test_production_fused_mlp():
     y0 = y.float()
     gemm.matmul(f, wp, out=y, epi="resadd")
     assert _rel(y, y0 + f.float() @ wp.float()) < 1e-2
+
+
+@pytest.mark.parametrize("Mt,K,N1,N2", [(65536, 1024, 3072, 1024), (16384, 1024, 3072, 1024), (4096, 264, 520, 136)])
+def test_wgrad_grouped_pair(Mt, K, N1, N2):
+    """qkv + o weight gradients from ONE grouped launch (tdl_gemm_wgrad_grouped: one output tile x
+    slice per workgroup, product chosen per workgroup) vs fp32, ragged tiles included; deterministic;
+    a pair whose items do not fit one round on the CUs is declined (caller runs them separately)."""
+    from trustworthy_dl.ops import gemm
+    x1, x2 = _rand(Mt, K), _rand(Mt, K)
+    d1, d2 = _rand(Mt, N1, scale=0.1), _rand(Mt, N2, scale=0.1)
+    acc1, acc2 = torch.randn(K, N1, device=DEV), torch.randn(K, N2, device=DEV)
+    ref1 = acc1 + x1.float().t() @ d1.float()
+    ref2 = acc2 + x2.float().t() @ d2.float()
+    assert gemm.matmul_f32_acc_grouped(acc1, x1.t(), d1, acc2, x2.t(), d2)
+    assert float((acc1 - ref1).norm() / ref1.norm()) < 1e-4
+    assert float((acc2 - ref2).norm() / ref2.norm()) < 1e-4
+    r = []
+    for _ in range(2):
+        a1, a2 = torch.zeros(K, N1, device=DEV), torch.zeros(K, N2, device=DEV)
+        assert gemm.matmul_f32_acc_grouped(a1, x1.t(), d1, a2, x2.t(), d2)
+        r.append((a1, a2))
+    assert torch.equal(r[0][0], r[1][0]) and torch.equal(r[0][1], r[1][1])
+    # the slabs path of the separate launches gives the same sums up to fp32 reassociation
+    s1 = torch.zeros(K, N1, device=DEV)
+    gemm.matmul_f32_acc(s1, x1.t(), d1, kernel="pd")
+    assert float((s1 - r[0][0]).norm() / s1.norm()) < 1e-5
+
+
+def test_wgrad_grouped_declines_oversized():
+    from trustworthy_dl.ops import gemm
+    Mt, K = 1024, 8192                                   # 32 x 16 tiles: more than one round
+    x = _rand(Mt, K)
+    d = _rand(Mt, 4096)
+    acc = torch.zeros(K, 4096, device=DEV)
+    assert not gemm.matmul_f32_acc_grouped(acc, x.t(), d, acc.clone(), x.t(), d)
+    assert float(acc.abs().max()) == 0.0

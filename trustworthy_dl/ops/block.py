@@ -38,9 +38,15 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import ptr, stream_ptr
 from .layers import (_f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, bump_weight_generation,  # noqa: F401
-                     fwd_weight, run_or_defer, take_stats_sink, wgrad_acc)
+                     fwd_weight, run_or_defer, take_stats_sink, wgrad_acc, wgrad_acc_pair)
 
 _FUSED_WIDTHS = (256, 512, 768, 1024, 1280, 1536, 2048)
+
+
+def gemm_grouped_wgrad() -> bool:
+    """qkv + o weight gradients as one grouped launch (gemm.matmul_f32_acc_grouped) enabled"""
+    from . import gemm
+    return gemm.WGRAD_GROUPED and gemm.WGRAD_KERNEL == "pd"
 
 
 def fused_block_enabled(width: int, device: torch.device) -> bool:
@@ -246,7 +252,11 @@ class _GPT2BlockFn(torch.autograd.Function):
         dy1 = _ln_bwd(dh2, y1, ln2_w, mean2, rstd2, g_ln2w, g_ln2b, dres=dy2, sres_acc=g_bp, sdx_acc=g_bo)
         del dh2
         # attention branch
-        wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1, sink=sk[id(g_wo)]))
+        # the o weight gradient goes with the qkv one (one grouped launch, wgrad_acc_pair) when both
+        # qualify for it
+        pair_o = dy1.is_cuda and gemm_grouped_wgrad()
+        if not pair_o:
+            wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1, sink=sk[id(g_wo)]))
         do = _mm(dy1, w_o.t())
         # the qkv bias gradient (column sums of dqkv) comes out of the attention backward kernels
         dqkv = attn_bwd(qkv.view(B, T, 3 * C), o2.view(B, T, C), lse, do.view(B, T, C), H, True, scale,
@@ -255,7 +265,10 @@ class _GPT2BlockFn(torch.autograd.Function):
         dqkv2 = dqkv.view(B * T, 3 * C)
 
         def _qkv_grads(dqkv2=dqkv2):
-            wgrad_acc(g_wqkv, h1.t(), dqkv2, sink=sk[id(g_wqkv)])
+            if pair_o:
+                wgrad_acc_pair(g_wqkv, h1.t(), dqkv2, g_wo, o2.t(), dy1, sink1=sk[id(g_wqkv)], sink2=sk[id(g_wo)])
+            else:
+                wgrad_acc(g_wqkv, h1.t(), dqkv2, sink=sk[id(g_wqkv)])
         wdefer(_qkv_grads)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -260,6 +260,18 @@ def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, sink=None):
     acc.add_(torch.mm(a, b, out_dtype=torch.float32).view(acc.shape))
 
 
+def wgrad_acc_pair(acc1: torch.Tensor, a1: torch.Tensor, b1: torch.Tensor, acc2: torch.Tensor, a2: torch.Tensor,
+                   b2: torch.Tensor, sink1=None, sink2=None):
+    """Two weight gradients sharing M (input width) and K (tokens) — the attention's qkv and o —
+    from one grouped launch when they qualify (gemm.matmul_f32_acc_grouped), else one by one."""
+    if a1.is_cuda:
+        from . import gemm
+        if gemm.matmul_f32_acc_grouped(acc1, a1, b1, acc2, a2, b2, sink1, sink2):
+            return
+    wgrad_acc(acc1, a1, b1, sink=sink1)
+    wgrad_acc(acc2, a2, b2, sink=sink2)
+
+
 def _wgrad_into(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
     """param grad += a @ b, accumulating in fp32 into ``main_grad`` when present."""
     mg = getattr(param, "main_grad", None)
