@@ -73,13 +73,13 @@ struct GemmParams {
     int splits;
     int group_m;          // tile order: 0 = row-major over (tm, tn); G > 0 = groups of G tile rows, tn-major
     unsigned long long* ts;  // diagnostics (tdl_gemm_set_timestamps): per-workgroup s_memrealtime stamps
-    // gemm_pd GROUPED (weight gradients): a second product sharing M, K and the split, its items
+    // gemm_pd GROUPED (weight gradients): a second product sharing K and the split, its items
     // numbered after the first product's items1 = tiles x splits
     struct Second {
         const bf16_t* A;
         const bf16_t* B;
         void* C;
-        int N, lda, ldb, ldc, tiles_n, tiles;
+        int M, N, lda, ldb, ldc, tiles_n, tiles;
         long long split_stride;
     } g2;
     int items1;
@@ -1331,6 +1331,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
             p.A = p.g2.A;
             p.B = p.g2.B;
             p.C = p.g2.C;
+            p.M = p.g2.M;
             p.N = p.g2.N;
             p.lda = p.g2.lda;
             p.ldb = p.g2.ldb;
@@ -1714,26 +1715,28 @@ TDL_API int tdl_gemm(const void* A, const void* B, void* C, const void* bias, vo
 // tokens).  The qkv (48 tiles) and out-projection (16 tiles) weight gradients of a GPT-2-medium
 // block fill the 256 CUs in one round at split 4 together, where apart they need split 16 (three
 // rounds of 16 fp32 slabs for qkv) to do so.  A stored [K][lda], B [K][ldb]; slabs [split][M][N].
-TDL_API int tdl_gemm_wgrad_grouped(const void* A1, const void* B1, float* C1, int N1, int lda1, int ldb1, const void* A2,
-                                   const void* B2, float* C2, int N2, int lda2, int ldb2, int M, int K, int split,
-                                   hipStream_t s) {
-    if (M <= 0 || N1 <= 0 || N2 <= 0 || K <= 0 || split < 1 || K % (BK * split) || K / BK / split < 2) return (int)hipErrorInvalidValue;
-    if (M % 8 || N1 % 8 || N2 % 8 || lda1 % 8 || ldb1 % 8 || lda2 % 8 || ldb2 % 8) return (int)hipErrorInvalidValue;
-    GemmParams p{(const bf16_t*)A1, (const bf16_t*)B1, C1, nullptr, nullptr, nullptr, M, N1, K, lda1, ldb1, N1,
-                 K / split, (long long)M * N1, (N1 + BN - 1) / BN, 0, split, 0, g_gemm_ts};
+TDL_API int tdl_gemm_wgrad_grouped(const void* A1, const void* B1, float* C1, int M1, int N1, int lda1, int ldb1,
+                                   const void* A2, const void* B2, float* C2, int M2, int N2, int lda2, int ldb2, int K,
+                                   int split, hipStream_t s) {
+    if (M1 <= 0 || M2 <= 0 || N1 <= 0 || N2 <= 0 || K <= 0 || split < 1 || K % (BK * split) || K / BK / split < 2)
+        return (int)hipErrorInvalidValue;
+    if (M1 % 8 || M2 % 8 || N1 % 8 || N2 % 8 || lda1 % 8 || ldb1 % 8 || lda2 % 8 || ldb2 % 8) return (int)hipErrorInvalidValue;
+    GemmParams p{(const bf16_t*)A1, (const bf16_t*)B1, C1, nullptr, nullptr, nullptr, M1, N1, K, lda1, ldb1, N1,
+                 K / split, (long long)M1 * N1, (N1 + BN - 1) / BN, 0, split, 0, g_gemm_ts};
     const char* g = std::getenv("TDL_GEMM_GROUPM");
     p.group_m = g ? std::atoi(g) : 8;
-    p.tiles = ((M + BM - 1) / BM) * p.tiles_n;
+    p.tiles = ((M1 + BM - 1) / BM) * p.tiles_n;
     p.g2.A = (const bf16_t*)A2;
     p.g2.B = (const bf16_t*)B2;
     p.g2.C = C2;
+    p.g2.M = M2;
     p.g2.N = N2;
     p.g2.lda = lda2;
     p.g2.ldb = ldb2;
     p.g2.ldc = N2;
     p.g2.tiles_n = (N2 + BN - 1) / BN;
-    p.g2.tiles = ((M + BM - 1) / BM) * p.g2.tiles_n;
-    p.g2.split_stride = (long long)M * N2;
+    p.g2.tiles = ((M2 + BM - 1) / BM) * p.g2.tiles_n;
+    p.g2.split_stride = (long long)M2 * N2;
     p.items1 = p.tiles * split;
     const int items = p.items1 + p.g2.tiles * split;
     if (items > num_cus()) return (int)hipErrorInvalidValue;   // one item per workgroup (the caller splits less)

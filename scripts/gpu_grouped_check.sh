@@ -9,4 +9,4 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   && timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
      tests/test_engine_gpu.py tests/test_fwd_weight_gpu.py > gpurun_out/grouped_engine_tests.log 2>&1 \
   && tail -3 gpurun_out/grouped_engine_tests.log \
-  && VARIANTS="sep=TDL_WGRAD_GROUPED=0;grp=TDL_WGRAD_GROUPED=1" bash scripts/gpu_bench_env_ab.sh
+  && VARIANTS="${VARIANTS:-sep=TDL_WGRAD_GROUPED=0;grp=TDL_WGRAD_GROUPED=1}" bash scripts/gpu_bench_env_ab.sh

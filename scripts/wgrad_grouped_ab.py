@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""qkv + o weight gradients at the bench shape (GPT-2-medium, 64k / 16k tokens): the two separate
+"""qkv + o and fc + proj weight gradients at the bench shape (GPT-2-medium, 64k / 16k tokens): the two separate
 launches (each its own split from the cost model, slabs reduced) vs ONE grouped launch
 (gemm.matmul_f32_acc_grouped), interleaved rounds, median us.  One JSON line per (tokens, variant).
 
@@ -37,14 +37,15 @@ def main():
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     f = open(a.out, "a")
     C = 1024
-    for K in (int(t) for t in a.tokens.split(",")):
+    pairs = {"attn": ((C, 3 * C), (C, C)), "mlp": ((C, 4 * C), (4 * C, C))}
+    for K, (pair, ((m1, n1), (m2, n2))) in ((int(t), pp) for t in a.tokens.split(",") for pp in pairs.items()):
         torch.manual_seed(0)
-        h = (torch.rand(K, C, device="cuda") * 2 - 1).bfloat16()
-        o = (torch.rand(K, C, device="cuda") * 2 - 1).bfloat16()
-        dqkv = ((torch.rand(K, 3 * C, device="cuda") * 2 - 1) * 0.05).bfloat16()
-        dy = ((torch.rand(K, C, device="cuda") * 2 - 1) * 0.05).bfloat16()
-        g1 = torch.zeros(C, 3 * C, device="cuda")
-        g2 = torch.zeros(C, C, device="cuda")
+        h = (torch.rand(K, m1, device="cuda") * 2 - 1).bfloat16()
+        o = (torch.rand(K, m2, device="cuda") * 2 - 1).bfloat16()
+        dqkv = ((torch.rand(K, n1, device="cuda") * 2 - 1) * 0.05).bfloat16()
+        dy = ((torch.rand(K, n2, device="cuda") * 2 - 1) * 0.05).bfloat16()
+        g1 = torch.zeros(m1, n1, device="cuda")
+        g2 = torch.zeros(m2, n2, device="cuda")
 
         def separate():
             gemm.matmul_f32_acc(g1, h.t(), dqkv)
@@ -60,13 +61,13 @@ def main():
         for _ in range(a.rounds):
             for k, fn in variants.items():
                 times[k].append(timed(fn, a.iters))
-        flop = 2.0 * K * C * 4 * C
+        flop = 2.0 * K * (m1 * n1 + m2 * n2)
         for k, ts in times.items():
             us = statistics.median(ts)
-            rec = {"tokens": K, "variant": k, "us": round(us, 1), "tflops": round(flop / us / 1e6, 1),
+            rec = {"tokens": K, "pair": pair, "variant": k, "us": round(us, 1), "tflops": round(flop / us / 1e6, 1),
                    "spread_us": round(max(ts) - min(ts), 1),
-                   "split_separate": [gemm.wgrad_split(K, C, 3 * C), gemm.wgrad_split(K, C, C)],
-                   "split_grouped": gemm.grouped_split(K, C, 3 * C, C)}
+                   "split_separate": [gemm.wgrad_split(K, m1, n1), gemm.wgrad_split(K, m2, n2)],
+                   "split_grouped": gemm.grouped_split(K, m1, n1, m2, n2)}
             print(json.dumps(rec), flush=True)
             f.write(json.dumps(rec) + "\n")
         del h, o, dqkv, dy, g1, g2

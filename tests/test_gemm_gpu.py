@@ -208,15 +208,17 @@ def test_production_fused_mlp():
     assert _rel(y, y0 + f.float() @ wp.float()) < 1e-2
 
 
-@pytest.mark.parametrize("Mt,K,N1,N2", [(65536, 1024, 3072, 1024), (16384, 1024, 3072, 1024), (4096, 264, 520, 136)])
-def test_wgrad_grouped_pair(Mt, K, N1, N2):
-    """qkv + o weight gradients from ONE grouped launch (tdl_gemm_wgrad_grouped: one output tile x
-    slice per workgroup, product chosen per workgroup) vs fp32, ragged tiles included; deterministic;
-    a pair whose items do not fit one round on the CUs is declined (caller runs them separately)."""
+@pytest.mark.parametrize("Mt,K,N1,K2,N2", [(65536, 1024, 3072, 1024, 1024), (16384, 1024, 3072, 1024, 1024),
+                                            (65536, 1024, 4096, 4096, 1024), (4096, 264, 520, 136, 200)])
+def test_wgrad_grouped_pair(Mt, K, N1, K2, N2):
+    """qkv + o (and fc + proj: different input widths) weight gradients from ONE grouped launch
+    (tdl_gemm_wgrad_grouped: one output tile x slice per workgroup, product chosen per workgroup) vs
+    fp32, ragged tiles included; deterministic; a pair whose items do not fit one round on the CUs
+    is declined (caller runs them separately)."""
     from trustworthy_dl.ops import gemm
-    x1, x2 = _rand(Mt, K), _rand(Mt, K)
+    x1, x2 = _rand(Mt, K), _rand(Mt, K2)
     d1, d2 = _rand(Mt, N1, scale=0.1), _rand(Mt, N2, scale=0.1)
-    acc1, acc2 = torch.randn(K, N1, device=DEV), torch.randn(K, N2, device=DEV)
+    acc1, acc2 = torch.randn(K, N1, device=DEV), torch.randn(K2, N2, device=DEV)
     ref1 = acc1 + x1.float().t() @ d1.float()
     ref2 = acc2 + x2.float().t() @ d2.float()
     assert gemm.matmul_f32_acc_grouped(acc1, x1.t(), d1, acc2, x2.t(), d2)
@@ -224,7 +226,7 @@ def test_wgrad_grouped_pair(Mt, K, N1, N2):
     assert float((acc2 - ref2).norm() / ref2.norm()) < 1e-4
     r = []
     for _ in range(2):
-        a1, a2 = torch.zeros(K, N1, device=DEV), torch.zeros(K, N2, device=DEV)
+        a1, a2 = torch.zeros(K, N1, device=DEV), torch.zeros(K2, N2, device=DEV)
         assert gemm.matmul_f32_acc_grouped(a1, x1.t(), d1, a2, x2.t(), d2)
         r.append((a1, a2))
     assert torch.equal(r[0][0], r[1][0]) and torch.equal(r[0][1], r[1][1])

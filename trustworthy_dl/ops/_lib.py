@@ -154,7 +154,7 @@ _SIGNATURES = {
     "tdl_attn_bwd": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P],
     # gemm.hip
     "tdl_gemm": [_P] * 6 + [_I] * 10 + [_L, _P],
-    "tdl_gemm_wgrad_grouped": [_P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "tdl_gemm_wgrad_grouped": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "tdl_gemm_set_timestamps": [_P],
     # audit.hip
     "tdl_b2s_nodes": [_P, _L, _L, _I, _I, _I, _I, _P, _L, _P],

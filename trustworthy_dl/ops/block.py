@@ -43,9 +43,12 @@ from .layers import (_f32_acc, _scratch, _wants_main_grad, attn_bwd, attn_fwd, b
 _FUSED_WIDTHS = (256, 512, 768, 1024, 1280, 1536, 2048)
 
 
-def gemm_grouped_wgrad() -> bool:
-    """qkv + o weight gradients as one grouped launch (gemm.matmul_f32_acc_grouped) enabled"""
+def gemm_grouped_wgrad(branch: str) -> bool:
+    """the branch's two weight gradients (attn: qkv + o, mlp: fc + proj) as one grouped launch
+    (gemm.matmul_f32_acc_grouped); TDL_WGRAD_GROUPED_MLP=0 keeps the MLP pair separate"""
     from . import gemm
+    if branch == "mlp" and os.environ.get("TDL_WGRAD_GROUPED_MLP", "1") == "0":
+        return False
     return gemm.WGRAD_GROUPED and gemm.WGRAD_KERNEL == "pd"
 
 
@@ -234,7 +237,10 @@ class _GPT2BlockFn(torch.autograd.Function):
         wdefer = run_or_defer if all(_wants_main_grad(p) for p in (w_qkv, b_qkv, w_o, w_fc, w_p)) else (lambda fn: fn())
         # MLP branch
         sk = {id(g): take_stats_sink(g) for g in (g_wp, g_wfc, g_wo, g_wqkv)}   # verifier's fused reduces
-        wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2, sink=sk[id(g_wp)]))
+        # the proj weight gradient goes with the fc one (one grouped launch) when both qualify
+        pair_p = dy2.is_cuda and gemm_grouped_wgrad("mlp")
+        if not pair_p:
+            wdefer(lambda: wgrad_acc(g_wp, f.t(), dy2, sink=sk[id(g_wp)]))
         if ctx.fused_mlp and _native_mlp(dy2, w_p.t(), b_fc):
             from . import gemm   # dpre = (dy @ Wp^T) * gelu'(pre), bfc grad as column sums
             dpre = gemm.matmul(dy2, w_p.t(), epi="dgelu", aux=pre, colsum=g_bfc)
@@ -245,7 +251,11 @@ class _GPT2BlockFn(torch.autograd.Function):
             else:
                 dpre = _bias_gelu_bwd(df, pre, b_fc, g_bfc)
             del df
-        wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre, sink=sk[id(g_wfc)]))
+        if pair_p:
+            wdefer(lambda dpre=dpre: wgrad_acc_pair(g_wfc, h2.t(), dpre, g_wp, f.t(), dy2, sink1=sk[id(g_wfc)],
+                                                    sink2=sk[id(g_wp)]))
+        else:
+            wdefer(lambda dpre=dpre: wgrad_acc(g_wfc, h2.t(), dpre, sink=sk[id(g_wfc)]))
         dh2 = _mm(dpre, w_fc.t())
         del dpre
         # dy1 = dy + LN2_bwd(dh2); bp grad = colsum(dy), bo grad = colsum(dy1) from the same pass
@@ -254,7 +264,7 @@ class _GPT2BlockFn(torch.autograd.Function):
         # attention branch
         # the o weight gradient goes with the qkv one (one grouped launch, wgrad_acc_pair) when both
         # qualify for it
-        pair_o = dy1.is_cuda and gemm_grouped_wgrad()
+        pair_o = dy1.is_cuda and gemm_grouped_wgrad("attn")
         if not pair_o:
             wdefer(lambda: wgrad_acc(g_wo, o2.t(), dy1, sink=sk[id(g_wo)]))
         do = _mm(dy1, w_o.t())

@@ -175,23 +175,23 @@ def matmul_f32_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, split: O
     return acc
 
 
-# two weight gradients with the same input width and token count (the attention's qkv and o
-# products) in ONE launch of the LDS-DMA kernel, one output tile x slice per workgroup: the two
+# two weight gradients with the same token count (the attention's qkv and o products; the MLP's fc
+# and proj) in ONE launch of the LDS-DMA kernel, one output tile x slice per workgroup: the two
 # launches' partial last rounds become one full round
 WGRAD_GROUPED = os.environ.get("TDL_WGRAD_GROUPED", "1") != "0"
 
 
-def grouped_split(K: int, M: int, N1: int, N2: int, num_cu: Optional[int] = None) -> int:
+def grouped_split(K: int, M1: int, N1: int, M2: int, N2: int, num_cu: Optional[int] = None) -> int:
     """Split for the grouped pair (csrc/gemm.hip tdl_gemm_wgrad_grouped): the wgrad_split cost model
     over the pair's tiles, restricted to splits >= 2 whose work items fit ONE round on the CUs (the
     kernel runs one item per workgroup); 0 when none does."""
     cu = num_cu or num_cus()
-    tiles = ((M + 255) // 256) * ((N1 + 255) // 256 + (N2 + 255) // 256)
+    tiles = ((M1 + 255) // 256) * ((N1 + 255) // 256) + ((M2 + 255) // 256) * ((N2 + 255) // 256)
     best, best_t = 0, float("inf")
     for s in (2, 4, 8, 16):
         if effective_split(K, s) != s or tiles * s > cu:
             continue
-        t = (K // s // BK) * 1.5 + 5.0 + s * M * (N1 + N2) * 8 / 5e6
+        t = (K // s // BK) * 1.5 + 5.0 + s * (M1 * N1 + M2 * N2) * 8 / 5e6
         if t < best_t - 1e-9:
             best, best_t = s, t
     return best
@@ -200,17 +200,18 @@ def grouped_split(K: int, M: int, N1: int, N2: int, num_cu: Optional[int] = None
 def matmul_f32_acc_grouped(acc1: torch.Tensor, a1: torch.Tensor, b1: torch.Tensor, acc2: torch.Tensor,
                            a2: torch.Tensor, b2: torch.Tensor, sink1=None, sink2=None) -> bool:
     """``acc1 += a1 @ b1`` and ``acc2 += a2 @ b2`` (fp32, weight-gradient layout: both operands
-    row-contiguous, same M and K) from one grouped launch, each product's slabs reduced by its own
+    row-contiguous, same K) from one grouped launch, each product's slabs reduced by its own
     pass (or taken by its sink).  Returns False, having done nothing, when the pair does not qualify
     (the caller runs the two products separately)."""
     if not WGRAD_GROUPED or WGRAD_KERNEL != "pd":
         return False
-    M, K = a1.shape
+    M1, K = a1.shape
+    M2 = a2.shape[0]
     N1, N2 = b1.shape[1], b2.shape[1]
-    if tuple(a2.shape) != (M, K) or b2.shape[0] != K or b1.shape[0] != K:
+    if a2.shape[1] != K or b2.shape[0] != K or b1.shape[0] != K:
         return False
-    for acc, n in ((acc1, N1), (acc2, N2)):
-        if acc.dtype != torch.float32 or tuple(acc.shape) != (M, n) or not acc.is_contiguous():
+    for acc, m, n in ((acc1, M1, N1), (acc2, M2, N2)):
+        if acc.dtype != torch.float32 or tuple(acc.shape) != (m, n) or not acc.is_contiguous():
             return False
     if not (supported(a1, b1) and supported(a2, b2)):
         return False
@@ -218,15 +219,15 @@ def matmul_f32_acc_grouped(acc1: torch.Tensor, a1: torch.Tensor, b1: torch.Tenso
     (ta2, lda2), (tb2, ldb2) = _operand_a(a2), _operand_b(b2)
     if not (ta1 and tb1 and ta2 and tb2):
         return False
-    S = grouped_split(K, M, N1, N2)
+    S = grouped_split(K, M1, N1, M2, N2)
     if S < 2:
         return False
-    slabs = torch.empty(S * M * (N1 + N2), dtype=torch.float32, device=acc1.device)
-    s1 = slabs[:S * M * N1].view(S, M, N1)
-    s2 = slabs[S * M * N1:].view(S, M, N2)
+    slabs = torch.empty(S * (M1 * N1 + M2 * N2), dtype=torch.float32, device=acc1.device)
+    s1 = slabs[:S * M1 * N1].view(S, M1, N1)
+    s2 = slabs[S * M1 * N1:].view(S, M2, N2)
     st = stream_ptr(acc1.device)
-    _lib.call("tdl_gemm_wgrad_grouped", ptr(a1), ptr(b1), ptr(s1), N1, lda1, ldb1, ptr(a2), ptr(b2), ptr(s2),
-              N2, lda2, ldb2, M, K, S, st)
+    _lib.call("tdl_gemm_wgrad_grouped", ptr(a1), ptr(b1), ptr(s1), M1, N1, lda1, ldb1, ptr(a2), ptr(b2), ptr(s2),
+              M2, N2, lda2, ldb2, K, S, st)
     for acc, sl, sink in ((acc1, s1, sink1), (acc2, s2, sink2)):
         if sink is not None and sink(sl, S):
             continue

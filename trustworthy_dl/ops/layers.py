@@ -262,7 +262,7 @@ def wgrad_acc(acc: torch.Tensor, a: torch.Tensor, b: torch.Tensor, sink=None):
 
 def wgrad_acc_pair(acc1: torch.Tensor, a1: torch.Tensor, b1: torch.Tensor, acc2: torch.Tensor, a2: torch.Tensor,
                    b2: torch.Tensor, sink1=None, sink2=None):
-    """Two weight gradients sharing M (input width) and K (tokens) — the attention's qkv and o —
+    """Two weight gradients sharing K (tokens) — the attention's qkv and o, the MLP's fc and proj —
     from one grouped launch when they qualify (gemm.matmul_f32_acc_grouped), else one by one."""
     if a1.is_cuda:
         from . import gemm
