@@ -16,6 +16,15 @@ x = ((torch.rand(T, C, device="cuda") * 2 - 1)).bfloat16()
 dy = ((torch.rand(T, N, device="cuda") * 2 - 1) * 0.05).bfloat16()
 acc = torch.zeros(C, N, dtype=torch.float32, device="cuda")
 KN = os.environ.get("PMC_KERNEL", "p4")
+if KN == "grouped":    # the qkv + o pair from one grouped launch (gemm.matmul_f32_acc_grouped)
+    o = ((torch.rand(T, C, device="cuda") * 2 - 1)).bfloat16()
+    dy1 = ((torch.rand(T, C, device="cuda") * 2 - 1) * 0.05).bfloat16()
+    acc_o = torch.zeros(C, C, dtype=torch.float32, device="cuda")
+    N = N + C
+
+    def _grouped(acc, a_op, b_op, kernel=None):
+        assert gemm.matmul_f32_acc_grouped(acc, a_op, b_op, acc_o, o.t(), dy1)
+    gemm.matmul_f32_acc = _grouped
 if os.environ.get("PMC_NT", "0") == "1":
     a_op, b_op = x.t().contiguous(), dy.t().contiguous().t()
 else:
