@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--tokens", type=int, default=65536)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--groups", default="")
+    ap.add_argument("--splits", default="1,2,3,4,6,8")
+    ap.add_argument("--lib", type=int, default=1)
     ap.add_argument("--out", default="gpurun_out/r6_lm_wgrad_ab.jsonl")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
@@ -42,9 +45,16 @@ def main():
     x = (torch.rand(T, C, device="cuda") * 2 - 1).bfloat16()
     acc = torch.zeros(V, C, device="cuda")
     variants = {"pd_model": lambda: gemm.matmul_f32_acc(acc, dl.t(), x, kernel="pd")}
-    for s in (1, 2, 3, 4, 6, 8):
+    for s in (int(v) for v in a.splits.split(",") if v):
         variants[f"pd_s{s}"] = lambda s=s: gemm.matmul_f32_acc(acc, dl.t(), x, split=s, kernel="pd")
-    variants["lib_f32"] = lambda: acc.add_(torch.mm(dl.t(), x, out_dtype=torch.float32))
+    if a.lib:
+        variants["lib_f32"] = lambda: acc.add_(torch.mm(dl.t(), x, out_dtype=torch.float32))
+    for g in (v for v in a.groups.split(",") if v):   # tile orders (TDL_GEMM_GROUPM, read per launch) at the model's split
+        def run(g=g):
+            os.environ["TDL_GEMM_GROUPM"] = g
+            gemm.matmul_f32_acc(acc, dl.t(), x, kernel="pd")
+            os.environ.pop("TDL_GEMM_GROUPM", None)
+        variants[f"pd_g{g}"] = run
     times = {k: [] for k in variants}
     for fn in variants.values():
         fn()
