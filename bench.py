@@ -316,7 +316,11 @@ def run(args):
                        "flagged": sorted({(a["step"], a["node_id"], a["attack_type"]) for a in engine.attack_history})[:8],
                        "p2p_mode": engine.p2p_mode, "p2p_mode_requested": args.p2p_mode,
                        "native_gemm": "fc fwd+gelu (pd), proj dgrad+dgelu (pp), LM-head dX (pd), all weight gradients "
-                                      f"({gemm_mod.WGRAD_KERNEL})",
+                                      f"({gemm_mod.WGRAD_KERNEL}"
+                                      + (", qkv+o and fc+proj grouped" if gemm_mod.WGRAD_GROUPED and gemm_mod.WGRAD_KERNEL == "pd"
+                                         and os.environ.get("TDL_WGRAD_GROUPED_MLP", "1") != "0" else "")
+                                      + (", qkv+o grouped" if gemm_mod.WGRAD_GROUPED and gemm_mod.WGRAD_KERNEL == "pd"
+                                         and os.environ.get("TDL_WGRAD_GROUPED_MLP", "1") == "0" else "") + ")",
                        "native_wgrad": gemm_mod.WGRAD_KERNEL,
                        "hw_queues": hwq, "hw_queues_per_rank": hwq_all,
                        # per-rank RCCL communicators / HIP streams (compute + verification + one per
