@@ -1371,6 +1371,11 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         qb = sb.rsrc(p.B, p.ldb, pn0, p.N, k0);
     };
     auto produce_advance = [&]() {
+        if constexpr (GROUPED) {   // one item: the producer never moves to another tile
+            if (--pleft > 0) ++pt;
+            else pleft = 0;
+            return;
+        }
         if (--pleft > 0) {
             if (++pt == nk) {
                 pt = 0;
@@ -1494,7 +1499,7 @@ __global__ __launch_bounds__(PNTHR, 1) void gemm_pd(GemmParams p) {
         produce_advance();
         ++s;
     };
-    for (int ci = 0; ci < n_mine; ++ci) {
+    for (int ci = 0; ci < (GROUPED ? 1 : n_mine); ++ci) {
         int cm0, cn0, csp;
         coords(ci, cm0, cn0, csp);
         bias_n0 = cn0 + wn * 128;
